@@ -1,0 +1,215 @@
+#!/usr/bin/env python3
+"""Benchmark: scans/s of TSDF integration (128x1024 Ouster scans, 5 cm voxels) on N MI355X.
+
+A step integrates one batch of synthetic scans that are already resident in HBM (the C1/M1
+workload of SURVEY.md §8d: OS-1-128 1024x10 beams, analytic scene, circular trajectory at 10 Hz,
+5 cm voxels, 15 cm truncation, no carving), scan after scan, through libtsdf_hip.so's
+tsdf_integrate_batch_device.  Multi-GPU (one process per GPU, torch.distributed over RCCL): every
+rank integrates its azimuth sector of every scan of the step into its own partial field (weak
+scaling: a step of N GPUs holds N * batch scans, each rank's share is `batch` scans' worth of rays);
+no collective runs on the data path — the border-brick merge is a read-out operation, timed
+separately (readout_merge_ms).
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "noetic-slam_amd"))
+
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=32, help="scans per GPU per step")
+    ap.add_argument("--voxel", type=float, default=0.05)
+    ap.add_argument("--trunc", type=float, default=0.15)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0,
+                    help="budget of the CPU-oracle baseline sample (rank 0, N=1)")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-profile", action="store_true",
+                    help="do not record per-kernel HIP events in the timed region")
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_r01.json"),
+                    help="PMC-measured HBM bytes per launch (from a separate rocprofv3 --pmc run)")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and world > 1:
+        raise SystemExit("--gpus %d but WORLD_SIZE %d" % (args.gpus, world))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+
+    from tsdf_map import HipTSDFVolume
+    from tsdf_map.scan_gen import TorchOusterSim, sector_mask_torch
+
+    # ---- synthesize every scan of every step, this rank's sector, resident in HBM -------------
+    sim = TorchOusterSim(dev)
+    n_steps = args.warmup + args.steps
+    scans_per_step = world * args.batch
+    steps = []
+    t_gen = time.time()
+    for s in range(n_steps):
+        parts, offs, origins = [], [0], []
+        for j in range(scans_per_step):
+            k = s * scans_per_step + j
+            pts, org = sim.scan(k)
+            if world > 1:
+                pts = pts[sector_mask_torch(pts, org, rank, world)]
+            parts.append(pts)
+            offs.append(offs[-1] + pts.shape[0])
+            origins.append(org)
+        steps.append((torch.cat(parts).contiguous(), np.array(offs, np.uint64),
+                      np.stack(origins)))
+    torch.cuda.synchronize()
+    t_gen = time.time() - t_gen
+    max_pts = max(int(np.diff(o).max()) for _, o, _ in steps)
+
+    vol = HipTSDFVolume(args.voxel, args.trunc, max_points=max(max_pts, 1 << 17),
+                        max_bricks=1 << 20, device_id=local)
+
+    def run_step(i):
+        x, offs, org = steps[i]
+        vol.integrate_batch_device(x.data_ptr(), offs, org)
+
+    for i in range(args.warmup):
+        run_step(i)
+    vol.sync()
+    vol.reset_stats()
+    if not args.no_profile:
+        vol.set_profiling(True)
+
+    # ---- timed region ---------------------------------------------------------------------------
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.warmup, n_steps):
+        run_step(i)
+    torch.cuda.synchronize()
+    vol.sync()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    st = vol.stats()
+
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+    total_scans = args.steps * scans_per_step
+    value = total_scans / elapsed
+
+    # ---- roofline of the dominant kernel (per-launch means, this rank) -------------------------
+    n_launch = max(1, args.steps * scans_per_step)
+    rays_per_scan = st["n_rays_total"] / n_launch
+    uvox_per_scan = st["n_voxels_total"] / n_launch
+    bytes_per_scan = 12.0 * rays_per_scan + 16.0 * uvox_per_scan  # SURVEY.md §8d B_scan
+    kms = st["kernel_ms"]
+    roofline = None
+    kernel_ms_per_scan = {k: (kms[k] / max(1, st["kernel_launches"][k])) for k in kms}
+    if not args.no_profile and sum(kms.values()) > 0:
+        dom = max(kms, key=lambda k: kms[k])
+        t_launch = kernel_ms_per_scan[dom] * 1e-3
+        achieved = bytes_per_scan / t_launch / 1e9
+        traffic = None
+        try:
+            with open(args.traffic_json) as f:
+                traffic = json.load(f).get(dom)
+        except (OSError, ValueError):
+            traffic = None
+        roofline = {"bound": "hbm", "kernel": "k_" + dom, "achieved": round(achieved, 2),
+                    "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 5),
+                    "traffic": traffic,
+                    "algorithmic_bytes_per_launch": round(bytes_per_scan),
+                    "avg_launch_ms": round(kernel_ms_per_scan[dom], 5)}
+    path_ms = sum(kernel_ms_per_scan.values())
+
+    # ---- read-out merge of border bricks (not in the timed region) ----------------------------
+    merge_ms = None
+    if world > 1:
+        from tsdf_map.distributed import merged_bricks
+        dist.barrier()
+        tm = time.perf_counter()
+        merged_bricks(vol, device=dev)
+        dist.barrier()
+        merge_ms = (time.perf_counter() - tm) * 1e3
+
+    # ---- CPU baseline: the oracle on a bounded sample of the same workload (rank 0, N=1) --------
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import oracle
+        ov = oracle.OracleTSDFVolume(args.voxel, args.trunc)
+        x, offs, org = steps[args.warmup]
+        xs = x.cpu().numpy()
+        n_done, tc = 0, time.perf_counter()
+        for j in range(len(org)):
+            ov.integrate(xs[offs[j]:offs[j + 1]], org[j])
+            n_done += 1
+            if time.perf_counter() - tc > args.cpu_seconds:
+                break
+        tc = time.perf_counter() - tc
+        cpu = {"value": round(n_done / tc, 4), "unit": "scans/s", "cores": 1, "kind": "port",
+               "sample": "%d scans of the first timed step, serial C oracle (scan-fused mode), "
+                         "same inputs" % n_done}
+
+    if rank == 0:
+        out = {
+            "metric": "scans/sec TSDF integration (128x1024 pts, 5 cm voxel)",
+            "value": round(value, 2),
+            "unit": "scans/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (OS-1-128 1024x10 beam angles from the reference's metadata "
+                    "fixture; analytic scene; resident in HBM)",
+            "config": {"workload": "C1/M1 ouster_os1_128_1024x10_synthetic_5cm",
+                       "voxel_size_m": args.voxel, "sdf_trunc_m": args.trunc,
+                       "scans_per_step": scans_per_step, "global_batch": scans_per_step,
+                       "points_per_scan": int(round(rays_per_scan * world)),
+                       "parallelism": "azimuth-sector x%d" % world if world > 1 else "single"},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "path_ms_per_scan": round(path_ms, 5),
+            "kernel_ms_per_scan": {k: round(v, 5) for k, v in kernel_ms_per_scan.items()},
+            "uvox_per_scan": round(uvox_per_scan),
+            "bytes_per_scan_algorithmic": round(bytes_per_scan),
+            "path_gbs": round(bytes_per_scan / (path_ms * 1e-3) / 1e9, 2) if path_ms else None,
+            "bricks": st["n_bricks"],
+            "readout_merge_ms": merge_ms,
+            "gen_seconds": round(t_gen, 2),
+        }
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,150 @@
+/*
+ * tsdf_hip.h — C-ABI of the MI355X-native TSDF integration backend (MAP_BACKEND_IDX = 4).
+ *
+ * The reference has no runtime plugin API for this path: backends are chosen by a compile-time
+ * switch `MAP_BACKEND_IDX` in the (unshipped) tsdf_map_node (reference README.md:44-50), and the
+ * node's per-scan slot is the subscriber callback that today lives in
+ * src/dliomapping/dliomapping.cpp:64-81 (`callback_pcl_deskewed`, fed by
+ * `robot/dlio/odom_node/pointcloud/deskewed`, dliomapping.cpp:44).  The backend semantics this
+ * ABI implements are VDBFusion's `VDBVolume::Integrate(points, origin, weighting_function)`
+ * (backend idx 3, named in README.md:48,75; not vendored — restated in DESIGN.md §2).
+ *
+ * Every entry point below replaces one operation that node performs on its backend:
+ *   tsdf_create            <- backend construction (VDBVolume(voxel_size, sdf_trunc, space_carving))
+ *   tsdf_integrate         <- backend.Integrate(cloud, origin) inside callback_pcl_deskewed
+ *                             (dliomapping.cpp:64-81; cloud layout dlio::Point, dlio.h:85-106)
+ *   tsdf_integrate_device  <- same, input already resident in HBM (bench / batched replay)
+ *   tsdf_integrate_batch_device <- a sequence of Integrate calls, one per scan, in order
+ *   tsdf_query_dense / tsdf_export_bricks <- the node's map write-out (dliomapping.cpp:53-61,72-80
+ *                             write PLY; .gitignore:9-15 hints the TSDF node wrote .grid/.h5)
+ *   tsdf_import_bricks     <- resume from an exported map (checkpoint) / multi-GPU border merge
+ *   tsdf_destroy           <- node destructor (dliomapping.cpp:53-61)
+ *
+ * Conventions: plain C types only; no exceptions cross the ABI; every call returns a status
+ * (TSDF_OK = 0, negative on error; tsdf_last_error() has the message).  One context is used by one
+ * host thread at a time (the ROS callback thread).  A context owns one HIP device, one stream, the
+ * brick hash table and the brick pool.  Host-pointer integrate copies the caller's points into
+ * pinned staging before returning; the GPU work itself is stream-ordered and may still be running
+ * when the call returns — tsdf_sync() / query / export block.
+ */
+#ifndef TSDF_HIP_H
+#define TSDF_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TSDF_ABI_VERSION 1
+#define TSDF_BRICK_SIDE 8 /* voxels per brick edge: a brick is 8^3 = 512 voxels */
+
+/* status codes */
+#define TSDF_OK 0
+#define TSDF_EINVAL (-1)    /* bad argument */
+#define TSDF_ENOMEM (-2)    /* host/device allocation failed, or brick pool / hash / pair buffer full */
+#define TSDF_EHIP (-3)      /* HIP runtime error (message in tsdf_last_error) */
+#define TSDF_ENODEV (-4)    /* no usable GPU */
+#define TSDF_EOVERFLOW (-5) /* caller buffer too small */
+
+/* weighting functions (VDBFusion's weighting_function argument; default constant 1) */
+#define TSDF_WEIGHT_CONSTANT 0
+
+typedef struct tsdf_params {
+    double voxel_size;     /* metres (VDBVolume voxel_size) */
+    double sdf_trunc;      /* metres, truncation tau (VDBVolume sdf_trunc) */
+    int32_t space_carving; /* 0: band [d-tau, d+tau]; 1: [0, d+tau] (VDBVolume space_carving) */
+    int32_t weight_mode;   /* TSDF_WEIGHT_CONSTANT */
+    double min_range;      /* rays with depth < min_range are dropped (Ouster r=0 -> (0,0,0)) */
+    double max_range;      /* rays with depth > max_range are dropped */
+    uint64_t max_bricks;   /* brick pool capacity (each brick: 512 x (sdf f32, weight f32) = 4 KiB) */
+    uint64_t max_points;   /* per-scan capacity of the host-pointer staging path */
+    uint64_t max_pairs;    /* per-scan capacity of (ray, brick) pairs; 0 = derive from max_points */
+    int32_t device_id;     /* HIP device ordinal */
+    int32_t brick_side;    /* must be TSDF_BRICK_SIDE */
+} tsdf_params;
+
+typedef struct tsdf_stats {
+    uint64_t n_scans;          /* integrate calls completed */
+    uint64_t n_points_in;      /* points handed in */
+    uint64_t n_bricks;         /* allocated bricks (after the last sync) */
+    uint64_t n_pairs_last;     /* (ray, brick) pairs of the last scan */
+    uint64_t n_active_last;    /* bricks touched by the last scan */
+    uint64_t n_voxels_last;    /* unique voxels updated by the last scan (U_vox) */
+    uint64_t n_voxels_total;   /* sum of U_vox over all scans since the last stats reset */
+    uint64_t n_rays_total;     /* valid rays (after range filter) since the last stats reset */
+    double kernel_ms[8];       /* per-kernel-kind accumulated device time when profiling is on */
+    uint64_t kernel_launches[8];
+} tsdf_stats;
+
+/* kernel kinds reported in tsdf_stats.kernel_ms (profiling on) */
+#define TSDF_K_RAYS 0      /* ray prep + brick hash insert + (ray, brick) pair emission */
+#define TSDF_K_OFFSETS 1   /* per-brick ray-list segment reservation */
+#define TSDF_K_SCATTER 2   /* pair -> per-brick ray list */
+#define TSDF_K_INTEGRATE 3 /* per-brick LDS tile accumulate + fuse into the persistent field */
+
+typedef struct tsdf_ctx tsdf_ctx;
+
+/* Fill *p with the defaults (5 cm voxel, 15 cm trunc, no carving, 1M bricks, 262144 points). */
+void tsdf_default_params(tsdf_params* p);
+int tsdf_abi_version(void);
+
+int tsdf_create(const tsdf_params* params, tsdf_ctx** out);
+void tsdf_destroy(tsdf_ctx* ctx);
+const char* tsdf_last_error(const tsdf_ctx* ctx);
+
+/* One scan from host memory, in any PointCloud2-like layout: point i's x,y,z are at
+ * (const char*)pts + i*point_step + xyz_offset, as three consecutive float32 (xyz_is_f64 = 0,
+ * e.g. dlio::Point: point_step 32, xyz_offset 0) or float64 (xyz_is_f64 = 1).  origin is the
+ * sensor position in the same (world) frame. */
+int tsdf_integrate(tsdf_ctx* ctx, const void* pts, uint64_t n, uint32_t point_step,
+                   uint32_t xyz_offset, int32_t xyz_is_f64, const double origin[3]);
+
+/* One scan already in device memory: d_xyz = n packed float32 triplets (12 B per point). */
+int tsdf_integrate_device(tsdf_ctx* ctx, const float* d_xyz, uint64_t n, const double origin[3]);
+
+/* n_scans scans in device memory, integrated in order.  Scan s is the points
+ * d_xyz[3*scan_offsets[s] .. 3*scan_offsets[s+1]) (offsets in points, host array of n_scans+1)
+ * seen from origins[3*s .. 3*s+3) (host array). */
+int tsdf_integrate_batch_device(tsdf_ctx* ctx, const float* d_xyz, const uint64_t* scan_offsets,
+                                uint32_t n_scans, const double* origins);
+
+/* Block until all queued work finished; reports a deferred capacity overflow as TSDF_ENOMEM. */
+int tsdf_sync(tsdf_ctx* ctx);
+
+/* Dense read-out of voxels lo..hi-1 (voxel index coordinates, voxel i spans [i*vs, (i+1)*vs)),
+ * x fastest: out[((z-lo2)*(hi1-lo1) + (y-lo1))*(hi0-lo0) + (x-lo0)].  Unobserved voxels read
+ * (sdf_trunc, 0) — VDBFusion's background values.  sdf / weight are host buffers. */
+int tsdf_query_dense(tsdf_ctx* ctx, const int32_t lo[3], const int32_t hi[3], float* sdf,
+                     float* weight);
+
+int tsdf_num_bricks(tsdf_ctx* ctx, uint64_t* n);
+
+/* Copy every allocated brick out: coords[3*i..] = brick coordinates (voxel = 8*brick + local),
+ * sdf/weight[512*i + (z*64 + y*8 + x)].  cap = capacity in bricks; *n_out = bricks written.
+ * Returns TSDF_EOVERFLOW (and *n_out = required count) when cap is too small. */
+int tsdf_export_bricks(tsdf_ctx* ctx, int32_t* coords, float* sdf, float* weight, uint64_t cap,
+                       uint64_t* n_out);
+
+/* Merge n unique bricks into the field: for every voxel with weight w_in > 0,
+ * sdf <- (sdf*W + sdf_in*w_in) / (W + w_in), W <- W + w_in, or a plain copy where W == 0
+ * (weighted-mean merge of partial fields; used for multi-GPU border bricks and for resuming
+ * from an export). */
+int tsdf_import_bricks(tsdf_ctx* ctx, const int32_t* coords, const float* sdf, const float* weight,
+                       uint64_t n);
+
+int tsdf_get_stats(tsdf_ctx* ctx, tsdf_stats* out);
+int tsdf_reset_stats(tsdf_ctx* ctx);
+/* Record HIP events around every kernel (per-kind device time in tsdf_stats.kernel_ms). */
+int tsdf_set_profiling(tsdf_ctx* ctx, int32_t on);
+
+/* Azimuth-sector selection for multi-GPU sharding: keep the points whose azimuth around origin
+ * (atan2(y-oy, x-ox) in [-pi, pi), offset by yaw0) falls in sector `sector` of `n_sectors`
+ * equal sectors.  Writes the selected points packed to out_xyz (host, 3 f32 each). */
+int tsdf_select_sector(const float* xyz, uint64_t n, const double origin[3], double yaw0,
+                       uint32_t sector, uint32_t n_sectors, float* out_xyz, uint64_t* n_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TSDF_HIP_H */

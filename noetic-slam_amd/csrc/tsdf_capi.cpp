@@ -1,0 +1,552 @@
+// tsdf_capi.cpp — extern "C" boundary of libtsdf_hip.so (declared in include/tsdf_hip.h).
+//
+// One tsdf_ctx = one HIP device + one non-blocking stream + the brick hash table, brick pool and
+// per-scan work buffers, all allocated once at create (no allocation on the integrate path).  The
+// host-pointer integrate packs the caller's PointCloud2-style records (any point_step/xyz_offset,
+// f32 or f64 xyz) into one of two pinned staging buffers, issues the H2D copy and the four kernels
+// on the stream and returns; tsdf_sync() waits and reports a deferred capacity overflow.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "../../include/tsdf_hip.h"
+#include "tsdf_device.h"
+
+using namespace tsdf;
+
+namespace {
+
+struct EventTimer final : KernelTimer {
+    struct Rec { int kind; hipEvent_t a, b; };
+    std::vector<hipEvent_t> free_ev;
+    std::vector<Rec> pending;
+    hipEvent_t open_ev[KIND_N] = {};
+    double ms[KIND_N] = {};
+    uint64_t launches[KIND_N] = {};
+
+    hipEvent_t get() {
+        if (free_ev.empty()) {
+            hipEvent_t e;
+            if (hipEventCreate(&e) != hipSuccess) return nullptr;
+            return e;
+        }
+        hipEvent_t e = free_ev.back();
+        free_ev.pop_back();
+        return e;
+    }
+    void begin(int kind, hipStream_t st) override {
+        open_ev[kind] = get();
+        if (open_ev[kind]) (void)hipEventRecord(open_ev[kind], st);
+    }
+    void end(int kind, hipStream_t st) override {
+        hipEvent_t e = get();
+        if (!e || !open_ev[kind]) return;
+        (void)hipEventRecord(e, st);
+        pending.push_back({kind, open_ev[kind], e});
+        open_ev[kind] = nullptr;
+    }
+    // call only after the stream drained
+    void harvest() {
+        for (auto& r : pending) {
+            float t = 0.f;
+            if (hipEventElapsedTime(&t, r.a, r.b) == hipSuccess) {
+                ms[r.kind] += t;
+                launches[r.kind]++;
+            }
+            free_ev.push_back(r.a);
+            free_ev.push_back(r.b);
+        }
+        pending.clear();
+    }
+    void reset() {
+        std::fill(ms, ms + KIND_N, 0.0);
+        std::fill(launches, launches + KIND_N, 0);
+    }
+    ~EventTimer() override {
+        for (auto& r : pending) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
+        for (auto e : free_ev) (void)hipEventDestroy(e);
+    }
+};
+
+uint64_t next_pow2(uint64_t v) {
+    uint64_t p = 1;
+    while (p < v) p <<= 1;
+    return p;
+}
+
+}  // namespace
+
+struct tsdf_ctx {
+    tsdf_params p{};
+    int device = 0;
+    hipStream_t stream = nullptr;
+    Table T{};
+    Pool Pl{};
+    Work Wk{};
+    Globals* G = nullptr;
+    uint64_t cap = 0;
+    uint64_t max_points = 0;
+    // host-pointer staging (double-buffered pinned memory + the device copy target)
+    float* h_stage[2] = {nullptr, nullptr};
+    hipEvent_t stage_done[2] = {nullptr, nullptr};
+    float* d_stage[2] = {nullptr, nullptr};
+    int stage_cur = 0;
+    uint64_t scan_id = 0;
+    uint64_t n_points_in = 0;
+    EventTimer* timer = nullptr;
+    std::string err;
+};
+
+static int fail(tsdf_ctx* c, int code, const char* fmt, ...) {
+    if (c) {
+        char buf[512];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof buf, fmt, ap);
+        va_end(ap);
+        c->err = buf;
+    }
+    return code;
+}
+
+#define HIPCHK(c, expr)                                                                        \
+    do {                                                                                       \
+        hipError_t e_ = (expr);                                                                \
+        if (e_ != hipSuccess)                                                                  \
+            return fail((c), TSDF_EHIP, "%s failed: %s", #expr, hipGetErrorString(e_));      \
+    } while (0)
+
+// pair slots per ray: the distinct bricks a DDA over a band of E voxels per axis can visit
+static uint32_t pairs_per_ray(const tsdf_params& p) {
+    double band;  // band length in voxels along the ray
+    if (p.space_carving) band = (p.max_range + p.sdf_trunc) / p.voxel_size;
+    else band = 2.0 * p.sdf_trunc / p.voxel_size;
+    const double e = std::ceil(band) + 2.0;              // visited extent per axis, with margin
+    const double per_axis = std::floor((e + 1.0) / TSDF_BRICK_SIDE) + 1.0;  // boundary crossings
+    return (uint32_t)(1.0 + 3.0 * per_axis);
+}
+
+extern "C" {
+
+void tsdf_default_params(tsdf_params* p) {
+    if (!p) return;
+    std::memset(p, 0, sizeof *p);
+    p->voxel_size = 0.05;
+    p->sdf_trunc = 0.15;
+    p->space_carving = 0;
+    p->weight_mode = TSDF_WEIGHT_CONSTANT;
+    p->min_range = 0.0;
+    p->max_range = INFINITY;
+    p->max_bricks = 1u << 20;
+    p->max_points = 1u << 18;
+    p->max_pairs = 0;
+    p->device_id = 0;
+    p->brick_side = TSDF_BRICK_SIDE;
+}
+
+int tsdf_abi_version(void) { return TSDF_ABI_VERSION; }
+
+const char* tsdf_last_error(const tsdf_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+void tsdf_destroy(tsdf_ctx* c) {
+    if (!c) return;
+    if (c->device >= 0) (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    delete c->timer;
+    void* dev[] = {c->T.keys, c->T.slots, c->T.cnt, c->T.toff, c->T.brick_keys, c->Pl.sdf,
+                   c->Pl.weight, c->Wk.pair_tidx, c->Wk.pair_local, c->Wk.ray_list, c->Wk.active,
+                   c->G, c->d_stage[0], c->d_stage[1]};
+    for (void* d : dev)
+        if (d) (void)hipFree(d);
+    for (int i = 0; i < 2; i++) {
+        if (c->h_stage[i]) (void)hipHostFree(c->h_stage[i]);
+        if (c->stage_done[i]) (void)hipEventDestroy(c->stage_done[i]);
+    }
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
+    c->p = *p;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        return fail(c, TSDF_ENODEV, "no HIP device available");
+    if (p->device_id < 0 || p->device_id >= ndev)
+        return fail(c, TSDF_EINVAL, "device_id %d out of range (%d devices)", p->device_id, ndev);
+    c->device = p->device_id;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+
+    const uint32_t maxp = pairs_per_ray(*p);
+    c->max_points = p->max_points;
+    uint64_t slots = c->max_points * maxp;
+    if (p->max_pairs && p->max_pairs < slots) slots = p->max_pairs;  // caller-imposed cap
+    if (slots >= 0xFFFFFFF0ull || slots == 0)
+        return fail(c, TSDF_EINVAL, "max_points * pairs_per_ray = %llu out of range",
+                    (unsigned long long)slots);
+    c->max_points = slots / maxp;
+    c->cap = next_pow2(2 * p->max_bricks);
+    c->T.mask = c->cap - 1;
+    c->T.max_bricks = (uint32_t)p->max_bricks;
+    c->Wk.maxp = maxp;
+
+    HIPCHK(c, hipMalloc(&c->T.keys, c->cap * sizeof(uint64_t)));
+    HIPCHK(c, hipMalloc(&c->T.slots, c->cap * sizeof(uint32_t)));
+    HIPCHK(c, hipMalloc(&c->T.cnt, c->cap * sizeof(uint32_t)));
+    HIPCHK(c, hipMalloc(&c->T.toff, c->cap * sizeof(uint32_t)));
+    HIPCHK(c, hipMalloc(&c->T.brick_keys, p->max_bricks * sizeof(uint64_t)));
+    HIPCHK(c, hipMalloc(&c->Pl.sdf, p->max_bricks * BRICK_VOX * sizeof(float)));
+    HIPCHK(c, hipMalloc(&c->Pl.weight, p->max_bricks * BRICK_VOX * sizeof(float)));
+    HIPCHK(c, hipMalloc(&c->Wk.pair_tidx, slots * sizeof(uint32_t)));
+    HIPCHK(c, hipMalloc(&c->Wk.pair_local, slots * sizeof(uint32_t)));
+    HIPCHK(c, hipMalloc(&c->Wk.ray_list, slots * sizeof(uint32_t)));
+    HIPCHK(c, hipMalloc(&c->Wk.active, slots * sizeof(uint32_t)));
+    HIPCHK(c, hipMalloc(&c->G, sizeof(Globals)));
+    for (int i = 0; i < 2; i++) {
+        HIPCHK(c, hipMalloc(&c->d_stage[i], c->max_points * 3 * sizeof(float)));
+        HIPCHK(c, hipHostMalloc(&c->h_stage[i], c->max_points * 3 * sizeof(float),
+                                hipHostMallocDefault));
+        HIPCHK(c, hipEventCreateWithFlags(&c->stage_done[i], hipEventDisableTiming));
+    }
+    // VDBFusion background: tsdf = sdf_trunc, weight = 0
+    HIPCHK(c, launch_fill_u64(c->T.keys, EMPTY_KEY, c->cap, c->stream));
+    HIPCHK(c, launch_fill_u32(c->T.slots, UNASSIGNED, c->cap, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->T.cnt, 0, c->cap * sizeof(uint32_t), c->stream));
+    HIPCHK(c, launch_fill(c->Pl.sdf, (float)p->sdf_trunc, p->max_bricks * BRICK_VOX, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->Pl.weight, 0, p->max_bricks * BRICK_VOX * sizeof(float),
+                             c->stream));
+    HIPCHK(c, hipMemsetAsync(c->G, 0, sizeof(Globals), c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return TSDF_OK;
+}
+
+int tsdf_create(const tsdf_params* p, tsdf_ctx** out) {
+    if (!p || !out) return TSDF_EINVAL;
+    *out = nullptr;
+    if (!(p->voxel_size > 0) || !(p->sdf_trunc > 0) || p->brick_side != TSDF_BRICK_SIDE ||
+        p->weight_mode != TSDF_WEIGHT_CONSTANT || p->max_bricks == 0 ||
+        p->max_bricks >= 0xFFFFFFF0ull || p->max_points == 0 || !(p->min_range >= 0) ||
+        !(p->max_range > p->min_range))
+        return TSDF_EINVAL;
+    if (p->space_carving && !std::isfinite(p->max_range)) return TSDF_EINVAL;
+    tsdf_ctx* c = new (std::nothrow) tsdf_ctx();
+    if (!c) return TSDF_ENOMEM;
+    c->device = -1;
+    const int rc = create_impl(c, p);
+    if (rc != TSDF_OK) {
+        fprintf(stderr, "tsdf_create: %s\n", c->err.c_str());
+        tsdf_destroy(c);
+        return rc;
+    }
+    *out = c;
+    return TSDF_OK;
+}
+
+static ScanParams scan_params(const tsdf_ctx* c, const double origin[3]) {
+    ScanParams P;
+    P.vs = (float)c->p.voxel_size;
+    P.inv_vs = 1.0f / P.vs;
+    P.tau = (float)c->p.sdf_trunc;
+    P.min_range = (float)c->p.min_range;
+    P.max_range = (float)c->p.max_range;
+    P.ox = (float)origin[0];
+    P.oy = (float)origin[1];
+    P.oz = (float)origin[2];
+    P.carving = c->p.space_carving ? 1 : 0;
+    return P;
+}
+
+static int run_scan(tsdf_ctx* c, const float* d_xyz, uint64_t n, const double origin[3]) {
+    if (n > c->max_points)
+        return fail(c, TSDF_EINVAL, "scan of %llu points exceeds max_points %llu",
+                    (unsigned long long)n, (unsigned long long)c->max_points);
+    const ScanParams P = scan_params(c, origin);
+    const int parity = (int)(c->scan_id & 1);
+    HIPCHK(c, launch_scan(d_xyz, (uint32_t)n, P, c->T, c->Wk, c->Pl, c->G, parity, c->stream,
+                          c->timer));
+    c->scan_id++;
+    c->n_points_in += n;
+    if (c->timer && c->timer->pending.size() > 8192) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        c->timer->harvest();
+    }
+    return TSDF_OK;
+}
+
+int tsdf_integrate(tsdf_ctx* c, const void* pts, uint64_t n, uint32_t point_step,
+                   uint32_t xyz_offset, int32_t xyz_is_f64, const double origin[3]) {
+    if (!c) return TSDF_EINVAL;
+    if ((!pts && n) || !origin) return fail(c, TSDF_EINVAL, "null argument");
+    const uint32_t need = xyz_is_f64 ? 24u : 12u;
+    if (point_step < need || xyz_offset > point_step - need)
+        return fail(c, TSDF_EINVAL, "point_step/xyz_offset inconsistent");
+    if (n > c->max_points)
+        return fail(c, TSDF_EINVAL, "scan of %llu points exceeds max_points %llu",
+                    (unsigned long long)n, (unsigned long long)c->max_points);
+    HIPCHK(c, hipSetDevice(c->device));
+    const int b = c->stage_cur;
+    c->stage_cur ^= 1;
+    HIPCHK(c, hipEventSynchronize(c->stage_done[b]));  // previous copy out of this buffer is done
+    float* h = c->h_stage[b];
+    const char* base = static_cast<const char*>(pts);
+    if (!xyz_is_f64 && point_step == 12 && xyz_offset == 0) {
+        std::memcpy(h, base, n * 12);
+    } else {
+        for (uint64_t i = 0; i < n; i++) {
+            const char* q = base + i * point_step + xyz_offset;
+            if (xyz_is_f64) {
+                double d[3];
+                std::memcpy(d, q, sizeof d);
+                h[3 * i] = (float)d[0];
+                h[3 * i + 1] = (float)d[1];
+                h[3 * i + 2] = (float)d[2];
+            } else {
+                std::memcpy(h + 3 * i, q, 12);
+            }
+        }
+    }
+    HIPCHK(c, hipMemcpyAsync(c->d_stage[b], h, n * 12, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipEventRecord(c->stage_done[b], c->stream));
+    return run_scan(c, c->d_stage[b], n, origin);
+}
+
+int tsdf_integrate_device(tsdf_ctx* c, const float* d_xyz, uint64_t n, const double origin[3]) {
+    if (!c) return TSDF_EINVAL;
+    if ((!d_xyz && n) || !origin) return fail(c, TSDF_EINVAL, "null argument");
+    HIPCHK(c, hipSetDevice(c->device));
+    return run_scan(c, d_xyz, n, origin);
+}
+
+int tsdf_integrate_batch_device(tsdf_ctx* c, const float* d_xyz, const uint64_t* offs,
+                                uint32_t n_scans, const double* origins) {
+    if (!c) return TSDF_EINVAL;
+    if (!offs || !origins || (!d_xyz && n_scans)) return fail(c, TSDF_EINVAL, "null argument");
+    HIPCHK(c, hipSetDevice(c->device));
+    for (uint32_t s = 0; s < n_scans; s++) {
+        if (offs[s + 1] < offs[s]) return fail(c, TSDF_EINVAL, "scan_offsets not monotone");
+        const int rc = run_scan(c, d_xyz + 3 * offs[s], offs[s + 1] - offs[s], origins + 3 * s);
+        if (rc != TSDF_OK) return rc;
+    }
+    return TSDF_OK;
+}
+
+int tsdf_sync(tsdf_ctx* c) {
+    if (!c) return TSDF_EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->timer) c->timer->harvest();
+    uint32_t ovf = 0;
+    HIPCHK(c, hipMemcpy(&ovf, &c->G->overflow, sizeof ovf, hipMemcpyDeviceToHost));
+    if (ovf) {
+        HIPCHK(c, hipMemset(&c->G->overflow, 0, sizeof ovf));
+        return fail(c, TSDF_ENOMEM, "capacity overflow (%s%s%s): updates were dropped",
+                    (ovf & OVF_TABLE) ? "hash table full " : "",
+                    (ovf & OVF_POOL) ? "brick pool exhausted " : "",
+                    (ovf & OVF_PAIRS) ? "ray brick-pair slots exceeded" : "");
+    }
+    return TSDF_OK;
+}
+
+int tsdf_query_dense(tsdf_ctx* c, const int32_t lo[3], const int32_t hi[3], float* sdf,
+                     float* weight) {
+    if (!c) return TSDF_EINVAL;
+    if (!lo || !hi) return fail(c, TSDF_EINVAL, "null argument");
+    int dims[3];
+    for (int a = 0; a < 3; a++) {
+        if (hi[a] < lo[a]) return fail(c, TSDF_EINVAL, "hi < lo");
+        dims[a] = hi[a] - lo[a];
+    }
+    const uint64_t total = (uint64_t)dims[0] * dims[1] * dims[2];
+    if (!total) return TSDF_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    float *ds = nullptr, *dw = nullptr;
+    HIPCHK(c, hipMalloc(&ds, total * sizeof(float)));
+    hipError_t e = hipMalloc(&dw, total * sizeof(float));
+    if (e == hipSuccess) e = launch_query_dense(c->T, c->Pl, lo, dims, (float)c->p.sdf_trunc, ds,
+                                                dw, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess && sdf) e = hipMemcpy(sdf, ds, total * 4, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && weight) e = hipMemcpy(weight, dw, total * 4, hipMemcpyDeviceToHost);
+    (void)hipFree(ds);
+    if (dw) (void)hipFree(dw);
+    if (e != hipSuccess) return fail(c, TSDF_EHIP, "query_dense: %s", hipGetErrorString(e));
+    return TSDF_OK;
+}
+
+static int pool_bricks(tsdf_ctx* c, uint64_t* n) {
+    uint32_t pc = 0;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMemcpy(&pc, &c->G->pool_count, sizeof pc, hipMemcpyDeviceToHost));
+    *n = std::min<uint64_t>(pc, c->p.max_bricks);
+    return TSDF_OK;
+}
+
+int tsdf_num_bricks(tsdf_ctx* c, uint64_t* n) {
+    if (!c || !n) return TSDF_EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    return pool_bricks(c, n);
+}
+
+int tsdf_export_bricks(tsdf_ctx* c, int32_t* coords, float* sdf, float* weight, uint64_t cap,
+                       uint64_t* n_out) {
+    if (!c || !n_out) return TSDF_EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    uint64_t nb = 0;
+    int rc = pool_bricks(c, &nb);
+    if (rc) return rc;
+    *n_out = nb;
+    if (nb > cap) return fail(c, TSDF_EOVERFLOW, "export needs %llu bricks", (unsigned long long)nb);
+    if (!nb) return TSDF_OK;
+    std::vector<uint64_t> keys(nb);
+    std::vector<float> s, w;
+    HIPCHK(c, hipMemcpy(keys.data(), c->T.brick_keys, nb * 8, hipMemcpyDeviceToHost));
+    if (sdf) {
+        s.resize(nb * BRICK_VOX);
+        HIPCHK(c, hipMemcpy(s.data(), c->Pl.sdf, nb * BRICK_VOX * 4, hipMemcpyDeviceToHost));
+    }
+    if (weight) {
+        w.resize(nb * BRICK_VOX);
+        HIPCHK(c, hipMemcpy(w.data(), c->Pl.weight, nb * BRICK_VOX * 4, hipMemcpyDeviceToHost));
+    }
+    auto coord = [&](uint64_t k, int a) {
+        return (int32_t)((keys[k] >> (21 * a)) & 0x1FFFFF) - BRICK_COORD_BIAS;
+    };
+    std::vector<uint64_t> order(nb);
+    std::iota(order.begin(), order.end(), 0);
+    std::sort(order.begin(), order.end(), [&](uint64_t a, uint64_t b) {
+        for (int ax = 2; ax >= 0; ax--)
+            if (coord(a, ax) != coord(b, ax)) return coord(a, ax) < coord(b, ax);
+        return false;
+    });
+    for (uint64_t i = 0; i < nb; i++) {
+        const uint64_t k = order[i];
+        if (coords)
+            for (int a = 0; a < 3; a++) coords[3 * i + a] = coord(k, a);
+        if (sdf) std::memcpy(sdf + i * BRICK_VOX, s.data() + k * BRICK_VOX, BRICK_VOX * 4);
+        if (weight) std::memcpy(weight + i * BRICK_VOX, w.data() + k * BRICK_VOX, BRICK_VOX * 4);
+    }
+    return TSDF_OK;
+}
+
+int tsdf_import_bricks(tsdf_ctx* c, const int32_t* coords, const float* sdf, const float* weight,
+                       uint64_t n) {
+    if (!c) return TSDF_EINVAL;
+    if (!n) return TSDF_OK;
+    if (!coords || !sdf || !weight) return fail(c, TSDF_EINVAL, "null argument");
+    if (n >= 0xFFFFFFF0ull) return fail(c, TSDF_EINVAL, "too many bricks");
+    {  // bricks must be unique and inside the packable range
+        std::vector<uint64_t> k(n);
+        for (uint64_t i = 0; i < n; i++) {
+            for (int a = 0; a < 3; a++)
+                if (coords[3 * i + a] < -BRICK_COORD_BIAS || coords[3 * i + a] >= BRICK_COORD_BIAS)
+                    return fail(c, TSDF_EINVAL, "brick coordinate out of range");
+            k[i] = (uint64_t)(coords[3 * i] + BRICK_COORD_BIAS) |
+                   ((uint64_t)(coords[3 * i + 1] + BRICK_COORD_BIAS) << 21) |
+                   ((uint64_t)(coords[3 * i + 2] + BRICK_COORD_BIAS) << 42);
+        }
+        std::sort(k.begin(), k.end());
+        if (std::adjacent_find(k.begin(), k.end()) != k.end())
+            return fail(c, TSDF_EINVAL, "duplicate brick in import");
+    }
+    HIPCHK(c, hipSetDevice(c->device));
+    int32_t* dc = nullptr;
+    float *ds = nullptr, *dw = nullptr;
+    uint32_t* dt = nullptr;
+    hipError_t e = hipMalloc(&dc, n * 12);
+    if (e == hipSuccess) e = hipMalloc(&ds, n * BRICK_VOX * 4);
+    if (e == hipSuccess) e = hipMalloc(&dw, n * BRICK_VOX * 4);
+    if (e == hipSuccess) e = hipMalloc(&dt, n * 4);
+    if (e == hipSuccess) e = hipMemcpyAsync(dc, coords, n * 12, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(ds, sdf, n * BRICK_VOX * 4, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(dw, weight, n * BRICK_VOX * 4, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = launch_import(c->T, c->Pl, dc, (uint32_t)n, ds, dw, dt, c->G, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    (void)hipFree(dc);
+    (void)hipFree(ds);
+    (void)hipFree(dw);
+    (void)hipFree(dt);
+    if (e != hipSuccess) return fail(c, TSDF_EHIP, "import: %s", hipGetErrorString(e));
+    return tsdf_sync(c);
+}
+
+int tsdf_get_stats(tsdf_ctx* c, tsdf_stats* out) {
+    if (!c || !out) return TSDF_EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->timer) c->timer->harvest();
+    Globals g;
+    HIPCHK(c, hipMemcpy(&g, c->G, sizeof g, hipMemcpyDeviceToHost));
+    std::memset(out, 0, sizeof *out);
+    out->n_scans = c->scan_id;
+    out->n_points_in = c->n_points_in;
+    out->n_bricks = std::min<uint64_t>(g.pool_count, c->p.max_bricks);
+    if (c->scan_id) {
+        const Counters& L = g.ctr[(c->scan_id - 1) & 1];
+        out->n_active_last = L.n_active;
+        for (int k = 0; k < 8; k++) {
+            out->n_voxels_last += L.n_vox[k];
+            out->n_pairs_last += L.n_pairs[k];
+        }
+    }
+    for (int k = 0; k < 8; k++) {
+        out->n_voxels_total += g.tot_vox[k];
+        out->n_rays_total += g.tot_rays[k];
+    }
+    if (c->timer)
+        for (int k = 0; k < KIND_N; k++) {
+            out->kernel_ms[k] = c->timer->ms[k];
+            out->kernel_launches[k] = c->timer->launches[k];
+        }
+    return TSDF_OK;
+}
+
+int tsdf_reset_stats(tsdf_ctx* c) {
+    if (!c) return TSDF_EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->timer) { c->timer->harvest(); c->timer->reset(); }
+    HIPCHK(c, hipMemset(c->G->tot_vox, 0, sizeof(c->G->tot_vox) * 3));
+    c->n_points_in = 0;
+    return TSDF_OK;
+}
+
+int tsdf_set_profiling(tsdf_ctx* c, int32_t on) {
+    if (!c) return TSDF_EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (on && !c->timer) c->timer = new (std::nothrow) EventTimer();
+    if (!on && c->timer) { delete c->timer; c->timer = nullptr; }
+    return (on && !c->timer) ? TSDF_ENOMEM : TSDF_OK;
+}
+
+int tsdf_select_sector(const float* xyz, uint64_t n, const double origin[3], double yaw0,
+                       uint32_t sector, uint32_t n_sectors, float* out_xyz, uint64_t* n_out) {
+    if (!xyz || !origin || !out_xyz || !n_out || n_sectors == 0 || sector >= n_sectors)
+        return TSDF_EINVAL;
+    const double two_pi = 6.283185307179586476925286766559;
+    uint64_t k = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        double az = std::atan2((double)xyz[3 * i + 1] - origin[1], (double)xyz[3 * i] - origin[0]) - yaw0;
+        az = std::fmod(az, two_pi);
+        if (az < 0) az += two_pi;
+        uint32_t s = (uint32_t)(az / two_pi * n_sectors);
+        if (s >= n_sectors) s = n_sectors - 1;
+        if (s == sector) {
+            std::memcpy(out_xyz + 3 * k, xyz + 3 * i, 12);
+            k++;
+        }
+    }
+    *n_out = k;
+    return TSDF_OK;
+}
+
+}  // extern "C"

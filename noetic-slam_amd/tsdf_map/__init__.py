@@ -1,0 +1,28 @@
+"""tsdf_map — host side of the MI355X TSDF backend (MAP_BACKEND_IDX = 4) for noetic-slam.
+
+Named after the reference's mapping package (src/tsdf_map, README.md:44-50).  The backend table
+mirrors the node's compile-time switch; indices 0-3 are the reference's CPU backends, which are not
+in the reference snapshot and so are listed but not constructible here.
+"""
+from ._abi import BRICK_SIDE, BRICK_VOX  # noqa: F401
+from ._lib import HIP_LIB, load_hip_library  # noqa: F401
+from .volume import (HipTSDFVolume, TSDFVolume, TsdfError, bricks_to_voxels,  # noqa: F401
+                     select_sector)
+
+MAP_BACKENDS = {
+    0: "CHAD TSDF (absent from the reference snapshot)",
+    1: "Octomap (absent from the reference snapshot)",
+    2: "Voxblox (absent from the reference snapshot)",
+    3: "VDBFusion (absent from the reference snapshot)",
+    4: "MI355X HIP TSDF (this package)",
+}
+MAP_BACKEND_IDX = 4
+
+
+def make_backend(idx=MAP_BACKEND_IDX, **kw):
+    """Construct backend `idx` the way tsdf_map_node's switch does."""
+    if idx == 4:
+        return HipTSDFVolume(**kw)
+    if idx in MAP_BACKENDS:
+        raise NotImplementedError("MAP_BACKEND_IDX=%d: %s" % (idx, MAP_BACKENDS[idx]))
+    raise ValueError("unknown MAP_BACKEND_IDX %r" % idx)

@@ -1,0 +1,120 @@
+"""ctypes declarations of the C-ABI in include/tsdf_hip.h (shared by every library exporting it)."""
+import ctypes as C
+import math
+
+TSDF_OK = 0
+TSDF_EINVAL = -1
+TSDF_ENOMEM = -2
+TSDF_EHIP = -3
+TSDF_ENODEV = -4
+TSDF_EOVERFLOW = -5
+BRICK_SIDE = 8
+BRICK_VOX = 512
+
+STATUS_NAMES = {
+    TSDF_OK: "TSDF_OK", TSDF_EINVAL: "TSDF_EINVAL", TSDF_ENOMEM: "TSDF_ENOMEM",
+    TSDF_EHIP: "TSDF_EHIP", TSDF_ENODEV: "TSDF_ENODEV", TSDF_EOVERFLOW: "TSDF_EOVERFLOW",
+}
+
+KERNEL_KINDS = ("rays", "compact", "scatter", "integrate")
+
+
+class TsdfParams(C.Structure):
+    _fields_ = [
+        ("voxel_size", C.c_double),
+        ("sdf_trunc", C.c_double),
+        ("space_carving", C.c_int32),
+        ("weight_mode", C.c_int32),
+        ("min_range", C.c_double),
+        ("max_range", C.c_double),
+        ("max_bricks", C.c_uint64),
+        ("max_points", C.c_uint64),
+        ("max_pairs", C.c_uint64),
+        ("device_id", C.c_int32),
+        ("brick_side", C.c_int32),
+    ]
+
+
+class TsdfStats(C.Structure):
+    _fields_ = [
+        ("n_scans", C.c_uint64),
+        ("n_points_in", C.c_uint64),
+        ("n_bricks", C.c_uint64),
+        ("n_pairs_last", C.c_uint64),
+        ("n_active_last", C.c_uint64),
+        ("n_voxels_last", C.c_uint64),
+        ("n_voxels_total", C.c_uint64),
+        ("n_rays_total", C.c_uint64),
+        ("kernel_ms", C.c_double * 8),
+        ("kernel_launches", C.c_uint64 * 8),
+    ]
+
+    def as_dict(self):
+        d = {k: getattr(self, k) for k, _ in self._fields_ if k not in ("kernel_ms", "kernel_launches")}
+        d["kernel_ms"] = {KERNEL_KINDS[i]: self.kernel_ms[i] for i in range(len(KERNEL_KINDS))}
+        d["kernel_launches"] = {KERNEL_KINDS[i]: self.kernel_launches[i]
+                                for i in range(len(KERNEL_KINDS))}
+        return d
+
+
+# every symbol include/tsdf_hip.h declares, with its signature
+P = C.c_void_p
+D3 = C.POINTER(C.c_double)
+I3 = C.POINTER(C.c_int32)
+FP = C.POINTER(C.c_float)
+U64P = C.POINTER(C.c_uint64)
+SIGNATURES = {
+    "tsdf_default_params": (None, [C.POINTER(TsdfParams)]),
+    "tsdf_abi_version": (C.c_int, []),
+    "tsdf_create": (C.c_int, [C.POINTER(TsdfParams), C.POINTER(P)]),
+    "tsdf_destroy": (None, [P]),
+    "tsdf_last_error": (C.c_char_p, [P]),
+    "tsdf_integrate": (C.c_int, [P, P, C.c_uint64, C.c_uint32, C.c_uint32, C.c_int32, D3]),
+    "tsdf_integrate_device": (C.c_int, [P, P, C.c_uint64, D3]),
+    "tsdf_integrate_batch_device": (C.c_int, [P, P, U64P, C.c_uint32, D3]),
+    "tsdf_sync": (C.c_int, [P]),
+    "tsdf_query_dense": (C.c_int, [P, I3, I3, FP, FP]),
+    "tsdf_num_bricks": (C.c_int, [P, U64P]),
+    "tsdf_export_bricks": (C.c_int, [P, I3, FP, FP, C.c_uint64, U64P]),
+    "tsdf_import_bricks": (C.c_int, [P, I3, FP, FP, C.c_uint64]),
+    "tsdf_get_stats": (C.c_int, [P, C.POINTER(TsdfStats)]),
+    "tsdf_reset_stats": (C.c_int, [P]),
+    "tsdf_set_profiling": (C.c_int, [P, C.c_int32]),
+    "tsdf_select_sector": (C.c_int, [FP, C.c_uint64, D3, C.c_double, C.c_uint32, C.c_uint32, FP,
+                                     U64P]),
+}
+
+
+def declare(lib, names=None, optional=()):
+    """Attach restype/argtypes for the ABI symbols present in `lib`; raise if a required one is
+    missing."""
+    missing = []
+    for name, (res, args) in SIGNATURES.items():
+        if names is not None and name not in names:
+            continue
+        fn = getattr(lib, name, None)
+        if fn is None:
+            if name not in optional:
+                missing.append(name)
+            continue
+        fn.restype = res
+        fn.argtypes = args
+    if missing:
+        raise RuntimeError("library %s lacks ABI symbols: %s" % (lib._name, ", ".join(missing)))
+    return lib
+
+
+def default_params(lib=None, **kw):
+    p = TsdfParams()
+    if lib is not None:
+        lib.tsdf_default_params(C.byref(p))
+    else:
+        p.voxel_size, p.sdf_trunc, p.space_carving, p.weight_mode = 0.05, 0.15, 0, 0
+        p.min_range, p.max_range = 0.0, math.inf
+        p.max_bricks, p.max_points, p.max_pairs = 1 << 20, 1 << 18, 0
+        p.device_id, p.brick_side = 0, BRICK_SIDE
+    for k, v in kw.items():
+        if not hasattr(p, k):
+            raise TypeError("unknown tsdf_params field %r" % k)
+        setattr(p, k, v)
+    return p

@@ -1,0 +1,28 @@
+"""Loader for the in-tree HIP library (noetic-slam_amd/lib/libtsdf_hip.so)."""
+import ctypes
+import os
+
+from . import _abi
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_DIR = os.path.join(PKG_ROOT, "lib")
+HIP_LIB = os.path.join(LIB_DIR, "libtsdf_hip.so")
+
+_hip = None
+
+
+def load_hip_library(path=None):
+    """Load and declare libtsdf_hip.so; raises (never falls back) when it is missing."""
+    global _hip
+    if _hip is not None and path is None:
+        return _hip
+    p = path or HIP_LIB
+    if not os.path.exists(p):
+        raise RuntimeError("libtsdf_hip.so not built (%s); run `python -c 'import __graft_entry__ "
+                           "as g; g.build()'` or `make -C noetic-slam_amd/csrc`" % p)
+    lib = _abi.declare(ctypes.CDLL(p))
+    if lib.tsdf_abi_version() != 1:
+        raise RuntimeError("libtsdf_hip.so ABI version mismatch")
+    if path is None:
+        _hip = lib
+    return lib

@@ -1,0 +1,106 @@
+"""The C-ABI boundary: libtsdf_hip.so loads, exports every symbol include/tsdf_hip.h declares, and
+fails loudly (no CPU fallback) where no GPU exists.  No compute calls here — CPU suite."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import REPO
+
+HEADER = os.path.join(REPO, "include", "tsdf_hip.h")
+
+
+def header_functions():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(tsdf_[a-z_]+)\s*\(", txt)))
+
+
+def dynamic_symbols(path):
+    out = subprocess.check_output(["nm", "-D", "--defined-only", path], text=True)
+    return {line.split()[-1] for line in out.splitlines() if line.strip()}
+
+
+def test_header_declares_the_abi():
+    fns = header_functions()
+    from tsdf_map import _abi
+    assert set(fns) == set(_abi.SIGNATURES), "ctypes table out of sync with the header"
+
+
+def test_hip_library_exports_every_declared_symbol():
+    from tsdf_map import HIP_LIB, load_hip_library
+    assert os.path.exists(HIP_LIB), "run __graft_entry__.build() first"
+    syms = dynamic_symbols(HIP_LIB)
+    missing = [f for f in header_functions() if f not in syms]
+    assert not missing, missing
+    lib = load_hip_library()
+    assert lib.tsdf_abi_version() == 1
+
+
+def test_hip_library_is_gfx950_code():
+    from tsdf_map import HIP_LIB
+    out = subprocess.check_output(["strings", HIP_LIB], text=True)
+    assert "amdgcn-amd-amdhsa--gfx950" in out
+
+
+def test_oracle_exports_the_host_subset():
+    import oracle
+    lib = oracle.load()
+    syms = dynamic_symbols(oracle.LIB_PATH)
+    for f in header_functions():
+        if f in oracle.HOST_ONLY:
+            continue
+        assert f in syms, f
+
+
+def test_default_params_roundtrip():
+    from tsdf_map import _abi, load_hip_library
+    lib = load_hip_library()
+    p = _abi.default_params(lib)
+    assert p.voxel_size == 0.05 and p.sdf_trunc == 0.15 and p.brick_side == 8
+    assert p.space_carving == 0 and np.isinf(p.max_range)
+
+
+@pytest.mark.skipif(os.path.exists("/dev/kfd") and os.access("/dev/kfd", os.R_OK),
+                    reason="a GPU is present")
+def test_no_gpu_fails_loudly():
+    """Without a GPU the product path raises (TSDF_ENODEV); it never falls back to the CPU."""
+    from tsdf_map import HipTSDFVolume, TsdfError, _abi
+    with pytest.raises(TsdfError) as e:
+        HipTSDFVolume(0.05, 0.15)
+    assert e.value.code in (_abi.TSDF_ENODEV, _abi.TSDF_EHIP)
+
+
+def test_invalid_params_rejected_before_device():
+    from tsdf_map import _abi, load_hip_library
+    lib = load_hip_library()
+    for kw in ({"voxel_size": 0.0}, {"sdf_trunc": -1.0}, {"brick_side": 16},
+               {"space_carving": 1}):  # carving needs a finite max_range
+        p = _abi.default_params(lib, **kw)
+        ctx = ctypes.c_void_p()
+        assert lib.tsdf_create(ctypes.byref(p), ctypes.byref(ctx)) == _abi.TSDF_EINVAL
+        assert not ctx.value
+
+
+def test_backend_switch():
+    import tsdf_map
+    assert tsdf_map.MAP_BACKEND_IDX == 4
+    for idx in range(4):
+        with pytest.raises(NotImplementedError):
+            tsdf_map.make_backend(idx, voxel_size=0.05, sdf_trunc=0.15)
+    with pytest.raises(ValueError):
+        tsdf_map.make_backend(9)
+
+
+def test_product_package_never_imports_the_oracle():
+    pkg = os.path.join(REPO, "noetic-slam_amd")
+    for root, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith((".py", ".cpp", ".hip", ".h", ".hpp", "Makefile")):
+                txt = open(os.path.join(root, f), errors="ignore").read()
+                for pat in (r"#\s*include\s*[\"<][^\">]*oracle", r"libtsdf_oracle", r"-ltsdf_oracle",
+                            r"^\s*(import|from)\s+oracle", r"oracle/build"):
+                    assert not re.search(pat, txt, flags=re.M), (f, pat)
