@@ -196,7 +196,7 @@ def test_device_resident_batch_matches_host_path(sim):
 def test_query_dense_matches_oracle(scan0):
     g, o = run_both([(decimate(scan0[0], 4), scan0[1])])
     ijk, _, _ = o.export_voxels()
-    lo = ijk.min(0) + np.array([30, 40, 5])
+    lo = ijk[len(ijk) // 2] - np.array([32, 24, 12])  # a box around an observed voxel
     hi = lo + np.array([64, 48, 24])
     gs, gw = g.query_dense(lo, hi)
     os_, ow = o.query_dense(lo, hi)

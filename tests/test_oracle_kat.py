@@ -249,14 +249,14 @@ def test_brick_export_matches_voxel_export(scan0):
         assert np.array_equal(x, y)
     # dense query over the bounding box agrees with the sparse export
     ijk, s, w = b
-    lo = ijk.min(0)
+    lo = ijk[len(ijk) // 2] - np.array([20, 20, 10])  # a box around an observed voxel
     hi = lo + np.array([40, 40, 20])
     qs, qw = v.query_dense(lo, hi)
     m = np.all((ijk >= lo) & (ijk < hi), 1)
     rel = ijk[m] - lo
     assert np.array_equal(qs[rel[:, 2], rel[:, 1], rel[:, 0]], s[m])
     assert np.array_equal(qw[rel[:, 2], rel[:, 1], rel[:, 0]], w[m])
-    assert np.count_nonzero(qw) == np.count_nonzero(m)
+    assert np.count_nonzero(qw) == np.count_nonzero(m) > 0
     assert np.all(qs[qw == 0] == np.float32(TAU))
 
 
