@@ -87,7 +87,7 @@ def main():
     max_pts = max(int(np.diff(o).max()) for _, o, _ in steps)
 
     vol = HipTSDFVolume(args.voxel, args.trunc, max_points=max(max_pts, 1 << 17),
-                        max_bricks=1 << 20, device_id=local)
+                        max_bricks=1 << 20, device_id=local, max_batch=min(args.batch, 64))
 
     def run_step(i):
         x, offs, org = steps[i]
@@ -122,17 +122,22 @@ def main():
     value = total_scans / elapsed
 
     # ---- roofline of the dominant kernel (per-launch means, this rank) -------------------------
-    n_launch = max(1, args.steps * scans_per_step)
-    rays_per_scan = st["n_rays_total"] / n_launch
-    uvox_per_scan = st["n_voxels_total"] / n_launch
+    # One launch = one batch of scans.  Algorithmic bytes of a batch: every valid
+    # ray's xyz read once (12 B) + every voxel the batch updates read and written once (8 + 8 B).
+    # The per-scan figure of SURVEY.md §8d (12 N + 16 U_vox per scan) is reported beside it.
+    n_batches = max(1, st["n_batches"])
+    n_scans_rank = max(1, st["n_scans"])
+    rays_per_scan = st["n_rays_total"] / n_scans_rank
+    uvox_per_scan = st["n_voxels_total"] / n_scans_rank
     bytes_per_scan = 12.0 * rays_per_scan + 16.0 * uvox_per_scan  # SURVEY.md §8d B_scan
+    bytes_per_batch = (12.0 * st["n_rays_total"] + 16.0 * st["n_dirty_total"]) / n_batches
     kms = st["kernel_ms"]
     roofline = None
-    kernel_ms_per_scan = {k: (kms[k] / max(1, st["kernel_launches"][k])) for k in kms}
+    kernel_ms_per_launch = {k: (kms[k] / max(1, st["kernel_launches"][k])) for k in kms}
     if not args.no_profile and sum(kms.values()) > 0:
         dom = max(kms, key=lambda k: kms[k])
-        t_launch = kernel_ms_per_scan[dom] * 1e-3
-        achieved = bytes_per_scan / t_launch / 1e9
+        t_launch = kernel_ms_per_launch[dom] * 1e-3
+        achieved = bytes_per_batch / t_launch / 1e9
         traffic = None
         try:
             with open(args.traffic_json) as f:
@@ -142,9 +147,10 @@ def main():
         roofline = {"bound": "hbm", "kernel": "k_" + dom, "achieved": round(achieved, 2),
                     "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 5),
                     "traffic": traffic,
-                    "algorithmic_bytes_per_launch": round(bytes_per_scan),
-                    "avg_launch_ms": round(kernel_ms_per_scan[dom], 5)}
-    path_ms = sum(kernel_ms_per_scan.values())
+                    "algorithmic_bytes_per_launch": round(bytes_per_batch),
+                    "scans_per_launch": round(n_scans_rank / n_batches, 2),
+                    "avg_launch_ms": round(kernel_ms_per_launch[dom], 5)}
+    path_ms_per_scan = sum(kernel_ms_per_launch.values()) * n_batches / n_scans_rank
 
     # ---- read-out merge of border bricks (not in the timed region) ----------------------------
     merge_ms = None
@@ -194,14 +200,17 @@ def main():
                        "voxel_size_m": args.voxel, "sdf_trunc_m": args.trunc,
                        "scans_per_step": scans_per_step, "global_batch": scans_per_step,
                        "points_per_scan": int(round(rays_per_scan * world)),
+                    "scans_per_gpu_batch": args.batch,
                        "parallelism": "azimuth-sector x%d" % world if world > 1 else "single"},
             "roofline": roofline,
             "cpu_baseline": cpu,
-            "path_ms_per_scan": round(path_ms, 5),
-            "kernel_ms_per_scan": {k: round(v, 5) for k, v in kernel_ms_per_scan.items()},
+            "path_ms_per_scan": round(path_ms_per_scan, 5),
+            "kernel_ms_per_launch": {k: round(v, 5) for k, v in kernel_ms_per_launch.items()},
             "uvox_per_scan": round(uvox_per_scan),
-            "bytes_per_scan_algorithmic": round(bytes_per_scan),
-            "path_gbs": round(bytes_per_scan / (path_ms * 1e-3) / 1e9, 2) if path_ms else None,
+            "dirty_voxels_per_batch": round(st["n_dirty_total"] / n_batches),
+            "survey_bytes_per_scan": round(bytes_per_scan),
+            "survey_gbs": round(bytes_per_scan / (path_ms_per_scan * 1e-3) / 1e9, 2)
+            if path_ms_per_scan else None,
             "bricks": st["n_bricks"],
             "readout_merge_ms": merge_ms,
             "gen_seconds": round(t_gen, 2),

@@ -36,7 +36,8 @@
 extern "C" {
 #endif
 
-#define TSDF_ABI_VERSION 1
+#define TSDF_ABI_VERSION 2
+#define TSDF_MAX_BATCH 64 /* scans per GPU batch (see tsdf_params.max_batch) */
 #define TSDF_BRICK_SIDE 8 /* voxels per brick edge: a brick is 8^3 = 512 voxels */
 
 /* status codes */
@@ -58,30 +59,41 @@ typedef struct tsdf_params {
     double min_range;      /* rays with depth < min_range are dropped (Ouster r=0 -> (0,0,0)) */
     double max_range;      /* rays with depth > max_range are dropped */
     uint64_t max_bricks;   /* brick pool capacity (each brick: 512 x (sdf f32, weight f32) = 4 KiB) */
-    uint64_t max_points;   /* per-scan capacity of the host-pointer staging path */
-    uint64_t max_pairs;    /* per-scan capacity of (ray, brick) pairs; 0 = derive from max_points */
+    uint64_t max_points;   /* per-scan point capacity */
+    uint64_t max_pairs;    /* cap on (ray, brick) pair slots per batch; 0 = derive */
     int32_t device_id;     /* HIP device ordinal */
     int32_t brick_side;    /* must be TSDF_BRICK_SIDE */
+    uint32_t max_batch;    /* scans integrated per GPU batch, 1..TSDF_MAX_BATCH (default 32) */
+    uint32_t reserved;
 } tsdf_params;
 
+/* Batching.  Scans are integrated in call order and the field after any sequence of calls is
+ * bitwise the one scan-at-a-time integration gives; the GPU merely processes up to max_batch
+ * consecutive scans per launch sequence (rays of all of them walk together; each brick applies
+ * its per-scan fuses in scan order).  Host-pointer scans are copied to device staging at once and
+ * queued until max_batch are pending; any other call (sync, query, export, import, stats, a
+ * device-pointer integrate) flushes the queue first. */
+
 typedef struct tsdf_stats {
-    uint64_t n_scans;          /* integrate calls completed */
+    uint64_t n_scans;          /* scans integrated (queued scans are flushed first) */
     uint64_t n_points_in;      /* points handed in */
-    uint64_t n_bricks;         /* allocated bricks (after the last sync) */
-    uint64_t n_pairs_last;     /* (ray, brick) pairs of the last scan */
-    uint64_t n_active_last;    /* bricks touched by the last scan */
-    uint64_t n_voxels_last;    /* unique voxels updated by the last scan (U_vox) */
-    uint64_t n_voxels_total;   /* sum of U_vox over all scans since the last stats reset */
-    uint64_t n_rays_total;     /* valid rays (after range filter) since the last stats reset */
+    uint64_t n_bricks;         /* allocated bricks */
+    uint64_t n_pairs_last;     /* (ray, brick) pairs of the last batch */
+    uint64_t n_active_last;    /* bricks touched by the last batch */
+    uint64_t n_voxels_last;    /* sum over the last batch's scans of their unique voxels */
+    uint64_t n_voxels_total;   /* sum over scans of U_vox (unique voxels of the scan) since reset */
+    uint64_t n_rays_total;     /* valid rays (after the range filter) since reset */
+    uint64_t n_dirty_total;    /* sum over batches of the distinct voxels the batch updated */
+    uint64_t n_batches;        /* GPU batches launched since reset */
     double kernel_ms[8];       /* per-kernel-kind accumulated device time when profiling is on */
     uint64_t kernel_launches[8];
 } tsdf_stats;
 
 /* kernel kinds reported in tsdf_stats.kernel_ms (profiling on) */
-#define TSDF_K_RAYS 0      /* ray prep + brick hash insert + (ray, brick) pair emission */
-#define TSDF_K_OFFSETS 1   /* per-brick ray-list segment reservation */
-#define TSDF_K_SCATTER 2   /* pair -> per-brick ray list */
-#define TSDF_K_INTEGRATE 3 /* per-brick LDS tile accumulate + fuse into the persistent field */
+#define TSDF_K_RAYS 0      /* ray walk + brick hash insert + (ray, brick) pair emission */
+#define TSDF_K_OFFSETS 1   /* per-brick ray-list segments, pool slots, per-scan cell prefix */
+#define TSDF_K_SCATTER 2   /* pair -> per-brick scan-ordered ray list */
+#define TSDF_K_INTEGRATE 3 /* per-brick LDS tile accumulate + in-order fuse into the field */
 
 typedef struct tsdf_ctx tsdf_ctx;
 
@@ -96,16 +108,19 @@ const char* tsdf_last_error(const tsdf_ctx* ctx);
 /* One scan from host memory, in any PointCloud2-like layout: point i's x,y,z are at
  * (const char*)pts + i*point_step + xyz_offset, as three consecutive float32 (xyz_is_f64 = 0,
  * e.g. dlio::Point: point_step 32, xyz_offset 0) or float64 (xyz_is_f64 = 1).  origin is the
- * sensor position in the same (world) frame. */
+ * sensor position in the same (world) frame.  The points are copied before the call returns;
+ * the scan joins the pending batch (see Batching). */
 int tsdf_integrate(tsdf_ctx* ctx, const void* pts, uint64_t n, uint32_t point_step,
                    uint32_t xyz_offset, int32_t xyz_is_f64, const double origin[3]);
 
-/* One scan already in device memory: d_xyz = n packed float32 triplets (12 B per point). */
+/* One scan already in device memory: d_xyz = n packed float32 triplets (12 B per point).
+ * Launched at once as a batch of one (after flushing the pending host scans). */
 int tsdf_integrate_device(tsdf_ctx* ctx, const float* d_xyz, uint64_t n, const double origin[3]);
 
-/* n_scans scans in device memory, integrated in order.  Scan s is the points
- * d_xyz[3*scan_offsets[s] .. 3*scan_offsets[s+1]) (offsets in points, host array of n_scans+1)
- * seen from origins[3*s .. 3*s+3) (host array). */
+/* n_scans scans in device memory, integrated in order, max_batch scans per GPU batch.  Scan s is
+ * the points d_xyz[3*scan_offsets[s] .. 3*scan_offsets[s+1]) (offsets in points, host array of
+ * n_scans+1) seen from origins[3*s .. 3*s+3) (host array).  d_xyz must stay valid until the
+ * work completes (tsdf_sync). */
 int tsdf_integrate_batch_device(tsdf_ctx* ctx, const float* d_xyz, const uint64_t* scan_offsets,
                                 uint32_t n_scans, const double* origins);
 

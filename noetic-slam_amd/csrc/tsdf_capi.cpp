@@ -1,10 +1,11 @@
 // tsdf_capi.cpp — extern "C" boundary of libtsdf_hip.so (declared in include/tsdf_hip.h).
 //
 // One tsdf_ctx = one HIP device + one non-blocking stream + the brick hash table, brick pool and
-// per-scan work buffers, all allocated once at create (no allocation on the integrate path).  The
+// batch work buffers, all allocated once at create (no allocation on the integrate path).  The
 // host-pointer integrate packs the caller's PointCloud2-style records (any point_step/xyz_offset,
-// f32 or f64 xyz) into one of two pinned staging buffers, issues the H2D copy and the four kernels
-// on the stream and returns; tsdf_sync() waits and reports a deferred capacity overflow.
+// f32 or f64 xyz) into one of two pinned staging buffers, copies them into the device staging
+// area of the pending batch and returns; the batch is launched when max_batch scans are pending
+// or when any other call needs the field (see "Batching" in the header).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -20,6 +21,8 @@
 #include "tsdf_device.h"
 
 using namespace tsdf;
+
+static_assert(TSDF_MAX_BATCH == MAX_BATCH, "header and device batch limits differ");
 
 namespace {
 
@@ -85,21 +88,25 @@ uint64_t next_pow2(uint64_t v) {
 
 struct tsdf_ctx {
     tsdf_params p{};
-    int device = 0;
+    int device = -1;
     hipStream_t stream = nullptr;
+    RayConst R{};
     Table T{};
     Pool Pl{};
     Work Wk{};
     Globals* G = nullptr;
     uint64_t cap = 0;
-    uint64_t max_points = 0;
-    // host-pointer staging (double-buffered pinned memory + the device copy target)
+    uint64_t max_points = 0;  // per scan
+    uint32_t max_batch = 0;
+    uint64_t batch_points = 0;  // pair-slot capacity / maxp: points one batch may hold
+    // host-pointer path: pinned double buffer per scan + device staging of the pending batch
     float* h_stage[2] = {nullptr, nullptr};
     hipEvent_t stage_done[2] = {nullptr, nullptr};
-    float* d_stage[2] = {nullptr, nullptr};
     int stage_cur = 0;
-    uint64_t scan_id = 0;
-    uint64_t n_points_in = 0;
+    float* d_stage = nullptr;
+    BatchDesc pend{};  // pending host scans (points in d_stage)
+    uint64_t batch_id = 0;
+    uint64_t n_scans = 0, n_batches = 0, n_points_in = 0;
     EventTimer* timer = nullptr;
     std::string err;
 };
@@ -128,9 +135,33 @@ static uint32_t pairs_per_ray(const tsdf_params& p) {
     double band;  // band length in voxels along the ray
     if (p.space_carving) band = (p.max_range + p.sdf_trunc) / p.voxel_size;
     else band = 2.0 * p.sdf_trunc / p.voxel_size;
-    const double e = std::ceil(band) + 2.0;              // visited extent per axis, with margin
-    const double per_axis = std::floor((e + 1.0) / TSDF_BRICK_SIDE) + 1.0;  // boundary crossings
+    const double e = std::ceil(band) + 2.0;                                 // extent per axis
+    const double per_axis = std::floor((e + 1.0) / TSDF_BRICK_SIDE) + 1.0;  // crossings per axis
     return (uint32_t)(1.0 + 3.0 * per_axis);
+}
+
+// Launch one batch (desc offsets relative to d_xyz).
+static int launch(tsdf_ctx* c, const float* d_xyz, const BatchDesc& D) {
+    if (D.n_scans == 0) return TSDF_OK;
+    const int parity = (int)(c->batch_id & 1);
+    HIPCHK(c, launch_batch(d_xyz, D, c->R, c->T, c->Wk, c->Pl, c->G, parity, c->stream,
+                           c->timer));
+    c->batch_id++;
+    c->n_batches++;
+    c->n_scans += D.n_scans;
+    if (c->timer && c->timer->pending.size() > 8192) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        c->timer->harvest();
+    }
+    return TSDF_OK;
+}
+
+static int flush(tsdf_ctx* c) {
+    if (c->pend.n_scans == 0) return TSDF_OK;
+    const int rc = launch(c, c->d_stage, c->pend);
+    c->pend.n_scans = 0;
+    c->pend.off[0] = 0;
+    return rc;
 }
 
 extern "C" {
@@ -149,6 +180,7 @@ void tsdf_default_params(tsdf_params* p) {
     p->max_pairs = 0;
     p->device_id = 0;
     p->brick_side = TSDF_BRICK_SIDE;
+    p->max_batch = 32;
 }
 
 int tsdf_abi_version(void) { return TSDF_ABI_VERSION; }
@@ -157,12 +189,18 @@ const char* tsdf_last_error(const tsdf_ctx* c) { return c ? c->err.c_str() : "nu
 
 void tsdf_destroy(tsdf_ctx* c) {
     if (!c) return;
-    if (c->device >= 0) (void)hipSetDevice(c->device);
-    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->device >= 0) {
+        (void)hipSetDevice(c->device);
+        if (c->stream) {
+            (void)flush(c);
+            (void)hipStreamSynchronize(c->stream);
+        }
+    }
     delete c->timer;
-    void* dev[] = {c->T.keys, c->T.slots, c->T.cnt, c->T.toff, c->T.brick_keys, c->Pl.sdf,
-                   c->Pl.weight, c->Wk.pair_tidx, c->Wk.pair_local, c->Wk.ray_list, c->Wk.active,
-                   c->G, c->d_stage[0], c->d_stage[1]};
+    void* dev[] = {c->T.keys,        c->T.slots,         c->T.cnt,         c->T.toff,
+                   c->T.cell,        c->T.brick_keys,    c->Pl.sdf,        c->Pl.weight,
+                   c->Wk.pair_tidx,  c->Wk.pair_local,   c->Wk.ray_list,   c->Wk.active,
+                   c->G,             c->d_stage};
     for (void* d : dev)
         if (d) (void)hipFree(d);
     for (int i = 0; i < 2; i++) {
@@ -184,33 +222,45 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
 
+    c->R.vs = (float)p->voxel_size;
+    c->R.inv_vs = 1.0f / c->R.vs;
+    c->R.tau = (float)p->sdf_trunc;
+    c->R.min_range = (float)p->min_range;
+    c->R.max_range = (float)p->max_range;
+    c->R.carving = p->space_carving ? 1 : 0;
+
     const uint32_t maxp = pairs_per_ray(*p);
     c->max_points = p->max_points;
-    uint64_t slots = c->max_points * maxp;
+    c->max_batch = p->max_batch;
+    uint64_t slots = c->max_points * c->max_batch * maxp;
     if (p->max_pairs && p->max_pairs < slots) slots = p->max_pairs;  // caller-imposed cap
-    if (slots >= 0xFFFFFFF0ull || slots == 0)
-        return fail(c, TSDF_EINVAL, "max_points * pairs_per_ray = %llu out of range",
+    if (slots >= 0xFFFFFFF0ull || slots < maxp)
+        return fail(c, TSDF_EINVAL, "max_batch * max_points * pairs_per_ray = %llu out of range",
                     (unsigned long long)slots);
-    c->max_points = slots / maxp;
+    c->batch_points = slots / maxp;
+    if (c->max_points > c->batch_points) c->max_points = c->batch_points;
     c->cap = next_pow2(2 * p->max_bricks);
     c->T.mask = c->cap - 1;
     c->T.max_bricks = (uint32_t)p->max_bricks;
+    c->T.cell_stride = (c->max_batch + 3u) & ~3u;
     c->Wk.maxp = maxp;
+    c->Wk.max_active = (uint32_t)std::min<uint64_t>(c->cap, slots);
 
     HIPCHK(c, hipMalloc(&c->T.keys, c->cap * sizeof(uint64_t)));
     HIPCHK(c, hipMalloc(&c->T.slots, c->cap * sizeof(uint32_t)));
     HIPCHK(c, hipMalloc(&c->T.cnt, c->cap * sizeof(uint32_t)));
     HIPCHK(c, hipMalloc(&c->T.toff, c->cap * sizeof(uint32_t)));
+    HIPCHK(c, hipMalloc(&c->T.cell, c->cap * c->T.cell_stride * sizeof(uint32_t)));
     HIPCHK(c, hipMalloc(&c->T.brick_keys, p->max_bricks * sizeof(uint64_t)));
     HIPCHK(c, hipMalloc(&c->Pl.sdf, p->max_bricks * BRICK_VOX * sizeof(float)));
     HIPCHK(c, hipMalloc(&c->Pl.weight, p->max_bricks * BRICK_VOX * sizeof(float)));
     HIPCHK(c, hipMalloc(&c->Wk.pair_tidx, slots * sizeof(uint32_t)));
     HIPCHK(c, hipMalloc(&c->Wk.pair_local, slots * sizeof(uint32_t)));
     HIPCHK(c, hipMalloc(&c->Wk.ray_list, slots * sizeof(uint32_t)));
-    HIPCHK(c, hipMalloc(&c->Wk.active, slots * sizeof(uint32_t)));
+    HIPCHK(c, hipMalloc(&c->Wk.active, (size_t)c->Wk.max_active * sizeof(uint32_t)));
     HIPCHK(c, hipMalloc(&c->G, sizeof(Globals)));
+    HIPCHK(c, hipMalloc(&c->d_stage, c->batch_points * 3 * sizeof(float)));
     for (int i = 0; i < 2; i++) {
-        HIPCHK(c, hipMalloc(&c->d_stage[i], c->max_points * 3 * sizeof(float)));
         HIPCHK(c, hipHostMalloc(&c->h_stage[i], c->max_points * 3 * sizeof(float),
                                 hipHostMallocDefault));
         HIPCHK(c, hipEventCreateWithFlags(&c->stage_done[i], hipEventDisableTiming));
@@ -219,6 +269,8 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
     HIPCHK(c, launch_fill_u64(c->T.keys, EMPTY_KEY, c->cap, c->stream));
     HIPCHK(c, launch_fill_u32(c->T.slots, UNASSIGNED, c->cap, c->stream));
     HIPCHK(c, hipMemsetAsync(c->T.cnt, 0, c->cap * sizeof(uint32_t), c->stream));
+    HIPCHK(c, hipMemsetAsync(c->T.cell, 0, c->cap * c->T.cell_stride * sizeof(uint32_t),
+                             c->stream));
     HIPCHK(c, launch_fill(c->Pl.sdf, (float)p->sdf_trunc, p->max_bricks * BRICK_VOX, c->stream));
     HIPCHK(c, hipMemsetAsync(c->Pl.weight, 0, p->max_bricks * BRICK_VOX * sizeof(float),
                              c->stream));
@@ -233,12 +285,11 @@ int tsdf_create(const tsdf_params* p, tsdf_ctx** out) {
     if (!(p->voxel_size > 0) || !(p->sdf_trunc > 0) || p->brick_side != TSDF_BRICK_SIDE ||
         p->weight_mode != TSDF_WEIGHT_CONSTANT || p->max_bricks == 0 ||
         p->max_bricks >= 0xFFFFFFF0ull || p->max_points == 0 || !(p->min_range >= 0) ||
-        !(p->max_range > p->min_range))
+        !(p->max_range > p->min_range) || p->max_batch == 0 || p->max_batch > TSDF_MAX_BATCH)
         return TSDF_EINVAL;
     if (p->space_carving && !std::isfinite(p->max_range)) return TSDF_EINVAL;
     tsdf_ctx* c = new (std::nothrow) tsdf_ctx();
     if (!c) return TSDF_ENOMEM;
-    c->device = -1;
     const int rc = create_impl(c, p);
     if (rc != TSDF_OK) {
         fprintf(stderr, "tsdf_create: %s\n", c->err.c_str());
@@ -249,35 +300,10 @@ int tsdf_create(const tsdf_params* p, tsdf_ctx** out) {
     return TSDF_OK;
 }
 
-static ScanParams scan_params(const tsdf_ctx* c, const double origin[3]) {
-    ScanParams P;
-    P.vs = (float)c->p.voxel_size;
-    P.inv_vs = 1.0f / P.vs;
-    P.tau = (float)c->p.sdf_trunc;
-    P.min_range = (float)c->p.min_range;
-    P.max_range = (float)c->p.max_range;
-    P.ox = (float)origin[0];
-    P.oy = (float)origin[1];
-    P.oz = (float)origin[2];
-    P.carving = c->p.space_carving ? 1 : 0;
-    return P;
-}
-
-static int run_scan(tsdf_ctx* c, const float* d_xyz, uint64_t n, const double origin[3]) {
-    if (n > c->max_points)
-        return fail(c, TSDF_EINVAL, "scan of %llu points exceeds max_points %llu",
-                    (unsigned long long)n, (unsigned long long)c->max_points);
-    const ScanParams P = scan_params(c, origin);
-    const int parity = (int)(c->scan_id & 1);
-    HIPCHK(c, launch_scan(d_xyz, (uint32_t)n, P, c->T, c->Wk, c->Pl, c->G, parity, c->stream,
-                          c->timer));
-    c->scan_id++;
-    c->n_points_in += n;
-    if (c->timer && c->timer->pending.size() > 8192) {
-        HIPCHK(c, hipStreamSynchronize(c->stream));
-        c->timer->harvest();
-    }
-    return TSDF_OK;
+static void set_origin(BatchDesc& D, uint32_t s, const double o[3]) {
+    D.ox[s] = (float)o[0];
+    D.oy[s] = (float)o[1];
+    D.oz[s] = (float)o[2];
 }
 
 int tsdf_integrate(tsdf_ctx* c, const void* pts, uint64_t n, uint32_t point_step,
@@ -291,6 +317,10 @@ int tsdf_integrate(tsdf_ctx* c, const void* pts, uint64_t n, uint32_t point_step
         return fail(c, TSDF_EINVAL, "scan of %llu points exceeds max_points %llu",
                     (unsigned long long)n, (unsigned long long)c->max_points);
     HIPCHK(c, hipSetDevice(c->device));
+    if (c->pend.n_scans == c->max_batch || c->pend.off[c->pend.n_scans] + n > c->batch_points) {
+        const int rc = flush(c);
+        if (rc) return rc;
+    }
     const int b = c->stage_cur;
     c->stage_cur ^= 1;
     HIPCHK(c, hipEventSynchronize(c->stage_done[b]));  // previous copy out of this buffer is done
@@ -312,45 +342,89 @@ int tsdf_integrate(tsdf_ctx* c, const void* pts, uint64_t n, uint32_t point_step
             }
         }
     }
-    HIPCHK(c, hipMemcpyAsync(c->d_stage[b], h, n * 12, hipMemcpyHostToDevice, c->stream));
+    BatchDesc& D = c->pend;
+    const uint32_t s = D.n_scans;
+    if (n) {
+        HIPCHK(c, hipMemcpyAsync(c->d_stage + 3 * (uint64_t)D.off[s], h, n * 12,
+                                 hipMemcpyHostToDevice, c->stream));
+    }
     HIPCHK(c, hipEventRecord(c->stage_done[b], c->stream));
-    return run_scan(c, c->d_stage[b], n, origin);
-}
-
-int tsdf_integrate_device(tsdf_ctx* c, const float* d_xyz, uint64_t n, const double origin[3]) {
-    if (!c) return TSDF_EINVAL;
-    if ((!d_xyz && n) || !origin) return fail(c, TSDF_EINVAL, "null argument");
-    HIPCHK(c, hipSetDevice(c->device));
-    return run_scan(c, d_xyz, n, origin);
+    set_origin(D, s, origin);
+    D.off[s + 1] = D.off[s] + (uint32_t)n;
+    D.n_scans = s + 1;
+    c->n_points_in += n;
+    if (D.n_scans == c->max_batch) return flush(c);
+    return TSDF_OK;
 }
 
 int tsdf_integrate_batch_device(tsdf_ctx* c, const float* d_xyz, const uint64_t* offs,
                                 uint32_t n_scans, const double* origins) {
     if (!c) return TSDF_EINVAL;
     if (!offs || !origins || (!d_xyz && n_scans)) return fail(c, TSDF_EINVAL, "null argument");
-    HIPCHK(c, hipSetDevice(c->device));
     for (uint32_t s = 0; s < n_scans; s++) {
         if (offs[s + 1] < offs[s]) return fail(c, TSDF_EINVAL, "scan_offsets not monotone");
-        const int rc = run_scan(c, d_xyz + 3 * offs[s], offs[s + 1] - offs[s], origins + 3 * s);
-        if (rc != TSDF_OK) return rc;
+        if (offs[s + 1] - offs[s] > c->max_points)
+            return fail(c, TSDF_EINVAL, "scan %u of %llu points exceeds max_points %llu", s,
+                        (unsigned long long)(offs[s + 1] - offs[s]),
+                        (unsigned long long)c->max_points);
+    }
+    HIPCHK(c, hipSetDevice(c->device));
+    int rc = flush(c);
+    if (rc) return rc;
+    uint32_t s = 0;
+    while (s < n_scans) {
+        BatchDesc D;
+        D.n_scans = 0;
+        D.off[0] = 0;
+        const uint64_t b0 = offs[s];
+        while (s < n_scans && D.n_scans < c->max_batch &&
+               offs[s + 1] - b0 <= c->batch_points) {
+            set_origin(D, D.n_scans, origins + 3 * (uint64_t)s);
+            D.off[D.n_scans + 1] = (uint32_t)(offs[s + 1] - b0);
+            D.n_scans++;
+            s++;
+        }
+        rc = launch(c, d_xyz + 3 * b0, D);
+        if (rc) return rc;
+        c->n_points_in += D.off[D.n_scans];
     }
     return TSDF_OK;
+}
+
+int tsdf_integrate_device(tsdf_ctx* c, const float* d_xyz, uint64_t n, const double origin[3]) {
+    if (!c) return TSDF_EINVAL;
+    if ((!d_xyz && n) || !origin) return fail(c, TSDF_EINVAL, "null argument");
+    const uint64_t offs[2] = {0, n};
+    return tsdf_integrate_batch_device(c, d_xyz, offs, 1, origin);
 }
 
 int tsdf_sync(tsdf_ctx* c) {
     if (!c) return TSDF_EINVAL;
     HIPCHK(c, hipSetDevice(c->device));
+    const int rc = flush(c);
+    if (rc) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (c->timer) c->timer->harvest();
     uint32_t ovf = 0;
     HIPCHK(c, hipMemcpy(&ovf, &c->G->overflow, sizeof ovf, hipMemcpyDeviceToHost));
     if (ovf) {
         HIPCHK(c, hipMemset(&c->G->overflow, 0, sizeof ovf));
-        return fail(c, TSDF_ENOMEM, "capacity overflow (%s%s%s): updates were dropped",
-                    (ovf & OVF_TABLE) ? "hash table full " : "",
-                    (ovf & OVF_POOL) ? "brick pool exhausted " : "",
-                    (ovf & OVF_PAIRS) ? "ray brick-pair slots exceeded" : "");
+        return fail(c, TSDF_ENOMEM, "capacity overflow (%s%s%s%s): updates were dropped",
+                    (ovf & OVF_TABLE) ? "hash table full; " : "",
+                    (ovf & OVF_POOL) ? "brick pool exhausted; " : "",
+                    (ovf & OVF_PAIRS) ? "ray brick-pair slots exceeded; " : "",
+                    (ovf & OVF_ACTIVE) ? "active-brick list full" : "");
     }
+    return TSDF_OK;
+}
+
+// flush + drain, ignoring (but keeping) the overflow flag for read-out calls
+static int drain(tsdf_ctx* c) {
+    HIPCHK(c, hipSetDevice(c->device));
+    const int rc = flush(c);
+    if (rc) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->timer) c->timer->harvest();
     return TSDF_OK;
 }
 
@@ -364,8 +438,9 @@ int tsdf_query_dense(tsdf_ctx* c, const int32_t lo[3], const int32_t hi[3], floa
         dims[a] = hi[a] - lo[a];
     }
     const uint64_t total = (uint64_t)dims[0] * dims[1] * dims[2];
+    int rc = drain(c);
+    if (rc) return rc;
     if (!total) return TSDF_OK;
-    HIPCHK(c, hipSetDevice(c->device));
     float *ds = nullptr, *dw = nullptr;
     HIPCHK(c, hipMalloc(&ds, total * sizeof(float)));
     hipError_t e = hipMalloc(&dw, total * sizeof(float));
@@ -381,8 +456,9 @@ int tsdf_query_dense(tsdf_ctx* c, const int32_t lo[3], const int32_t hi[3], floa
 }
 
 static int pool_bricks(tsdf_ctx* c, uint64_t* n) {
+    const int rc = drain(c);
+    if (rc) return rc;
     uint32_t pc = 0;
-    HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, hipMemcpy(&pc, &c->G->pool_count, sizeof pc, hipMemcpyDeviceToHost));
     *n = std::min<uint64_t>(pc, c->p.max_bricks);
     return TSDF_OK;
@@ -390,14 +466,12 @@ static int pool_bricks(tsdf_ctx* c, uint64_t* n) {
 
 int tsdf_num_bricks(tsdf_ctx* c, uint64_t* n) {
     if (!c || !n) return TSDF_EINVAL;
-    HIPCHK(c, hipSetDevice(c->device));
     return pool_bricks(c, n);
 }
 
 int tsdf_export_bricks(tsdf_ctx* c, int32_t* coords, float* sdf, float* weight, uint64_t cap,
                        uint64_t* n_out) {
     if (!c || !n_out) return TSDF_EINVAL;
-    HIPCHK(c, hipSetDevice(c->device));
     uint64_t nb = 0;
     int rc = pool_bricks(c, &nb);
     if (rc) return rc;
@@ -455,7 +529,8 @@ int tsdf_import_bricks(tsdf_ctx* c, const int32_t* coords, const float* sdf, con
         if (std::adjacent_find(k.begin(), k.end()) != k.end())
             return fail(c, TSDF_EINVAL, "duplicate brick in import");
     }
-    HIPCHK(c, hipSetDevice(c->device));
+    int rc = drain(c);
+    if (rc) return rc;
     int32_t* dc = nullptr;
     float *ds = nullptr, *dw = nullptr;
     uint32_t* dt = nullptr;
@@ -480,17 +555,17 @@ int tsdf_import_bricks(tsdf_ctx* c, const int32_t* coords, const float* sdf, con
 
 int tsdf_get_stats(tsdf_ctx* c, tsdf_stats* out) {
     if (!c || !out) return TSDF_EINVAL;
-    HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    if (c->timer) c->timer->harvest();
+    const int rc = drain(c);
+    if (rc) return rc;
     Globals g;
     HIPCHK(c, hipMemcpy(&g, c->G, sizeof g, hipMemcpyDeviceToHost));
     std::memset(out, 0, sizeof *out);
-    out->n_scans = c->scan_id;
+    out->n_scans = c->n_scans;
+    out->n_batches = c->n_batches;
     out->n_points_in = c->n_points_in;
     out->n_bricks = std::min<uint64_t>(g.pool_count, c->p.max_bricks);
-    if (c->scan_id) {
-        const Counters& L = g.ctr[(c->scan_id - 1) & 1];
+    if (c->batch_id) {
+        const Counters& L = g.ctr[(c->batch_id - 1) & 1];
         out->n_active_last = L.n_active;
         for (int k = 0; k < 8; k++) {
             out->n_voxels_last += L.n_vox[k];
@@ -500,6 +575,7 @@ int tsdf_get_stats(tsdf_ctx* c, tsdf_stats* out) {
     for (int k = 0; k < 8; k++) {
         out->n_voxels_total += g.tot_vox[k];
         out->n_rays_total += g.tot_rays[k];
+        out->n_dirty_total += g.tot_dirty[k];
     }
     if (c->timer)
         for (int k = 0; k < KIND_N; k++) {
@@ -511,18 +587,20 @@ int tsdf_get_stats(tsdf_ctx* c, tsdf_stats* out) {
 
 int tsdf_reset_stats(tsdf_ctx* c) {
     if (!c) return TSDF_EINVAL;
-    HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    if (c->timer) { c->timer->harvest(); c->timer->reset(); }
-    HIPCHK(c, hipMemset(c->G->tot_vox, 0, sizeof(c->G->tot_vox) * 3));
+    const int rc = drain(c);
+    if (rc) return rc;
+    if (c->timer) c->timer->reset();
+    HIPCHK(c, hipMemset(c->G->tot_vox, 0, sizeof(c->G->tot_vox) * 4));
     c->n_points_in = 0;
+    c->n_scans = 0;
+    c->n_batches = 0;
     return TSDF_OK;
 }
 
 int tsdf_set_profiling(tsdf_ctx* c, int32_t on) {
     if (!c) return TSDF_EINVAL;
-    HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const int rc = drain(c);
+    if (rc) return rc;
     if (on && !c->timer) c->timer = new (std::nothrow) EventTimer();
     if (!on && c->timer) { delete c->timer; c->timer = nullptr; }
     return (on && !c->timer) ? TSDF_ENOMEM : TSDF_OK;

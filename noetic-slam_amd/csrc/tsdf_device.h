@@ -1,15 +1,21 @@
 // tsdf_device.h — device-side data layout shared by the kernels and the C-ABI host code.
 //
-// HBM layout (DESIGN.md §3):
+// The unit of GPU work is a BATCH of up to MAX_BATCH consecutive scans.  Ray
+// walking, brick allocation and bucketing do not depend on the field, so they run for every ray of
+// the batch at once; only the per-scan fuse has a cross-scan order, and k_integrate applies it scan
+// by scan inside each brick — bitwise the same field as integrating the scans one at a time.
+//
+// HBM layout:
 //   Table   open-addressing brick hash, capacity 2^k >= 2 * max_bricks, linear probing:
 //           keys[cap]  u64  packed brick coords (21 bits/axis, biased by 2^20); EMPTY = ~0
-//           slots[cap] u32  brick-pool slot (UNASSIGNED until the scan's compaction pass)
-//           cnt[cap]   u32  this scan's (ray, brick) pair count (zeroed by k_integrate)
-//           toff[cap]  u32  this scan's ray-list segment offset
+//           slots[cap] u32  brick-pool slot (UNASSIGNED until the batch's compaction pass)
+//           cnt[cap]   u32  this batch's (ray, brick) pair count          (zeroed by k_integrate)
+//           toff[cap]  u32  this batch's ray-list segment offset
+//           cell[cap * cell_stride] u32  per (brick, scan) pair counts, then their prefix
 //   Pool    sdf[max_bricks][512] f32, weight[max_bricks][512] f32 — voxel l = z*64 + y*8 + x;
 //           brick_keys[max_bricks] u64 (slot -> key, for export)
-//   Work    per-ray fixed pair slots: pair_tidx / pair_local[max_points * maxp] u32,
-//           ray_list[max_points * maxp] u32, active[max_points * maxp] u32
+//   Work    per-ray fixed pair slots (max_batch * max_points * maxp): pair_tidx, pair_local u32;
+//           ray_list u32 (same size); active u32 (bricks touched by the batch)
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -17,21 +23,31 @@
 namespace tsdf {
 
 constexpr uint64_t EMPTY_KEY = ~0ull;
-constexpr uint32_t UNASSIGNED = 0xFFFFFFFFu;  // table entry inserted, pool slot not yet given
+constexpr uint32_t UNASSIGNED = 0xFFFFFFFFu;    // table entry inserted, pool slot not yet given
 constexpr uint32_t INVALID_SLOT = 0xFFFFFFFEu;  // pool exhausted for this brick
 constexpr uint32_t NO_PAIR = 0xFFFFFFFFu;
 constexpr int BRICK_VOX = 512;
 constexpr int BRICK_COORD_BIAS = 1 << 20;
 constexpr int VOX_LIMIT = 1 << 23;  // |voxel index| < 2^23 on every axis (same as the oracle)
 constexpr int MAX_DDA_STEPS = 1 << 20;
+constexpr int MAX_BATCH = 64;            // scans per batch (pair_local packs the scan in 6 bits)
+constexpr uint32_t RANK_BITS = 25;       // pair rank inside its (brick, scan) cell
+constexpr uint32_t RANK_MASK = (1u << RANK_BITS) - 1;
 
 // overflow bits (sticky until tsdf_sync reads them)
-constexpr uint32_t OVF_TABLE = 1u, OVF_POOL = 2u, OVF_PAIRS = 4u;
+constexpr uint32_t OVF_TABLE = 1u, OVF_POOL = 2u, OVF_PAIRS = 4u, OVF_ACTIVE = 8u;
 
-struct ScanParams {
+// per-context constants of the ray model
+struct RayConst {
     float vs, inv_vs, tau, min_range, max_range;
-    float ox, oy, oz;  // sensor origin (world), fp32
     int carving;
+};
+
+// one batch: scan s = points [off[s], off[s+1]) seen from (ox[s], oy[s], oz[s]) (fp32)
+struct BatchDesc {
+    uint32_t n_scans;
+    uint32_t off[MAX_BATCH + 1];
+    float ox[MAX_BATCH], oy[MAX_BATCH], oz[MAX_BATCH];
 };
 
 struct Table {
@@ -39,9 +55,11 @@ struct Table {
     uint32_t* slots;
     uint32_t* cnt;
     uint32_t* toff;
+    uint32_t* cell;
     uint64_t* brick_keys;  // pool slot -> key
     uint64_t mask;
     uint32_t max_bricks;
+    uint32_t cell_stride;  // >= max_batch, multiple of 4
 };
 
 struct Pool {
@@ -51,21 +69,22 @@ struct Pool {
 
 struct Work {
     uint32_t* pair_tidx;
-    uint32_t* pair_local;
+    uint32_t* pair_local;  // bit 31..25: scan, 24..0: rank in the (brick, scan) cell
     uint32_t* ray_list;
     uint32_t* active;
-    uint32_t maxp;  // pair slots per ray
+    uint32_t maxp;        // pair slots per ray
+    uint32_t max_active;  // capacity of `active`
 };
 
-// per-scan counters, double-buffered by scan parity (k_rays zeroes the other set)
+// per-batch counters, double-buffered by batch parity (k_rays zeroes the other set)
 struct Counters {
     uint32_t n_active;
     uint32_t cursor;
-    uint32_t n_new;
-    uint32_t pad0;
-    unsigned long long n_vox[8];   // U_vox of this scan, sharded by blockIdx & 7
-    unsigned long long n_rays[8];  // valid rays of this scan
+    uint32_t pad0, pad1;
+    unsigned long long n_vox[8];   // sum over scans of U_vox, sharded by blockIdx & 7
+    unsigned long long n_rays[8];  // valid rays
     unsigned long long n_pairs[8];
+    unsigned long long n_dirty[8];  // distinct voxels updated by the batch
 };
 
 // persistent device globals (one allocation, zeroed at create)
@@ -77,6 +96,7 @@ struct Globals {
     unsigned long long tot_vox[8];  // running totals since the last stats reset (sharded)
     unsigned long long tot_rays[8];
     unsigned long long tot_pairs[8];
+    unsigned long long tot_dirty[8];
 };
 
 enum KernelKind { KIND_RAYS = 0, KIND_OFFSETS = 1, KIND_SCATTER = 2, KIND_INTEGRATE = 3, KIND_N = 4 };
@@ -88,9 +108,9 @@ struct KernelTimer {
     virtual ~KernelTimer() {}
 };
 
-hipError_t launch_scan(const float* d_xyz, uint32_t n, const ScanParams& P, const Table& T,
-                       const Work& Wk, const Pool& Pl, Globals* G, int parity, hipStream_t st,
-                       KernelTimer* timer);
+hipError_t launch_batch(const float* d_xyz, const BatchDesc& D, const RayConst& R, const Table& T,
+                        const Work& Wk, const Pool& Pl, Globals* G, int parity, hipStream_t st,
+                        KernelTimer* timer);
 hipError_t launch_query_dense(const Table& T, const Pool& Pl, const int lo[3], const int dims[3],
                               float bg, float* d_sdf, float* d_w, hipStream_t st);
 hipError_t launch_import(const Table& T, const Pool& Pl, const int32_t* d_coords, uint32_t n,

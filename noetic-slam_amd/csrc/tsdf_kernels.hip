@@ -1,25 +1,29 @@
 // tsdf_kernels.hip — gfx950 kernels of the TSDF integration hot path (MAP_BACKEND_IDX = 4).
 //
-// Per scan, four stream-ordered launches:
-//   k_rays      one lane per ray: range filter, DDA over the truncation band, brick find-or-insert
-//               (CAS on the open-addressing table), one (ray, brick) pair per distinct brick the ray
-//               updates, written to the ray's FIXED pair slots (no global counter); the pair's rank
-//               inside its brick comes from a per-brick atomicAdd (spread over ~31k addresses)
-//   k_compact   8 pair slots per lane, block-wide scans: the first pair of every brick makes the
-//               brick active (compacted active list), reserves its contiguous ray-list segment and,
-//               for a brick new to the map, its pool slot — 3 atomics per 8192 pair slots
-//   k_scatter   pair -> ray-list segment
-//   k_integrate one wave per active brick: 8^3 tile of (fixed-point sum, count) in LDS; the brick's
-//               rays re-walk their DDA and add their in-brick samples with LDS atomics; the wave then
-//               fuses the tile into the persistent (sdf, weight) brick, reading and writing only the
-//               voxels it updated
+// One launch sequence integrates a BATCH of up to 64 consecutive scans:
+//   k_rays      one lane per ray of every scan of the batch: range filter, DDA over the truncation
+//               band, and at every step where some lanes enter a new brick, a wave-level
+//               aggregation round: lanes with the same (brick, scan) elect a leader (ballot + shfl,
+//               no LDS), the leaders find-or-insert their brick in the open-addressing table and
+//               reserve their lanes' ranks with ONE atomicAdd per group on the brick count and one
+//               on the (brick, scan) cell count; every (ray, brick) pair goes to the ray's fixed pair
+//               slots.  Bricks first touched in the batch are listed in LDS and appended to the
+//               active list with one atomic per flush.
+//   k_compact   per active brick: block-wide scans give its contiguous ray-list segment, its pool
+//               slot if it is new, and the prefix of its per-scan cells (ray lists scan-ordered)
+//   k_scatter   pair -> ray list position (segment + cell prefix + rank)
+//   k_integrate one wave per active brick: the brick's (sdf, weight) live in the wave's registers
+//               (8 voxels per lane) for the whole batch; for each scan in order, the scan's rays
+//               re-walk their DDA and add their in-brick samples as exact fixed point into an LDS
+//               tile, then each lane fuses its own voxels — so each touched brick is read once
+//               and its dirty voxels written once per batch instead of once per scan.
 //
 // Semantics: VDBFusion's VDBVolume::Integrate, restated in oracle/tsdf_oracle.c, which is the
 // bit-exact CPU twin of this file's arithmetic.  Ray arithmetic is fp32 with contraction off
 // (-ffp-contract=off) and correctly rounded div/sqrt, so the voxel sequence, the gate and every
 // sample are the oracle's bits.  Per scan, the samples of a voxel are summed as exact 64-bit fixed
-// point (trunc(s * 2^32)) plus a count, so the fused result does not depend on lane, wave or atomic
-// order: the field is bitwise reproducible and bitwise equal to the oracle's.
+// point (trunc(s * 2^32)) plus a count, and fused in scan order, so the field does not depend on
+// lane, wave, atomic or batch composition: it is bitwise reproducible and equal to the oracle's.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -59,20 +63,20 @@ __device__ __forceinline__ void axis_init(float u, float s, float t0i, int v, fl
 }
 
 // Returns false when the ray is filtered out (zero/NaN length, outside [min_range, max_range]).
-__device__ __forceinline__ bool ray_init(const ScanParams& P, float px, float py, float pz,
-                                         RayState& r) {
-    const float dx = px - P.ox, dy = py - P.oy, dz = pz - P.oz;
+__device__ __forceinline__ bool ray_init(const RayConst& R, float ox, float oy, float oz, float px,
+                                         float py, float pz, RayState& r) {
+    const float dx = px - ox, dy = py - oy, dz = pz - oz;
     const float depth = __builtin_sqrtf(dx * dx + dy * dy + dz * dz);
     if (!(depth > 0.0f)) return false;
-    if (!(depth >= P.min_range) || !(depth <= P.max_range)) return false;
+    if (!(depth >= R.min_range) || !(depth <= R.max_range)) return false;
     const float ux = dx / depth, uy = dy / depth, uz = dz / depth;
-    const float t0 = P.carving ? 0.0f : depth - P.tau;
-    const float t1 = depth + P.tau;
-    const float t0i = t0 * P.inv_vs;
-    r.t1i = t1 * P.inv_vs;
-    const float sx = P.ox * P.inv_vs + ux * t0i;
-    const float sy = P.oy * P.inv_vs + uy * t0i;
-    const float sz = P.oz * P.inv_vs + uz * t0i;
+    const float t0 = R.carving ? 0.0f : depth - R.tau;
+    const float t1 = depth + R.tau;
+    const float t0i = t0 * R.inv_vs;
+    r.t1i = t1 * R.inv_vs;
+    const float sx = ox * R.inv_vs + ux * t0i;
+    const float sy = oy * R.inv_vs + uy * t0i;
+    const float sz = oz * R.inv_vs + uz * t0i;
     r.vx = (int)__builtin_floorf(sx);
     r.vy = (int)__builtin_floorf(sy);
     r.vz = (int)__builtin_floorf(sz);
@@ -86,35 +90,40 @@ __device__ __forceinline__ bool ray_init(const ScanParams& P, float px, float py
 }
 
 // ComputeSDF at the current voxel; true (and the truncated sample) when it passes sdf > -tau.
-__device__ __forceinline__ bool voxel_sample(const ScanParams& P, const RayState& r, float& s) {
+__device__ __forceinline__ bool voxel_sample(const RayConst& R, float ox, float oy, float oz,
+                                             const RayState& r, float& s) {
     if (!(r.vx > -VOX_LIMIT && r.vx < VOX_LIMIT && r.vy > -VOX_LIMIT && r.vy < VOX_LIMIT &&
           r.vz > -VOX_LIMIT && r.vz < VOX_LIMIT))
         return false;
-    const float cx = ((float)r.vx + 0.5f) * P.vs;
-    const float cy = ((float)r.vy + 0.5f) * P.vs;
-    const float cz = ((float)r.vz + 0.5f) * P.vs;
-    const float ax = cx - P.ox, ay = cy - P.oy, az = cz - P.oz;
+    const float cx = ((float)r.vx + 0.5f) * R.vs;
+    const float cy = ((float)r.vy + 0.5f) * R.vs;
+    const float cz = ((float)r.vz + 0.5f) * R.vs;
+    const float ax = cx - ox, ay = cy - oy, az = cz - oz;
     const float bx = r.px - cx, by = r.py - cy, bz = r.pz - cz;
     const float dist = __builtin_sqrtf(bx * bx + by * by + bz * bz);
     const float proj = ax * bx + ay * by + az * bz;
     if (!(proj > 0.0f || proj < 0.0f)) return false;
     const float sdf = proj > 0.0f ? dist : -dist;
-    if (!(sdf > -P.tau)) return false;
-    s = sdf < P.tau ? sdf : P.tau;
+    if (!(sdf > -R.tau)) return false;
+    s = sdf < R.tau ? sdf : R.tau;
     return true;
 }
 
 // One DDA step (math::MinIndex tie-break: equal entries resolve to the higher axis).
 // Returns false when the next entry time is past the band end.
+// Written with selects only: an axis index would make hipcc spill the state to scratch.
 __device__ __forceinline__ bool ray_step(RayState& r) {
-    int a;
-    if (r.tnx < r.tny) a = (r.tnx < r.tnz) ? 0 : 2;
-    else a = (r.tny < r.tnz) ? 1 : 2;
-    const float t = a == 0 ? r.tnx : (a == 1 ? r.tny : r.tnz);
+    const bool mx = (r.tnx < r.tny) && (r.tnx < r.tnz);  // == oracle: a = 0
+    const bool my = !mx && (r.tny < r.tnz);              // == oracle: a = 1
+    const bool mz = !mx && !my;                          // == oracle: a = 2 (ties -> higher)
+    const float t = mx ? r.tnx : (my ? r.tny : r.tnz);
     if (!(t <= r.t1i)) return false;
-    if (a == 0) { r.tnx += r.tdx; r.vx += r.sx; }
-    else if (a == 1) { r.tny += r.tdy; r.vy += r.sy; }
-    else { r.tnz += r.tdz; r.vz += r.sz; }
+    r.tnx = mx ? r.tnx + r.tdx : r.tnx;
+    r.tny = my ? r.tny + r.tdy : r.tny;
+    r.tnz = mz ? r.tnz + r.tdz : r.tnz;
+    r.vx += mx ? r.sx : 0;
+    r.vy += my ? r.sy : 0;
+    r.vz += mz ? r.sz : 0;
     return true;
 }
 
@@ -173,54 +182,158 @@ __device__ __forceinline__ Tv wave_sum(Tv v) {
     return v;
 }
 
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // ------------------------------------------------------------------------------------------------
 // k_rays
 
-__global__ __launch_bounds__(256) void k_rays(const float* __restrict__ xyz, uint32_t n,
-                                              ScanParams P, Table T, Work Wk, Globals* G,
+constexpr int ACT_LDS = 2048;  // block-local list of bricks first touched by this block
+
+__device__ __forceinline__ void push_active(uint32_t h, uint32_t* s_act, uint32_t* s_nact,
+                                            Counters* C, const Work& Wk, Globals* G) {
+    const uint32_t q = atomicAdd(s_nact, 1u);
+    if (q < (uint32_t)ACT_LDS) {
+        s_act[q] = h;
+    } else {  // LDS list full (only long carving rays get here): append directly
+        const uint32_t g = atomicAdd(&C->n_active, 1u);
+        if (g < Wk.max_active) Wk.active[g] = h;
+        else atomicOr(&G->overflow, OVF_ACTIVE);
+    }
+}
+
+// Block-wide flush of the LDS first-touch list (called by all threads, uniform).
+__device__ __forceinline__ void flush_active(uint32_t* s_act, uint32_t* s_nact, uint32_t* s_base,
+                                             Counters* C, const Work& Wk, Globals* G) {
+    __syncthreads();
+    const uint32_t n = min(*s_nact, (uint32_t)ACT_LDS);
+    if (n) {
+        if (threadIdx.x == 0) *s_base = atomicAdd(&C->n_active, n);
+        __syncthreads();
+        const uint32_t b = *s_base;
+        for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) {
+            if (b + j < Wk.max_active) Wk.active[b + j] = s_act[j];
+            else atomicOr(&G->overflow, OVF_ACTIVE);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) *s_nact = 0;
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void k_rays(const float* __restrict__ xyz, BatchDesc D,
+                                              RayConst R, Table T, Work Wk, Globals* G,
                                               int parity) {
+    __shared__ uint32_t s_off[MAX_BATCH + 1];
+    __shared__ float s_o[3][MAX_BATCH];
+    __shared__ uint32_t s_act[ACT_LDS];
+    __shared__ uint32_t s_nact, s_base;
     __shared__ unsigned long long red[2][4];
     Counters* C = &G->ctr[parity];
     if (blockIdx.x == 0 && threadIdx.x < sizeof(Counters) / 4)
-        reinterpret_cast<uint32_t*>(&G->ctr[parity ^ 1])[threadIdx.x] = 0u;  // next scan's set
+        reinterpret_cast<uint32_t*>(&G->ctr[parity ^ 1])[threadIdx.x] = 0u;  // next batch's set
+    const uint32_t ns = D.n_scans;
+    for (uint32_t j = threadIdx.x; j <= ns; j += blockDim.x) s_off[j] = D.off[j];
+    for (uint32_t j = threadIdx.x; j < ns; j += blockDim.x) {
+        s_o[0][j] = D.ox[j];
+        s_o[1][j] = D.oy[j];
+        s_o[2][j] = D.oz[j];
+    }
+    if (threadIdx.x == 0) s_nact = 0;
+    __syncthreads();
+    const uint32_t total = s_off[ns];
     const uint32_t maxp = Wk.maxp;
+    const int lane = threadIdx.x & 63;
     uint32_t valid = 0, npairs = 0;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    for (uint32_t base = blockIdx.x * blockDim.x; base < total; base += gridDim.x * blockDim.x) {
+        const uint32_t i = base + threadIdx.x;
+        const bool live = i < total;
+        uint32_t t = 0;  // scan of ray i: the largest t with off[t] <= i
+        if (live) {
+            uint32_t lo = 0, hi = ns;  // off[lo] <= i < off[hi]
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (s_off[mid] <= i) lo = mid;
+                else hi = mid;
+            }
+            t = lo;
+        }
+        const float ox = s_o[0][t], oy = s_o[1][t], oz = s_o[2][t];
+        RayState r;
+        bool walking = live && ray_init(R, ox, oy, oz, xyz[3 * (size_t)i], xyz[3 * (size_t)i + 1],
+                                        xyz[3 * (size_t)i + 2], r);
+        valid += walking ? 1u : 0u;
         uint32_t* pt = Wk.pair_tidx + (size_t)i * maxp;
         uint32_t* pl = Wk.pair_local + (size_t)i * maxp;
         uint32_t k = 0;
-        RayState r;
-        if (ray_init(P, xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2], r)) {
-            valid++;
-            uint64_t last = EMPTY_KEY;
-            for (int it = 0; it < MAX_DDA_STEPS; it++) {
+        uint64_t last = EMPTY_KEY;
+        int it = 0;
+        while (__any(walking)) {
+            bool emit = false;
+            uint64_t key = 0;
+            if (walking) {
                 float s;
-                if (voxel_sample(P, r, s)) {
-                    const uint64_t key = brick_key_of(r.vx, r.vy, r.vz);
+                if (voxel_sample(R, ox, oy, oz, r, s)) {
+                    key = brick_key_of(r.vx, r.vy, r.vz);
                     if (key != last) {
                         last = key;
-                        if (k < maxp) {
-                            const int64_t h = table_insert(T, key, &G->overflow);
-                            if (h >= 0) {
-                                pl[k] = atomicAdd(&T.cnt[h], 1u);
-                                pt[k] = (uint32_t)h;
-                                k++;
-                            }
-                        } else {
-                            atomicOr(&G->overflow, OVF_PAIRS);
-                        }
+                        if (k < maxp) emit = true;
+                        else atomicOr(&G->overflow, OVF_PAIRS);
                     }
                 }
-                if (!ray_step(r)) break;
             }
+            if (__ballot(emit)) {
+                // --- wave-level aggregation: one leader per distinct (brick, scan) ---
+                uint64_t pending = __ballot(emit);
+                int leader = lane;
+                uint32_t gcount = 0, myrank = 0;
+                while (pending) {
+                    const int ld = __ffsll((unsigned long long)pending) - 1;
+                    const uint64_t lk = __shfl(key, ld, 64);
+                    const uint32_t lt = __shfl(t, ld, 64);
+                    const uint64_t grp = __ballot(emit && key == lk && t == lt) & pending;
+                    if ((grp >> lane) & 1ull) {
+                        leader = ld;
+                        myrank = __popcll(grp & ((1ull << lane) - 1ull));
+                    }
+                    if (lane == ld) gcount = __popcll(grp);
+                    pending &= ~grp;
+                }
+                uint32_t hh = NO_PAIR, cbase = 0;
+                if (emit && leader == lane) {
+                    const int64_t hx = table_insert(T, key, &G->overflow);
+                    if (hx >= 0) {
+                        hh = (uint32_t)hx;
+                        const uint32_t c = atomicAdd(&T.cnt[hh], gcount);
+                        if (c == 0) push_active(hh, s_act, &s_nact, C, Wk, G);
+                        cbase = atomicAdd(&T.cell[(size_t)hh * T.cell_stride + t], gcount);
+                    }
+                }
+                const uint32_t h = __shfl(hh, leader, 64);
+                const uint32_t rank = __shfl(cbase, leader, 64) + myrank;
+                if (emit && h != NO_PAIR) {
+                    pt[k] = h;
+                    pl[k] = (t << RANK_BITS) | rank;
+                    k++;
+                }
+            }
+            if (walking) walking = ray_step(r) && (++it < MAX_DDA_STEPS);
         }
         npairs += k;
-        for (uint32_t j = k; j < maxp; j++) pt[j] = NO_PAIR;
+        if (live)
+            for (uint32_t j = k; j < maxp; j++) pt[j] = NO_PAIR;
+        __syncthreads();
+        if (s_nact > (uint32_t)ACT_LDS / 2)  // uniform: read after the barrier
+            flush_active(s_act, &s_nact, &s_base, C, Wk, G);
     }
+    flush_active(s_act, &s_nact, &s_base, C, Wk, G);
     // block-reduce the stats, one atomic per block on a shard picked by block index
     unsigned long long v = wave_sum<unsigned long long>(valid);
     unsigned long long q = wave_sum<unsigned long long>(npairs);
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int wid = threadIdx.x >> 6;
     if (lane == 0) { red[0][wid] = v; red[1][wid] = q; }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -238,75 +351,60 @@ __global__ __launch_bounds__(256) void k_rays(const float* __restrict__ xyz, uin
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_compact: active-brick list, ray-list segments and new pool slots, block-aggregated
+// k_compact: per active brick — ray-list segment, new pool slot, per-scan cell prefix
 
-constexpr int CMP_THREADS = 1024, CMP_ITEMS = 8, CMP_CHUNK = CMP_THREADS * CMP_ITEMS;
+constexpr int CMP_THREADS = 1024;
 
-__global__ __launch_bounds__(CMP_THREADS) void k_compact(uint32_t n_slots, Table T, Work Wk,
-                                                         Globals* G, int parity) {
-    __shared__ uint32_t s_a[16], s_c[16];
-    __shared__ uint32_t base_a, base_c, base_n;
-    Counters* C = &G->ctr[parity];
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t* s_w, uint32_t* total) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    for (uint32_t chunk = blockIdx.x * CMP_CHUNK; chunk < n_slots; chunk += gridDim.x * CMP_CHUNK) {
-        const uint32_t s0 = chunk + threadIdx.x * CMP_ITEMS;
-        uint32_t tid[CMP_ITEMS], cnt[CMP_ITEMS];
-        uint32_t fa = 0, fn = 0, fc = 0;  // first-pair flags, new-brick flags (bit per item), counts
+    uint32_t v = x;
 #pragma unroll
-        for (int j = 0; j < CMP_ITEMS; j++) {
-            const uint32_t s = s0 + j;
-            tid[j] = NO_PAIR;
-            cnt[j] = 0;
-            if (s < n_slots) {
-                const uint32_t h = Wk.pair_tidx[s];
-                if (h != NO_PAIR && Wk.pair_local[s] == 0u) {
-                    tid[j] = h;
-                    cnt[j] = T.cnt[h];
-                    fa += 1;
-                    fc += cnt[j];
-                    if (T.slots[h] == UNASSIGNED) fn |= 1u << j;
-                }
-            }
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(v, d, 64);
+        if (lane >= d) v += y;
+    }
+    if (lane == 63) s_w[wid] = v;
+    __syncthreads();
+    if (threadIdx.x < 16) {
+        uint32_t u = s_w[threadIdx.x];
+#pragma unroll
+        for (int d = 1; d < 16; d <<= 1) {
+            const uint32_t y = __shfl_up(u, d, 16);
+            if ((int)threadIdx.x >= d) u += y;
         }
-        const uint32_t nnew = __builtin_popcount(fn);
-        // block exclusive scan of (fa | nnew << 16) and fc
-        uint32_t x = fa | (nnew << 16), y = fc;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t xs = __shfl_up(x, d, 64), ys = __shfl_up(y, d, 64);
-            if (lane >= d) { x += xs; y += ys; }
-        }
-        if (lane == 63) { s_a[wid] = x; s_c[wid] = y; }
-        __syncthreads();
-        if (threadIdx.x < 16) {
-            uint32_t u = s_a[threadIdx.x], w = s_c[threadIdx.x];
-#pragma unroll
-            for (int d = 1; d < 16; d <<= 1) {
-                const uint32_t us = __shfl_up(u, d, 16), ws = __shfl_up(w, d, 16);
-                if ((int)threadIdx.x >= d) { u += us; w += ws; }
-            }
-            s_a[threadIdx.x] = u;
-            s_c[threadIdx.x] = w;
-            if (threadIdx.x == 15) {
-                base_a = (u & 0xFFFFu) ? atomicAdd(&C->n_active, u & 0xFFFFu) : 0u;
-                base_c = w ? atomicAdd(&C->cursor, w) : 0u;
-                base_n = (u >> 16) ? atomicAdd(&G->pool_count, u >> 16) : 0u;
-            }
+        s_w[threadIdx.x] = u;
+    }
+    __syncthreads();
+    *total = s_w[15];
+    const uint32_t r = v - x + (wid ? s_w[wid - 1] : 0u);
+    __syncthreads();
+    return r;
+}
+
+__global__ __launch_bounds__(CMP_THREADS) void k_compact(uint32_t n_scans, Table T, Work Wk,
+                                                         Globals* G, int parity) {
+    __shared__ uint32_t s_w[16];
+    __shared__ uint32_t base_c, base_n;
+    Counters* C = &G->ctr[parity];
+    const uint32_t n_active = min(C->n_active, Wk.max_active);
+    for (uint32_t chunk = blockIdx.x * CMP_THREADS; chunk < n_active;
+         chunk += gridDim.x * CMP_THREADS) {
+        const uint32_t a = chunk + threadIdx.x;
+        const uint32_t h = a < n_active ? Wk.active[a] : NO_PAIR;
+        const uint32_t n = h != NO_PAIR ? T.cnt[h] : 0u;
+        const uint32_t isnew = (h != NO_PAIR && T.slots[h] == UNASSIGNED) ? 1u : 0u;
+        uint32_t tot_c, tot_n;
+        const uint32_t ec = block_excl_scan(n, s_w, &tot_c);
+        const uint32_t en = block_excl_scan(isnew, s_w, &tot_n);
+        if (threadIdx.x == 0) {
+            base_c = tot_c ? atomicAdd(&C->cursor, tot_c) : 0u;
+            base_n = tot_n ? atomicAdd(&G->pool_count, tot_n) : 0u;
         }
         __syncthreads();
-        const uint32_t pa = x - (fa | (nnew << 16)) + (wid ? s_a[wid - 1] : 0u);
-        uint32_t ia = base_a + (pa & 0xFFFFu);
-        uint32_t in = base_n + (pa >> 16);
-        uint32_t ic = base_c + y - fc + (wid ? s_c[wid - 1] : 0u);
-#pragma unroll
-        for (int j = 0; j < CMP_ITEMS; j++) {
-            if (tid[j] == NO_PAIR) continue;
-            const uint32_t h = tid[j];
-            Wk.active[ia++] = h;
-            T.toff[h] = ic;
-            ic += cnt[j];
-            if (fn & (1u << j)) {
-                const uint32_t slot = in++;
+        if (h != NO_PAIR) {
+            T.toff[h] = base_c + ec;
+            if (isnew) {
+                const uint32_t slot = base_n + en;
                 if (slot < T.max_bricks) {
                     T.slots[h] = slot;
                     T.brick_keys[slot] = T.keys[h];
@@ -314,6 +412,18 @@ __global__ __launch_bounds__(CMP_THREADS) void k_compact(uint32_t n_slots, Table
                     T.slots[h] = INVALID_SLOT;
                     atomicOr(&G->overflow, OVF_POOL);
                 }
+            }
+            // exclusive prefix of the per-scan cell counts (cell_stride is a multiple of 4)
+            uint4* cp = reinterpret_cast<uint4*>(T.cell + (size_t)h * T.cell_stride);
+            uint32_t run = 0;
+            for (uint32_t q = 0; q < (n_scans + 3) / 4; q++) {
+                uint4 v = cp[q];
+                const uint32_t x0 = v.x, x1 = v.y, x2 = v.z, x3 = v.w;
+                v.x = run; run += x0;
+                v.y = run; run += x1;
+                v.z = run; run += x2;
+                v.w = run; run += x3;
+                cp[q] = v;
             }
         }
         __syncthreads();
@@ -329,92 +439,126 @@ __global__ __launch_bounds__(256) void k_scatter(uint32_t n_slots, Table T, Work
          s += gridDim.x * blockDim.x) {
         const uint32_t h = Wk.pair_tidx[s];
         if (h == NO_PAIR) continue;
-        Wk.ray_list[T.toff[h] + Wk.pair_local[s]] = s / maxp;
+        const uint32_t pk = Wk.pair_local[s];
+        const uint32_t t = pk >> RANK_BITS, r = pk & RANK_MASK;
+        Wk.ray_list[T.toff[h] + T.cell[(size_t)h * T.cell_stride + t] + r] = s / maxp;
     }
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_integrate: one wave per active brick, LDS tile, fused write-back
+// k_integrate: one wave per active brick; brick in registers, per-scan LDS tile, fused in order
 
 constexpr int INT_WAVES = 4;  // waves per 256-thread workgroup, one brick tile each
 
-__global__ __launch_bounds__(256) void k_integrate(const float* __restrict__ xyz, ScanParams P,
-                                                  Table T, Work Wk, Pool Pl, Globals* G,
-                                                  int parity) {
+__global__ __launch_bounds__(256) void k_integrate(const float* __restrict__ xyz, BatchDesc D,
+                                                  RayConst R, Table T, Work Wk, Pool Pl,
+                                                  Globals* G, int parity) {
     __shared__ unsigned long long tileA[INT_WAVES][BRICK_VOX];  // sum of trunc(s * 2^32)
     __shared__ uint32_t tileB[INT_WAVES][BRICK_VOX];            // sample count
     Counters* C = &G->ctr[parity];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     unsigned long long* A = tileA[wid];
     uint32_t* B = tileB[wid];
-    const uint32_t n_active = C->n_active;
-    uint32_t nvox = 0;
+    const uint32_t n_active = min(C->n_active, Wk.max_active);
+    const uint32_t ns = D.n_scans;
+#pragma unroll
+    for (int k = 0; k < BRICK_VOX / 64; k++) {
+        A[lane + 64 * k] = 0ull;
+        B[lane + 64 * k] = 0u;
+    }
+    wave_sync_lds();
+    uint32_t nvox = 0, ndirty = 0;
     for (uint32_t a = blockIdx.x * INT_WAVES + wid; a < n_active; a += gridDim.x * INT_WAVES) {
         const uint32_t h = Wk.active[a];
         const uint32_t slot = T.slots[h];
         const uint32_t n = T.cnt[h];
-        const uint32_t off = T.toff[h];
+        const uint32_t base = T.toff[h];
+        const uint32_t* cellp = T.cell + (size_t)h * T.cell_stride;
+        const uint32_t cs = (uint32_t)lane < ns ? cellp[lane] : n;  // start of scan `lane`'s rays
         const uint64_t key = T.keys[h];
         const int bx = (int)(key & 0x1FFFFF) - BRICK_COORD_BIAS;
         const int by = (int)((key >> 21) & 0x1FFFFF) - BRICK_COORD_BIAS;
         const int bz = (int)((key >> 42) & 0x1FFFFF) - BRICK_COORD_BIAS;
+        const bool has_slot = slot < T.max_bricks;
+        float* Sg = Pl.sdf + (size_t)(has_slot ? slot : 0) * BRICK_VOX;
+        float* Wg = Pl.weight + (size_t)(has_slot ? slot : 0) * BRICK_VOX;
+        float sv[BRICK_VOX / 64], wv[BRICK_VOX / 64];
 #pragma unroll
         for (int k = 0; k < BRICK_VOX / 64; k++) {
-            A[lane + 64 * k] = 0ull;
-            B[lane + 64 * k] = 0u;
+            sv[k] = has_slot ? Sg[lane + 64 * k] : R.tau;
+            wv[k] = has_slot ? Wg[lane + 64 * k] : 0.0f;
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        for (uint32_t j = lane; j < n; j += 64) {
-            const uint32_t i = Wk.ray_list[off + j];
-            RayState r;
-            if (!ray_init(P, xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2], r)) continue;
-            for (int it = 0; it < MAX_DDA_STEPS; it++) {
-                if ((r.vx >> 3) == bx && (r.vy >> 3) == by && (r.vz >> 3) == bz) {
-                    float s;
-                    if (voxel_sample(P, r, s)) {
-                        const int l = ((r.vz & 7) << 6) | ((r.vy & 7) << 3) | (r.vx & 7);
-                        const long long q = (long long)(s * 4294967296.0f);
-                        atomicAdd(&A[l], (unsigned long long)q);
-                        atomicAdd(&B[l], 1u);
+        uint32_t dirty = 0;
+        for (uint32_t t = 0; t < ns; t++) {
+            const uint32_t c0 = __shfl(cs, (int)t, 64);
+            const uint32_t c1 = __shfl(cs, (int)t + 1, 64);  // lane ns holds n
+            if (c0 == c1) continue;
+            const float ox = D.ox[t], oy = D.oy[t], oz = D.oz[t];
+            for (uint32_t j = c0 + lane; j < c1; j += 64) {
+                const size_t i = Wk.ray_list[base + j];
+                RayState r;
+                if (!ray_init(R, ox, oy, oz, xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2], r))
+                    continue;
+                for (int it = 0; it < MAX_DDA_STEPS; it++) {
+                    if ((r.vx >> 3) == bx && (r.vy >> 3) == by && (r.vz >> 3) == bz) {
+                        float s;
+                        if (voxel_sample(R, ox, oy, oz, r, s)) {
+                            const int l = ((r.vz & 7) << 6) | ((r.vy & 7) << 3) | (r.vx & 7);
+                            const long long q = (long long)(s * 4294967296.0f);
+                            atomicAdd(&A[l], (unsigned long long)q);
+                            atomicAdd(&B[l], 1u);
+                        }
                     }
+                    if (!ray_step(r)) break;
                 }
-                if (!ray_step(r)) break;
             }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (slot < T.max_bricks) {
-            float* S = Pl.sdf + (size_t)slot * BRICK_VOX;
-            float* W = Pl.weight + (size_t)slot * BRICK_VOX;
+            wave_sync_lds();
 #pragma unroll
             for (int k = 0; k < BRICK_VOX / 64; k++) {
                 const int l = lane + 64 * k;
                 const uint32_t b = B[l];
                 if (b) {
-                    const float s0 = S[l], w0 = W[l];
                     const float bf = (float)b;
                     const float af = (float)((double)(long long)A[l] * (1.0 / 4294967296.0));
-                    const float nw = w0 + bf;
-                    S[l] = (s0 * w0 + af) / nw;
-                    W[l] = nw;
+                    const float nw = wv[k] + bf;
+                    sv[k] = (sv[k] * wv[k] + af) / nw;
+                    wv[k] = nw;
+                    A[l] = 0ull;
+                    B[l] = 0u;
+                    dirty |= 1u << k;
                     nvox++;
                 }
             }
+            wave_sync_lds();
         }
-        if (lane == 0) T.cnt[h] = 0u;  // ready for the next scan
+        if (has_slot) {
+#pragma unroll
+            for (int k = 0; k < BRICK_VOX / 64; k++) {
+                if (dirty & (1u << k)) {
+                    Sg[lane + 64 * k] = sv[k];
+                    Wg[lane + 64 * k] = wv[k];
+                }
+            }
+        }
+        ndirty += __popc(dirty);
+        if (lane == 0) T.cnt[h] = 0u;  // ready for the next batch
+        if ((uint32_t)lane < ns) T.cell[(size_t)h * T.cell_stride + lane] = 0u;
     }
-    __shared__ unsigned long long red[INT_WAVES];
+    __shared__ unsigned long long red[2][INT_WAVES];
     const unsigned long long v = wave_sum<unsigned long long>(nvox);
-    if (lane == 0) red[wid] = v;
+    const unsigned long long d = wave_sum<unsigned long long>(ndirty);
+    if (lane == 0) { red[0][wid] = v; red[1][wid] = d; }
     __syncthreads();
     if (threadIdx.x == 0) {
-        const unsigned long long t = red[0] + red[1] + red[2] + red[3];
-        if (t) {
-            atomicAdd(&C->n_vox[blockIdx.x & 7], t);
-            atomicAdd(&G->tot_vox[blockIdx.x & 7], t);
+        const unsigned long long tv = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+        const unsigned long long td = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+        if (tv) {
+            atomicAdd(&C->n_vox[blockIdx.x & 7], tv);
+            atomicAdd(&G->tot_vox[blockIdx.x & 7], tv);
+        }
+        if (td) {
+            atomicAdd(&C->n_dirty[blockIdx.x & 7], td);
+            atomicAdd(&G->tot_dirty[blockIdx.x & 7], td);
         }
     }
 }
@@ -449,7 +593,7 @@ __global__ void k_query_dense(Table T, Pool Pl, int lo0, int lo1, int lo2, int n
     }
 }
 
-// Import is not on the hot path: per-brick slot claims use a plain atomicAdd + CAS.  Bricks in one
+// Import is not on the hot path: per-brick slot claims use a plain atomicAdd.  Bricks in one
 // import call are unique (checked on the host).
 __global__ void k_import_insert(Table T, const int32_t* __restrict__ coords, uint32_t n,
                                 uint32_t* __restrict__ tidx_out, Globals* G) {
@@ -512,22 +656,22 @@ static int grid_for(uint64_t items, int per_block, int cap) {
     return (int)(g < 1 ? 1 : (g > (uint64_t)cap ? (uint64_t)cap : g));
 }
 
-hipError_t launch_scan(const float* d_xyz, uint32_t n, const ScanParams& P, const Table& T,
-                       const Work& Wk, const Pool& Pl, Globals* G, int parity, hipStream_t st,
-                       KernelTimer* timer) {
-    const uint32_t n_slots = n * Wk.maxp;
+hipError_t launch_batch(const float* d_xyz, const BatchDesc& D, const RayConst& R, const Table& T,
+                        const Work& Wk, const Pool& Pl, Globals* G, int parity, hipStream_t st,
+                        KernelTimer* timer) {
+    const uint32_t total = D.off[D.n_scans];
+    const uint32_t n_slots = total * Wk.maxp;
     if (timer) timer->begin(KIND_RAYS, st);
-    k_rays<<<grid_for(n, 256, 8192), 256, 0, st>>>(d_xyz, n, P, T, Wk, G, parity);
+    k_rays<<<grid_for(total, 256, 2048), 256, 0, st>>>(d_xyz, D, R, T, Wk, G, parity);
     if (timer) timer->end(KIND_RAYS, st);
     if (timer) timer->begin(KIND_OFFSETS, st);
-    k_compact<<<grid_for(n_slots, CMP_CHUNK, 256), CMP_THREADS, 0, st>>>(n_slots, T, Wk, G,
-                                                                        parity);
+    k_compact<<<64, CMP_THREADS, 0, st>>>(D.n_scans, T, Wk, G, parity);
     if (timer) timer->end(KIND_OFFSETS, st);
     if (timer) timer->begin(KIND_SCATTER, st);
-    k_scatter<<<grid_for(n_slots, 256, 4096), 256, 0, st>>>(n_slots, T, Wk);
+    k_scatter<<<grid_for(n_slots, 256, 8192), 256, 0, st>>>(n_slots, T, Wk);
     if (timer) timer->end(KIND_SCATTER, st);
     if (timer) timer->begin(KIND_INTEGRATE, st);
-    k_integrate<<<1536, 256, 0, st>>>(d_xyz, P, T, Wk, Pl, G, parity);
+    k_integrate<<<1536, 256, 0, st>>>(d_xyz, D, R, T, Wk, Pl, G, parity);
     if (timer) timer->end(KIND_INTEGRATE, st);
     return hipGetLastError();
 }

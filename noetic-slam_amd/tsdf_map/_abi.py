@@ -32,6 +32,8 @@ class TsdfParams(C.Structure):
         ("max_pairs", C.c_uint64),
         ("device_id", C.c_int32),
         ("brick_side", C.c_int32),
+        ("max_batch", C.c_uint32),
+        ("reserved", C.c_uint32),
     ]
 
 
@@ -45,6 +47,8 @@ class TsdfStats(C.Structure):
         ("n_voxels_last", C.c_uint64),
         ("n_voxels_total", C.c_uint64),
         ("n_rays_total", C.c_uint64),
+        ("n_dirty_total", C.c_uint64),
+        ("n_batches", C.c_uint64),
         ("kernel_ms", C.c_double * 8),
         ("kernel_launches", C.c_uint64 * 8),
     ]
@@ -112,7 +116,7 @@ def default_params(lib=None, **kw):
         p.voxel_size, p.sdf_trunc, p.space_carving, p.weight_mode = 0.05, 0.15, 0, 0
         p.min_range, p.max_range = 0.0, math.inf
         p.max_bricks, p.max_points, p.max_pairs = 1 << 20, 1 << 18, 0
-        p.device_id, p.brick_side = 0, BRICK_SIDE
+        p.device_id, p.brick_side, p.max_batch = 0, BRICK_SIDE, 32
     for k, v in kw.items():
         if not hasattr(p, k):
             raise TypeError("unknown tsdf_params field %r" % k)

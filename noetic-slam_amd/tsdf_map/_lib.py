@@ -8,6 +8,8 @@ PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_DIR = os.path.join(PKG_ROOT, "lib")
 HIP_LIB = os.path.join(LIB_DIR, "libtsdf_hip.so")
 
+ABI_VERSION = 2  # TSDF_ABI_VERSION of include/tsdf_hip.h
+
 _hip = None
 
 
@@ -21,7 +23,7 @@ def load_hip_library(path=None):
         raise RuntimeError("libtsdf_hip.so not built (%s); run `python -c 'import __graft_entry__ "
                            "as g; g.build()'` or `make -C noetic-slam_amd/csrc`" % p)
     lib = _abi.declare(ctypes.CDLL(p))
-    if lib.tsdf_abi_version() != 1:
+    if lib.tsdf_abi_version() != ABI_VERSION:
         raise RuntimeError("libtsdf_hip.so ABI version mismatch")
     if path is None:
         _hip = lib

@@ -44,7 +44,8 @@ class TSDFVolume:
     """A sparse TSDF volume of 8^3-voxel bricks behind the C-ABI of `lib`."""
 
     def __init__(self, lib, voxel_size, sdf_trunc, space_carving=False, min_range=0.0,
-                 max_range=math.inf, max_bricks=1 << 20, max_points=1 << 18, device_id=0):
+                 max_range=math.inf, max_bricks=1 << 20, max_points=1 << 18, device_id=0,
+                 max_batch=32):
         self._lib = lib
         self._ctx = C.c_void_p()
         p = _abi.default_params(lib)
@@ -55,6 +56,7 @@ class TSDFVolume:
         p.max_range = float(max_range)
         p.max_bricks = int(max_bricks)
         p.max_points = int(max_points)
+        p.max_batch = int(max_batch)
         p.device_id = int(device_id)
         self.params = p
         rc = lib.tsdf_create(C.byref(p), C.byref(self._ctx))

@@ -165,6 +165,7 @@ void tsdf_default_params(tsdf_params* p) {
     p->max_pairs = 0;
     p->device_id = 0;
     p->brick_side = TSDF_BRICK_SIDE;
+    p->max_batch = 32; /* accepted for ABI parity; the oracle integrates scan by scan */
 }
 
 int tsdf_abi_version(void) { return TSDF_ABI_VERSION; }

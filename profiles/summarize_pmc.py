@@ -1,0 +1,41 @@
+"""Summarise rocprofv3 --pmc CSVs: mean counter value per dispatch for the tsdf kernels.
+
+FETCH_SIZE / WRITE_SIZE are in KiB.  On gfx950 FETCH_SIZE under-reports wide coalesced reads by 2x
+(MI355X_MICROARCH.md, HBM) — both the raw value and the x2-corrected read bytes are printed; the
+correction is exact only for 16-B/lane streaming reads, so it is an upper bound for this mix.
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def main(root):
+    vals = collections.defaultdict(lambda: collections.defaultdict(list))
+    for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                k = row.get("Kernel_Name", "")
+                if "tsdf::" not in k:
+                    continue
+                name = k.split("tsdf::")[1].split("(")[0]
+                vals[name][row["Counter_Name"]].append(float(row["Counter_Value"]))
+    out = {}
+    for kname in sorted(vals):
+        out[kname] = {c: sum(v) / len(v) for c, v in sorted(vals[kname].items())}
+        print(kname)
+        for c, v in sorted(out[kname].items()):
+            print("  %-24s %16.1f  (n=%d)" % (c, v, len(vals[kname][c])))
+        d = out[kname]
+        if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
+            print("  HBM bytes/launch: read %.1f MB (x2 corr %.1f MB), write %.1f MB" %
+                  (d["FETCH_SIZE"] * 1024 / 1e6, 2 * d["FETCH_SIZE"] * 1024 / 1e6,
+                   d["WRITE_SIZE"] * 1024 / 1e6))
+    with open(os.path.join(root, "summary.json"), "w") as fh:
+        json.dump(out, fh, indent=1)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc")

@@ -77,6 +77,43 @@ def test_scan_sequence_bitwise(sim):
     assert_bitwise(g, o)
 
 
+def test_batch_composition_is_invisible(sim):
+    """Scans integrated 1, 3 or 32 per GPU batch (host queue) and through the device batch API
+    give the same bits, equal to the oracle's scan-by-scan integration."""
+    import torch
+    scans = [(decimate(p, 4), o) for p, o in (sim.scan(k) for k in range(10))]
+    o = ora()
+    for p, org in scans:
+        o.integrate(p, org)
+    ref = o.export_voxels()
+    for mb in (1, 3, 32):
+        g = hip(max_batch=mb)
+        for p, org in scans:
+            g.integrate(p, org)
+        got = g.export_voxels()
+        st = g.stats()
+        assert st["n_batches"] == -(-10 // mb) and st["n_scans"] == 10
+        for x, y in zip(got, ref):
+            assert np.array_equal(x, y), mb
+    allp = np.concatenate([p for p, _ in scans])
+    offs = np.cumsum([0] + [p.shape[0] for p, _ in scans]).astype(np.uint64)
+    d = torch.from_numpy(allp).to("cuda:0")
+    torch.cuda.synchronize()
+    g = hip(max_batch=4)
+    g.integrate_batch_device(d.data_ptr(), offs, np.stack([org for _, org in scans]))
+    for x, y in zip(g.export_voxels(), ref):
+        assert np.array_equal(x, y)
+
+
+def test_queued_scans_flush_before_readout(sim):
+    """A query right after queued host scans sees them (the queue is flushed first)."""
+    p, org = sim.scan(0)
+    g = hip(max_batch=32)
+    g.integrate(decimate(p, 4), org)
+    assert g.num_bricks() > 0
+    assert g.stats()["n_scans"] == 1
+
+
 def test_golden_fixture(tmp_path):
     from conftest import GOLDEN
     import os
