@@ -99,6 +99,7 @@ struct tsdf_ctx {
     uint64_t max_points = 0;  // per scan
     uint32_t max_batch = 0;
     uint64_t batch_points = 0;  // pair-slot capacity / maxp: points one batch may hold
+    uint32_t max_blocks = 0;    // k_count / k_place workgroups one batch may need
     // host-pointer path: pinned double buffer per scan + device staging of the pending batch
     float* h_stage[2] = {nullptr, nullptr};
     hipEvent_t stage_done[2] = {nullptr, nullptr};
@@ -130,19 +131,28 @@ static int fail(tsdf_ctx* c, int code, const char* fmt, ...) {
             return fail((c), TSDF_EHIP, "%s failed: %s", #expr, hipGetErrorString(e_));      \
     } while (0)
 
-// pair slots per ray: the distinct bricks a DDA over a band of E voxels per axis can visit
+// Pair slots per ray: the distinct bricks a DDA over the band can visit.  A segment of length L
+// (voxels) covers at most E = floor(L) + 2 cells along an axis, E cells cross at most
+// floor((E - 1) / 8) + 1 brick boundaries, and a line crosses them monotonically, one axis per
+// step: 1 + 3 * crossings bricks.  (5 cm / 15 cm: 4.)  Exceeding it is reported (OVF_PAIRS).
 static uint32_t pairs_per_ray(const tsdf_params& p) {
     double band;  // band length in voxels along the ray
     if (p.space_carving) band = (p.max_range + p.sdf_trunc) / p.voxel_size;
     else band = 2.0 * p.sdf_trunc / p.voxel_size;
-    const double e = std::ceil(band) + 2.0;                                 // extent per axis
-    const double per_axis = std::floor((e + 1.0) / TSDF_BRICK_SIDE) + 1.0;  // crossings per axis
-    return (uint32_t)(1.0 + 3.0 * per_axis);
+    const double e = std::floor(band) + 2.0;
+    const double crossings = std::floor((e - 1.0) / TSDF_BRICK_SIDE) + 1.0;
+    return (uint32_t)(1.0 + 3.0 * crossings);
 }
 
-// Launch one batch (desc offsets relative to d_xyz).
-static int launch(tsdf_ctx* c, const float* d_xyz, const BatchDesc& D) {
+// Launch one batch (desc offsets relative to d_xyz); fills the workgroup prefix of D.
+static int launch(tsdf_ctx* c, const float* d_xyz, BatchDesc& D) {
     if (D.n_scans == 0) return TSDF_OK;
+    D.blk[0] = 0;
+    for (uint32_t s = 0; s < D.n_scans; s++)
+        D.blk[s + 1] = D.blk[s] + (D.off[s + 1] - D.off[s] + RPB - 1) / RPB;
+    D.n_blocks = D.blk[D.n_scans];
+    if (D.n_blocks > c->max_blocks)
+        return fail(c, TSDF_EINVAL, "batch needs %u workgroups > %u", D.n_blocks, c->max_blocks);
     const int parity = (int)(c->batch_id & 1);
     HIPCHK(c, launch_batch(d_xyz, D, c->R, c->T, c->Wk, c->Pl, c->G, parity, c->stream,
                            c->timer));
@@ -198,8 +208,10 @@ void tsdf_destroy(tsdf_ctx* c) {
     }
     delete c->timer;
     void* dev[] = {c->T.keys,        c->T.slots,         c->T.cnt,         c->T.toff,
+                   c->T.touched,
                    c->T.cell,        c->T.brick_keys,    c->Pl.sdf,        c->Pl.weight,
-                   c->Wk.pair_tidx,  c->Wk.pair_local,   c->Wk.ray_list,   c->Wk.active,
+                   c->Wk.pair,       c->Wk.blk,          c->Wk.blk_occ,    c->Wk.fb,
+                   c->Wk.rec,        c->Wk.active,
                    c->G,             c->d_stage};
     for (void* d : dev)
         if (d) (void)hipFree(d);
@@ -245,18 +257,26 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
     c->T.cell_stride = (c->max_batch + 3u) & ~3u;
     c->Wk.maxp = maxp;
     c->Wk.max_active = (uint32_t)std::min<uint64_t>(c->cap, slots);
+    c->Wk.max_rec = (uint32_t)slots;
+    // fallback pairs (a workgroup's LDS brick hash is full): rare without carving, the rule with it
+    c->Wk.max_fb = (uint32_t)(p->space_carving ? slots : std::max<uint64_t>(slots / 16, 1u << 20));
+    c->max_blocks = (uint32_t)(c->batch_points / RPB + MAX_BATCH + 1);
 
     HIPCHK(c, hipMalloc(&c->T.keys, c->cap * sizeof(uint64_t)));
     HIPCHK(c, hipMalloc(&c->T.slots, c->cap * sizeof(uint32_t)));
     HIPCHK(c, hipMalloc(&c->T.cnt, c->cap * sizeof(uint32_t)));
     HIPCHK(c, hipMalloc(&c->T.toff, c->cap * sizeof(uint32_t)));
+    HIPCHK(c, hipMalloc(&c->T.touched, c->cap * sizeof(uint32_t)));
+    HIPCHK(c, hipMemsetAsync(c->T.touched, 0, c->cap * sizeof(uint32_t), c->stream));
     HIPCHK(c, hipMalloc(&c->T.cell, c->cap * c->T.cell_stride * sizeof(uint32_t)));
     HIPCHK(c, hipMalloc(&c->T.brick_keys, p->max_bricks * sizeof(uint64_t)));
     HIPCHK(c, hipMalloc(&c->Pl.sdf, p->max_bricks * BRICK_VOX * sizeof(float)));
     HIPCHK(c, hipMalloc(&c->Pl.weight, p->max_bricks * BRICK_VOX * sizeof(float)));
-    HIPCHK(c, hipMalloc(&c->Wk.pair_tidx, slots * sizeof(uint32_t)));
-    HIPCHK(c, hipMalloc(&c->Wk.pair_local, slots * sizeof(uint32_t)));
-    HIPCHK(c, hipMalloc(&c->Wk.ray_list, slots * sizeof(uint32_t)));
+    HIPCHK(c, hipMalloc(&c->Wk.pair, slots * sizeof(uint32_t)));
+    HIPCHK(c, hipMalloc(&c->Wk.blk, (size_t)c->max_blocks * HCAP * sizeof(uint2)));
+    HIPCHK(c, hipMalloc(&c->Wk.blk_occ, (size_t)c->max_blocks * (HCAP / 32) * sizeof(uint32_t)));
+    HIPCHK(c, hipMalloc(&c->Wk.fb, (size_t)c->Wk.max_fb * sizeof(uint4)));
+    HIPCHK(c, hipMalloc(&c->Wk.rec, slots * sizeof(float4)));
     HIPCHK(c, hipMalloc(&c->Wk.active, (size_t)c->Wk.max_active * sizeof(uint32_t)));
     HIPCHK(c, hipMalloc(&c->G, sizeof(Globals)));
     HIPCHK(c, hipMalloc(&c->d_stage, c->batch_points * 3 * sizeof(float)));

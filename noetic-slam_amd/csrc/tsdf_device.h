@@ -9,13 +9,18 @@
 //   Table   open-addressing brick hash, capacity 2^k >= 2 * max_bricks, linear probing:
 //           keys[cap]  u64  packed brick coords (21 bits/axis, biased by 2^20); EMPTY = ~0
 //           slots[cap] u32  brick-pool slot (UNASSIGNED until the batch's compaction pass)
-//           cnt[cap]   u32  this batch's (ray, brick) pair count          (zeroed by k_integrate)
-//           toff[cap]  u32  this batch's ray-list segment offset
+//           cnt[cap]   u32  this batch's (ray, brick) pair count (written by k_compact)
+//           toff[cap]  u32  this batch's ray-record segment offset
+//           touched[cap] u32  1 if the batch touches the brick (k_count sets, k_compact clears)
 //           cell[cap * cell_stride] u32  per (brick, scan) pair counts, then their prefix
 //   Pool    sdf[max_bricks][512] f32, weight[max_bricks][512] f32 — voxel l = z*64 + y*8 + x;
 //           brick_keys[max_bricks] u64 (slot -> key, for export)
-//   Work    per-ray fixed pair slots (max_batch * max_points * maxp): pair_tidx, pair_local u32;
-//           ray_list u32 (same size); active u32 (bricks touched by the batch)
+//   Work    pair[max_batch_points * maxp] u32    per-ray pair codes (see PAIR_*)
+//           blk[n_blocks * HCAP] uint2          per-block local brick table (tidx, cell base)
+//           fb[..] uint4                        fallback pairs (block's LDS hash full)
+//           rec[pairs] float4                   per-brick, scan-ordered ray records:
+//                                               (x, y, z, in-brick sample count)
+//           active[..] u32                      bricks touched by the batch
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -30,12 +35,21 @@ constexpr int BRICK_VOX = 512;
 constexpr int BRICK_COORD_BIAS = 1 << 20;
 constexpr int VOX_LIMIT = 1 << 23;  // |voxel index| < 2^23 on every axis (same as the oracle)
 constexpr int MAX_DDA_STEPS = 1 << 20;
-constexpr int MAX_BATCH = 64;            // scans per batch (pair_local packs the scan in 6 bits)
-constexpr uint32_t RANK_BITS = 25;       // pair rank inside its (brick, scan) cell
-constexpr uint32_t RANK_MASK = (1u << RANK_BITS) - 1;
+constexpr int MAX_BATCH = 64;          // scans per batch
+constexpr int RPB = 1024;              // rays per k_count / k_place block (one scan per block)
+constexpr int HCAP = 2048;             // LDS brick-hash slots per k_count block (~300-800 used)
+constexpr int LDS_PROBES = 64;         // probe limit before a pair takes the global fallback
+constexpr int MAX_IN_BRICK = 22;       // a line visits at most 8+8+8-2 voxels of an 8^3 brick
+
+// pair codes (one u32 per (ray, k-th brick) slot)
+//   local:    bit 31 = 0 | count << 26 | lid << 10 | lrank   (lid < HCAP, lrank < RPB)
+//   fallback: bit 31 = 1 | count << 26 | fb index            (fb index < 2^26)
+//   none:     NO_PAIR
+constexpr uint32_t PAIR_FB = 0x80000000u;
+constexpr int PAIR_CNT_SHIFT = 26;
 
 // overflow bits (sticky until tsdf_sync reads them)
-constexpr uint32_t OVF_TABLE = 1u, OVF_POOL = 2u, OVF_PAIRS = 4u, OVF_ACTIVE = 8u;
+constexpr uint32_t OVF_TABLE = 1u, OVF_POOL = 2u, OVF_PAIRS = 4u, OVF_ACTIVE = 8u, OVF_FB = 16u;
 
 // per-context constants of the ray model
 struct RayConst {
@@ -43,10 +57,13 @@ struct RayConst {
     int carving;
 };
 
-// one batch: scan s = points [off[s], off[s+1]) seen from (ox[s], oy[s], oz[s]) (fp32)
+// one batch: scan s = points [off[s], off[s+1]) seen from (ox[s], oy[s], oz[s]) (fp32);
+// k_count / k_place blocks [blk[s], blk[s+1]) cover scan s, RPB rays each
 struct BatchDesc {
     uint32_t n_scans;
+    uint32_t n_blocks;
     uint32_t off[MAX_BATCH + 1];
+    uint32_t blk[MAX_BATCH + 1];
     float ox[MAX_BATCH], oy[MAX_BATCH], oz[MAX_BATCH];
 };
 
@@ -55,6 +72,7 @@ struct Table {
     uint32_t* slots;
     uint32_t* cnt;
     uint32_t* toff;
+    uint32_t* touched;  // set (plain store) by k_count for every brick the batch touches
     uint32_t* cell;
     uint64_t* brick_keys;  // pool slot -> key
     uint64_t mask;
@@ -68,21 +86,26 @@ struct Pool {
 };
 
 struct Work {
-    uint32_t* pair_tidx;
-    uint32_t* pair_local;  // bit 31..25: scan, 24..0: rank in the (brick, scan) cell
-    uint32_t* ray_list;
+    uint32_t* pair;
+    uint2* blk;      // n_blocks * HCAP
+    uint32_t* blk_occ;  // n_blocks * HCAP/32 occupancy bits
+    uint4* fb;       // fallback pairs: (tidx, scan, rank, 0)
+    float4* rec;
     uint32_t* active;
     uint32_t maxp;        // pair slots per ray
     uint32_t max_active;  // capacity of `active`
+    uint32_t max_fb;      // capacity of `fb`
+    uint32_t max_rec;     // capacity of `rec`
 };
 
-// per-batch counters, double-buffered by batch parity (k_rays zeroes the other set)
+// per-batch counters, double-buffered by batch parity (k_count zeroes the other set)
 struct Counters {
     uint32_t n_active;
     uint32_t cursor;
-    uint32_t pad0, pad1;
-    unsigned long long n_vox[8];   // sum over scans of U_vox, sharded by blockIdx & 7
-    unsigned long long n_rays[8];  // valid rays
+    uint32_t n_fb;
+    uint32_t pad0;
+    unsigned long long n_vox[8];    // sum over scans of U_vox, sharded by blockIdx & 7
+    unsigned long long n_rays[8];   // valid rays
     unsigned long long n_pairs[8];
     unsigned long long n_dirty[8];  // distinct voxels updated by the batch
 };
@@ -99,7 +122,7 @@ struct Globals {
     unsigned long long tot_dirty[8];
 };
 
-enum KernelKind { KIND_RAYS = 0, KIND_OFFSETS = 1, KIND_SCATTER = 2, KIND_INTEGRATE = 3, KIND_N = 4 };
+enum KernelKind { KIND_COUNT = 0, KIND_COMPACT = 1, KIND_PLACE = 2, KIND_INTEGRATE = 3, KIND_N = 4 };
 
 // Optional per-kernel HIP-event timing (profiling mode); implemented in tsdf_capi.cpp.
 struct KernelTimer {

@@ -1,22 +1,24 @@
 // tsdf_kernels.hip — gfx950 kernels of the TSDF integration hot path (MAP_BACKEND_IDX = 4).
 //
 // One launch sequence integrates a BATCH of up to 64 consecutive scans:
-//   k_rays      one lane per ray of every scan of the batch: range filter, DDA over the truncation
-//               band, and at every step where some lanes enter a new brick, a wave-level
-//               aggregation round: lanes with the same (brick, scan) elect a leader (ballot + shfl,
-//               no LDS), the leaders find-or-insert their brick in the open-addressing table and
-//               reserve their lanes' ranks with ONE atomicAdd per group on the brick count and one
-//               on the (brick, scan) cell count; every (ray, brick) pair goes to the ray's fixed pair
-//               slots.  Bricks first touched in the batch are listed in LDS and appended to the
-//               active list with one atomic per flush.
-//   k_compact   per active brick: block-wide scans give its contiguous ray-list segment, its pool
-//               slot if it is new, and the prefix of its per-scan cells (ray lists scan-ordered)
-//   k_scatter   pair -> ray list position (segment + cell prefix + rank)
-//   k_integrate one wave per active brick: the brick's (sdf, weight) live in the wave's registers
-//               (8 voxels per lane) for the whole batch; for each scan in order, the scan's rays
-//               re-walk their DDA and add their in-brick samples as exact fixed point into an LDS
-//               tile, then each lane fuses its own voxels — so each touched brick is read once
-//               and its dirty voxels written once per batch instead of once per scan.
+//   k_count     one workgroup per 1024 consecutive rays of one scan: every lane walks its rays' DDA
+//               over the truncation band; each distinct brick a ray updates goes into the
+//               workgroup's LDS hash (one LDS CAS + one LDS atomicAdd per (ray, brick) pair, which
+//               also gives the pair its rank).  Then one lane per distinct brick finds-or-inserts it
+//               in the global open-addressing table and reserves the workgroup's ranks with ONE
+//               atomicAdd on the brick's pair count and one on its (brick, scan) cell — global
+//               atomics per distinct brick per workgroup instead of per pair.
+//   k_compact   per active brick: block-wide scans give its contiguous ray-record segment, its pool
+//               slot if it is new, and the prefix of its per-scan cells (records scan-ordered)
+//   k_place     same workgroups as k_count: coalesced read of the rays, one record
+//               (x, y, z, in-brick sample count) written per pair to its brick segment
+//   k_integrate one wave per active brick: the brick's (sdf, weight) live in registers (8 voxels
+//               per lane) for the whole batch.  The brick's records are read 64 at a time
+//               (coalesced); every lane walks its ray and writes its in-brick samples to an LDS
+//               buffer (positions from a wave prefix of the counts); then, for each scan of the
+//               chunk in order, the scan's samples are added as exact fixed point into an LDS tile
+//               and — once the scan is complete — each lane fuses its own voxels.  Each touched
+//               brick is read once and its dirty voxels written once per batch.
 //
 // Semantics: VDBFusion's VDBVolume::Integrate, restated in oracle/tsdf_oracle.c, which is the
 // bit-exact CPU twin of this file's arithmetic.  Ray arithmetic is fp32 with contraction off
@@ -189,156 +191,151 @@ __device__ __forceinline__ void wave_sync_lds() {
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_rays
+// shared helpers of the batch kernels
 
-constexpr int ACT_LDS = 2048;  // block-local list of bricks first touched by this block
-
-__device__ __forceinline__ void push_active(uint32_t h, uint32_t* s_act, uint32_t* s_nact,
-                                            Counters* C, const Work& Wk, Globals* G) {
-    const uint32_t q = atomicAdd(s_nact, 1u);
-    if (q < (uint32_t)ACT_LDS) {
-        s_act[q] = h;
-    } else {  // LDS list full (only long carving rays get here): append directly
-        const uint32_t g = atomicAdd(&C->n_active, 1u);
-        if (g < Wk.max_active) Wk.active[g] = h;
-        else atomicOr(&G->overflow, OVF_ACTIVE);
+// Scan and ray range of k_count / k_place workgroup b (uniform: scalar loads of the descriptor).
+__device__ __forceinline__ void block_range(const BatchDesc& D, uint32_t b, uint32_t& t,
+                                            uint32_t& r0, uint32_t& r1) {
+    uint32_t lo = 0, hi = D.n_scans;  // blk[lo] <= b < blk[hi]
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (D.blk[mid] <= b) lo = mid;
+        else hi = mid;
     }
+    t = lo;
+    r0 = D.off[t] + (b - D.blk[t]) * RPB;
+    r1 = min(D.off[t + 1], r0 + RPB);
 }
 
-// Block-wide flush of the LDS first-touch list (called by all threads, uniform).
-__device__ __forceinline__ void flush_active(uint32_t* s_act, uint32_t* s_nact, uint32_t* s_base,
-                                             Counters* C, const Work& Wk, Globals* G) {
-    __syncthreads();
-    const uint32_t n = min(*s_nact, (uint32_t)ACT_LDS);
-    if (n) {
-        if (threadIdx.x == 0) *s_base = atomicAdd(&C->n_active, n);
-        __syncthreads();
-        const uint32_t b = *s_base;
-        for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) {
-            if (b + j < Wk.max_active) Wk.active[b + j] = s_act[j];
-            else atomicOr(&G->overflow, OVF_ACTIVE);
+// LDS brick hash of one k_count workgroup: slot index of key (inserted if new), -1 when no slot
+// is found within LDS_PROBES probes (the pair then takes the global fallback).
+__device__ __forceinline__ int lds_insert(unsigned long long* s_key, uint64_t key) {
+    uint32_t hs = (uint32_t)(mix64(key) >> 40) & (HCAP - 1);
+    for (int p = 0; p < LDS_PROBES; p++) {
+        const unsigned long long k = s_key[hs];
+        if (k == key) return (int)hs;
+        if (k == EMPTY_KEY) {
+            const unsigned long long old = atomicCAS(&s_key[hs], EMPTY_KEY, key);
+            if (old == EMPTY_KEY || old == key) return (int)hs;
         }
+        hs = (hs + 1) & (HCAP - 1);
     }
-    __syncthreads();
-    if (threadIdx.x == 0) *s_nact = 0;
-    __syncthreads();
+    return -1;
 }
 
-__global__ __launch_bounds__(256) void k_rays(const float* __restrict__ xyz, BatchDesc D,
-                                              RayConst R, Table T, Work Wk, Globals* G,
-                                              int parity) {
-    __shared__ uint32_t s_off[MAX_BATCH + 1];
-    __shared__ float s_o[3][MAX_BATCH];
-    __shared__ uint32_t s_act[ACT_LDS];
-    __shared__ uint32_t s_nact, s_base;
-    __shared__ unsigned long long red[2][4];
+// ------------------------------------------------------------------------------------------------
+// k_count
+
+constexpr int CNT_THREADS = 256;
+
+__global__ __launch_bounds__(CNT_THREADS) void k_count(const float* __restrict__ xyz, BatchDesc D,
+                                                      RayConst R, Table T, Work Wk, Globals* G,
+                                                      int parity) {
+    __shared__ unsigned long long s_key[HCAP];
+    __shared__ uint32_t s_cnt[HCAP];
+    __shared__ uint32_t s_occ[HCAP / 32];
+    __shared__ unsigned long long red[2][CNT_THREADS / 64];
     Counters* C = &G->ctr[parity];
     if (blockIdx.x == 0 && threadIdx.x < sizeof(Counters) / 4)
         reinterpret_cast<uint32_t*>(&G->ctr[parity ^ 1])[threadIdx.x] = 0u;  // next batch's set
-    const uint32_t ns = D.n_scans;
-    for (uint32_t j = threadIdx.x; j <= ns; j += blockDim.x) s_off[j] = D.off[j];
-    for (uint32_t j = threadIdx.x; j < ns; j += blockDim.x) {
-        s_o[0][j] = D.ox[j];
-        s_o[1][j] = D.oy[j];
-        s_o[2][j] = D.oz[j];
+    for (int j = threadIdx.x; j < HCAP; j += CNT_THREADS) {
+        s_key[j] = EMPTY_KEY;
+        s_cnt[j] = 0u;
     }
-    if (threadIdx.x == 0) s_nact = 0;
+    if (threadIdx.x < HCAP / 32) s_occ[threadIdx.x] = 0u;
     __syncthreads();
-    const uint32_t total = s_off[ns];
+    uint32_t t, r0, r1;
+    block_range(D, blockIdx.x, t, r0, r1);
+    const float ox = D.ox[t], oy = D.oy[t], oz = D.oz[t];
     const uint32_t maxp = Wk.maxp;
-    const int lane = threadIdx.x & 63;
     uint32_t valid = 0, npairs = 0;
-    for (uint32_t base = blockIdx.x * blockDim.x; base < total; base += gridDim.x * blockDim.x) {
-        const uint32_t i = base + threadIdx.x;
-        const bool live = i < total;
-        uint32_t t = 0;  // scan of ray i: the largest t with off[t] <= i
-        if (live) {
-            uint32_t lo = 0, hi = ns;  // off[lo] <= i < off[hi]
-            while (hi - lo > 1) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (s_off[mid] <= i) lo = mid;
-                else hi = mid;
-            }
-            t = lo;
-        }
-        const float ox = s_o[0][t], oy = s_o[1][t], oz = s_o[2][t];
-        RayState r;
-        bool walking = live && ray_init(R, ox, oy, oz, xyz[3 * (size_t)i], xyz[3 * (size_t)i + 1],
-                                        xyz[3 * (size_t)i + 2], r);
-        valid += walking ? 1u : 0u;
-        uint32_t* pt = Wk.pair_tidx + (size_t)i * maxp;
-        uint32_t* pl = Wk.pair_local + (size_t)i * maxp;
+    for (uint32_t i = r0 + threadIdx.x; i < r1; i += CNT_THREADS) {
+        uint32_t* pc = Wk.pair + (size_t)i * maxp;
         uint32_t k = 0;
-        uint64_t last = EMPTY_KEY;
-        int it = 0;
-        while (__any(walking)) {
-            bool emit = false;
-            uint64_t key = 0;
-            if (walking) {
+        RayState r;
+        if (ray_init(R, ox, oy, oz, xyz[3 * (size_t)i], xyz[3 * (size_t)i + 1],
+                     xyz[3 * (size_t)i + 2], r)) {
+            valid++;
+            // One pair per distinct brick; a line visits a brick in one contiguous run of DDA
+            // voxels, so the pair is closed when the next gated voxel's brick differs.  cnt_in =
+            // the pair's gated voxels (<= MAX_IN_BRICK), sizes k_integrate's sample buffer.
+            auto emit = [&](uint64_t bkey, uint32_t cnt_in) {
+                if (k >= maxp) {
+                    atomicOr(&G->overflow, OVF_PAIRS);
+                    return;
+                }
+                const int lid = lds_insert(s_key, bkey);
+                if (lid >= 0) {
+                    const uint32_t lr = atomicAdd(&s_cnt[lid], 1u);  // < RPB: one pair per ray
+                    pc[k++] = (cnt_in << PAIR_CNT_SHIFT) | ((uint32_t)lid << 10) | lr;
+                    return;
+                }
+                // LDS hash full: this pair takes the global path
+                const uint32_t f = atomicAdd(&C->n_fb, 1u);
+                if (f >= Wk.max_fb) {
+                    atomicOr(&G->overflow, OVF_FB);
+                    return;
+                }
+                const int64_t hx = table_insert(T, bkey, &G->overflow);
+                if (hx < 0) return;
+                const uint32_t h = (uint32_t)hx;
+                T.touched[h] = 1u;
+                const uint32_t rk = atomicAdd(&T.cell[(size_t)h * T.cell_stride + t], 1u);
+                Wk.fb[f] = make_uint4(h, t, rk, 0u);
+                pc[k++] = PAIR_FB | (cnt_in << PAIR_CNT_SHIFT) | f;
+            };
+            uint64_t cur = EMPTY_KEY;
+            uint32_t ccount = 0;
+            for (int it = 0; it < MAX_DDA_STEPS; it++) {
                 float s;
                 if (voxel_sample(R, ox, oy, oz, r, s)) {
-                    key = brick_key_of(r.vx, r.vy, r.vz);
-                    if (key != last) {
-                        last = key;
-                        if (k < maxp) emit = true;
-                        else atomicOr(&G->overflow, OVF_PAIRS);
+                    const uint64_t key = brick_key_of(r.vx, r.vy, r.vz);
+                    if (key != cur) {
+                        if (cur != EMPTY_KEY) emit(cur, ccount);
+                        cur = key;
+                        ccount = 0;
                     }
+                    ccount++;
                 }
+                if (!ray_step(r)) break;
             }
-            if (__ballot(emit)) {
-                // --- wave-level aggregation: one leader per distinct (brick, scan) ---
-                uint64_t pending = __ballot(emit);
-                int leader = lane;
-                uint32_t gcount = 0, myrank = 0;
-                while (pending) {
-                    const int ld = __ffsll((unsigned long long)pending) - 1;
-                    const uint64_t lk = __shfl(key, ld, 64);
-                    const uint32_t lt = __shfl(t, ld, 64);
-                    const uint64_t grp = __ballot(emit && key == lk && t == lt) & pending;
-                    if ((grp >> lane) & 1ull) {
-                        leader = ld;
-                        myrank = __popcll(grp & ((1ull << lane) - 1ull));
-                    }
-                    if (lane == ld) gcount = __popcll(grp);
-                    pending &= ~grp;
-                }
-                uint32_t hh = NO_PAIR, cbase = 0;
-                if (emit && leader == lane) {
-                    const int64_t hx = table_insert(T, key, &G->overflow);
-                    if (hx >= 0) {
-                        hh = (uint32_t)hx;
-                        const uint32_t c = atomicAdd(&T.cnt[hh], gcount);
-                        if (c == 0) push_active(hh, s_act, &s_nact, C, Wk, G);
-                        cbase = atomicAdd(&T.cell[(size_t)hh * T.cell_stride + t], gcount);
-                    }
-                }
-                const uint32_t h = __shfl(hh, leader, 64);
-                const uint32_t rank = __shfl(cbase, leader, 64) + myrank;
-                if (emit && h != NO_PAIR) {
-                    pt[k] = h;
-                    pl[k] = (t << RANK_BITS) | rank;
-                    k++;
-                }
-            }
-            if (walking) walking = ray_step(r) && (++it < MAX_DDA_STEPS);
+            if (cur != EMPTY_KEY) emit(cur, ccount);
         }
         npairs += k;
-        if (live)
-            for (uint32_t j = k; j < maxp; j++) pt[j] = NO_PAIR;
-        __syncthreads();
-        if (s_nact > (uint32_t)ACT_LDS / 2)  // uniform: read after the barrier
-            flush_active(s_act, &s_nact, &s_base, C, Wk, G);
+        for (uint32_t j = k; j < maxp; j++) pc[j] = NO_PAIR;
     }
-    flush_active(s_act, &s_nact, &s_base, C, Wk, G);
+    __syncthreads();
+    // one global find-or-insert + one atomic per distinct brick of the workgroup: the cell
+    // (brick, scan) count reserves the workgroup's ranks; `touched` (a plain store) lists the brick
+    // for k_compact, which also derives the brick's total from its cells
+    uint2* bt = Wk.blk + (size_t)blockIdx.x * HCAP;
+    for (int slot = threadIdx.x; slot < HCAP; slot += CNT_THREADS) {
+        const uint64_t key = s_key[slot];
+        if (key == EMPTY_KEY) continue;
+        const uint32_t n = s_cnt[slot];
+        const int64_t hx = table_insert(T, key, &G->overflow);
+        uint2 e = make_uint2(NO_PAIR, 0u);
+        if (hx >= 0) {
+            const uint32_t h = (uint32_t)hx;
+            T.touched[h] = 1u;
+            e = make_uint2(h, atomicAdd(&T.cell[(size_t)h * T.cell_stride + t], n));
+        }
+        bt[slot] = e;
+        atomicOr(&s_occ[slot >> 5], 1u << (slot & 31));
+    }
+    __syncthreads();
+    if (threadIdx.x < HCAP / 32) Wk.blk_occ[(size_t)blockIdx.x * (HCAP / 32) + threadIdx.x] =
+        s_occ[threadIdx.x];
     // block-reduce the stats, one atomic per block on a shard picked by block index
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     unsigned long long v = wave_sum<unsigned long long>(valid);
     unsigned long long q = wave_sum<unsigned long long>(npairs);
-    const int wid = threadIdx.x >> 6;
     if (lane == 0) { red[0][wid] = v; red[1][wid] = q; }
     __syncthreads();
     if (threadIdx.x == 0) {
-        v = red[0][0] + red[0][1] + red[0][2] + red[0][3];
-        q = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+        v = 0;
+        q = 0;
+        for (int w = 0; w < CNT_THREADS / 64; w++) { v += red[0][w]; q += red[1][w]; }
         if (v) {
             atomicAdd(&C->n_rays[blockIdx.x & 7], v);
             atomicAdd(&G->tot_rays[blockIdx.x & 7], v);
@@ -351,7 +348,7 @@ __global__ __launch_bounds__(256) void k_rays(const float* __restrict__ xyz, Bat
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_compact: per active brick — ray-list segment, new pool slot, per-scan cell prefix
+// k_compact: per active brick — record segment, new pool slot, per-scan cell prefix
 
 constexpr int CMP_THREADS = 1024;
 
@@ -381,27 +378,50 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t* s_w, u
     return r;
 }
 
+// Sweeps the `touched` words of the whole table (coalesced, cap * 4 B) — cheaper than any
+// per-brick first-touch atomic in k_count.  For each touched brick: its per-scan cell counts
+// become their exclusive prefix (and their sum its pair count), it gets its record segment, a pool
+// slot if it is new, and an active-list entry; three atomics per CMP_THREADS table entries.
 __global__ __launch_bounds__(CMP_THREADS) void k_compact(uint32_t n_scans, Table T, Work Wk,
                                                          Globals* G, int parity) {
     __shared__ uint32_t s_w[16];
-    __shared__ uint32_t base_c, base_n;
+    __shared__ uint32_t base_a, base_c, base_n;
     Counters* C = &G->ctr[parity];
-    const uint32_t n_active = min(C->n_active, Wk.max_active);
-    for (uint32_t chunk = blockIdx.x * CMP_THREADS; chunk < n_active;
+    const uint32_t cap = (uint32_t)(T.mask + 1);
+    for (uint32_t chunk = blockIdx.x * CMP_THREADS; chunk < cap;
          chunk += gridDim.x * CMP_THREADS) {
-        const uint32_t a = chunk + threadIdx.x;
-        const uint32_t h = a < n_active ? Wk.active[a] : NO_PAIR;
-        const uint32_t n = h != NO_PAIR ? T.cnt[h] : 0u;
-        const uint32_t isnew = (h != NO_PAIR && T.slots[h] == UNASSIGNED) ? 1u : 0u;
-        uint32_t tot_c, tot_n;
+        const uint32_t h = chunk + threadIdx.x;
+        const bool hit = T.touched[h] != 0u;
+        uint32_t n = 0, isnew = 0;
+        if (hit) {
+            T.touched[h] = 0u;
+            isnew = T.slots[h] == UNASSIGNED ? 1u : 0u;
+            // exclusive prefix of the per-scan cell counts (cell_stride is a multiple of 4)
+            uint4* cp = reinterpret_cast<uint4*>(T.cell + (size_t)h * T.cell_stride);
+            for (uint32_t q = 0; q < (n_scans + 3) / 4; q++) {
+                uint4 v = cp[q];
+                const uint32_t x0 = v.x, x1 = v.y, x2 = v.z, x3 = v.w;
+                v.x = n; n += x0;
+                v.y = n; n += x1;
+                v.z = n; n += x2;
+                v.w = n; n += x3;
+                cp[q] = v;
+            }
+            T.cnt[h] = n;
+        }
+        uint32_t tot_a, tot_c, tot_n;
+        const uint32_t ea = block_excl_scan(hit ? 1u : 0u, s_w, &tot_a);
         const uint32_t ec = block_excl_scan(n, s_w, &tot_c);
         const uint32_t en = block_excl_scan(isnew, s_w, &tot_n);
         if (threadIdx.x == 0) {
+            base_a = tot_a ? atomicAdd(&C->n_active, tot_a) : 0u;
             base_c = tot_c ? atomicAdd(&C->cursor, tot_c) : 0u;
             base_n = tot_n ? atomicAdd(&G->pool_count, tot_n) : 0u;
         }
         __syncthreads();
-        if (h != NO_PAIR) {
+        if (hit) {
+            if (base_a + ea < Wk.max_active) Wk.active[base_a + ea] = h;
+            else atomicOr(&G->overflow, OVF_ACTIVE);
             T.toff[h] = base_c + ec;
             if (isnew) {
                 const uint32_t slot = base_n + en;
@@ -413,152 +433,213 @@ __global__ __launch_bounds__(CMP_THREADS) void k_compact(uint32_t n_scans, Table
                     atomicOr(&G->overflow, OVF_POOL);
                 }
             }
-            // exclusive prefix of the per-scan cell counts (cell_stride is a multiple of 4)
-            uint4* cp = reinterpret_cast<uint4*>(T.cell + (size_t)h * T.cell_stride);
-            uint32_t run = 0;
-            for (uint32_t q = 0; q < (n_scans + 3) / 4; q++) {
-                uint4 v = cp[q];
-                const uint32_t x0 = v.x, x1 = v.y, x2 = v.z, x3 = v.w;
-                v.x = run; run += x0;
-                v.y = run; run += x1;
-                v.z = run; run += x2;
-                v.w = run; run += x3;
-                cp[q] = v;
-            }
         }
         __syncthreads();
     }
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_scatter: pair -> ray list
+// k_place: ray records into the bricks' scan-ordered segments
 
-__global__ __launch_bounds__(256) void k_scatter(uint32_t n_slots, Table T, Work Wk) {
+__global__ __launch_bounds__(CNT_THREADS) void k_place(const float* __restrict__ xyz, BatchDesc D,
+                                                      Table T, Work Wk) {
+    __shared__ uint32_t s_base[HCAP];
+    uint32_t t, r0, r1;
+    block_range(D, blockIdx.x, t, r0, r1);
+    const uint2* bt = Wk.blk + (size_t)blockIdx.x * HCAP;
+    const uint32_t* occ = Wk.blk_occ + (size_t)blockIdx.x * (HCAP / 32);
+    for (int slot = threadIdx.x; slot < HCAP; slot += CNT_THREADS) {
+        uint32_t b = NO_PAIR;
+        if ((occ[slot >> 5] >> (slot & 31)) & 1u) {
+            const uint2 e = bt[slot];
+            if (e.x != NO_PAIR)
+                b = T.toff[e.x] + T.cell[(size_t)e.x * T.cell_stride + t] + e.y;
+        }
+        s_base[slot] = b;
+    }
+    __syncthreads();
     const uint32_t maxp = Wk.maxp;
-    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < n_slots;
-         s += gridDim.x * blockDim.x) {
-        const uint32_t h = Wk.pair_tidx[s];
-        if (h == NO_PAIR) continue;
-        const uint32_t pk = Wk.pair_local[s];
-        const uint32_t t = pk >> RANK_BITS, r = pk & RANK_MASK;
-        Wk.ray_list[T.toff[h] + T.cell[(size_t)h * T.cell_stride + t] + r] = s / maxp;
+    for (uint32_t i = r0 + threadIdx.x; i < r1; i += CNT_THREADS) {
+        const uint32_t* pc = Wk.pair + (size_t)i * maxp;
+        const float px = xyz[3 * (size_t)i], py = xyz[3 * (size_t)i + 1],
+                    pz = xyz[3 * (size_t)i + 2];
+        for (uint32_t k = 0; k < maxp; k++) {
+            const uint32_t code = pc[k];
+            if (code == NO_PAIR) break;
+            const uint32_t cnt_in = (code >> PAIR_CNT_SHIFT) & 31u;
+            uint32_t pos;
+            if (code & PAIR_FB) {
+                const uint4 f = Wk.fb[code & ((1u << PAIR_CNT_SHIFT) - 1u)];
+                pos = T.toff[f.x] + T.cell[(size_t)f.x * T.cell_stride + f.y] + f.z;
+            } else {
+                const uint32_t b = s_base[(code >> 10) & (HCAP - 1)];
+                if (b == NO_PAIR) continue;
+                pos = b + (code & 1023u);
+            }
+            if (pos < Wk.max_rec) Wk.rec[pos] = make_float4(px, py, pz, __uint_as_float(cnt_in));
+        }
     }
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_integrate: one wave per active brick; brick in registers, per-scan LDS tile, fused in order
+// k_integrate: one wave per active brick; brick in registers, samples and tile in LDS
 
-constexpr int INT_WAVES = 4;  // waves per 256-thread workgroup, one brick tile each
+constexpr int SBUF = 64 * MAX_IN_BRICK;
 
-__global__ __launch_bounds__(256) void k_integrate(const float* __restrict__ xyz, BatchDesc D,
-                                                  RayConst R, Table T, Work Wk, Pool Pl,
-                                                  Globals* G, int parity) {
-    __shared__ unsigned long long tileA[INT_WAVES][BRICK_VOX];  // sum of trunc(s * 2^32)
-    __shared__ uint32_t tileB[INT_WAVES][BRICK_VOX];            // sample count
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t x, int lane) {
+    uint32_t v = x;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(v, d, 64);
+        if (lane >= d) v += y;
+    }
+    return v - x;
+}
+
+__global__ __launch_bounds__(64) void k_integrate(BatchDesc D, RayConst R, Table T, Work Wk,
+                                                 Pool Pl, Globals* G, int parity) {
+    __shared__ __attribute__((aligned(16))) unsigned long long A[BRICK_VOX];  // sum trunc(s*2^32)
+    __shared__ __attribute__((aligned(16))) uint32_t B[BRICK_VOX];            // sample count
+    __shared__ float smp_s[SBUF];
+    __shared__ uint16_t smp_l[SBUF];
     Counters* C = &G->ctr[parity];
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    unsigned long long* A = tileA[wid];
-    uint32_t* B = tileB[wid];
+    const int lane = threadIdx.x;
+    const int l0 = lane * 8;  // this lane owns voxels l0 .. l0 + 7
     const uint32_t n_active = min(C->n_active, Wk.max_active);
     const uint32_t ns = D.n_scans;
 #pragma unroll
-    for (int k = 0; k < BRICK_VOX / 64; k++) {
-        A[lane + 64 * k] = 0ull;
-        B[lane + 64 * k] = 0u;
+    for (int k = 0; k < 8; k++) {
+        A[l0 + k] = 0ull;
+        B[l0 + k] = 0u;
     }
     wave_sync_lds();
     uint32_t nvox = 0, ndirty = 0;
-    for (uint32_t a = blockIdx.x * INT_WAVES + wid; a < n_active; a += gridDim.x * INT_WAVES) {
+    for (uint32_t a = blockIdx.x; a < n_active; a += gridDim.x) {
         const uint32_t h = Wk.active[a];
         const uint32_t slot = T.slots[h];
         const uint32_t n = T.cnt[h];
         const uint32_t base = T.toff[h];
-        const uint32_t* cellp = T.cell + (size_t)h * T.cell_stride;
-        const uint32_t cs = (uint32_t)lane < ns ? cellp[lane] : n;  // start of scan `lane`'s rays
+        const uint32_t cs = (uint32_t)lane < ns ? T.cell[(size_t)h * T.cell_stride + lane] : n;
         const uint64_t key = T.keys[h];
         const int bx = (int)(key & 0x1FFFFF) - BRICK_COORD_BIAS;
         const int by = (int)((key >> 21) & 0x1FFFFF) - BRICK_COORD_BIAS;
         const int bz = (int)((key >> 42) & 0x1FFFFF) - BRICK_COORD_BIAS;
         const bool has_slot = slot < T.max_bricks;
-        float* Sg = Pl.sdf + (size_t)(has_slot ? slot : 0) * BRICK_VOX;
-        float* Wg = Pl.weight + (size_t)(has_slot ? slot : 0) * BRICK_VOX;
-        float sv[BRICK_VOX / 64], wv[BRICK_VOX / 64];
-#pragma unroll
-        for (int k = 0; k < BRICK_VOX / 64; k++) {
-            sv[k] = has_slot ? Sg[lane + 64 * k] : R.tau;
-            wv[k] = has_slot ? Wg[lane + 64 * k] : 0.0f;
+        float4* Sg = reinterpret_cast<float4*>(Pl.sdf + (size_t)(has_slot ? slot : 0) * BRICK_VOX + l0);
+        float4* Wg = reinterpret_cast<float4*>(Pl.weight + (size_t)(has_slot ? slot : 0) * BRICK_VOX + l0);
+        float sv[8], wv[8];
+        {
+            const float4 s0 = has_slot ? Sg[0] : make_float4(R.tau, R.tau, R.tau, R.tau);
+            const float4 s1 = has_slot ? Sg[1] : make_float4(R.tau, R.tau, R.tau, R.tau);
+            const float4 w0 = has_slot ? Wg[0] : make_float4(0.f, 0.f, 0.f, 0.f);
+            const float4 w1 = has_slot ? Wg[1] : make_float4(0.f, 0.f, 0.f, 0.f);
+            sv[0] = s0.x; sv[1] = s0.y; sv[2] = s0.z; sv[3] = s0.w;
+            sv[4] = s1.x; sv[5] = s1.y; sv[6] = s1.z; sv[7] = s1.w;
+            wv[0] = w0.x; wv[1] = w0.y; wv[2] = w0.z; wv[3] = w0.w;
+            wv[4] = w1.x; wv[5] = w1.y; wv[6] = w1.z; wv[7] = w1.w;
         }
         uint32_t dirty = 0;
-        for (uint32_t t = 0; t < ns; t++) {
-            const uint32_t c0 = __shfl(cs, (int)t, 64);
-            const uint32_t c1 = __shfl(cs, (int)t + 1, 64);  // lane ns holds n
-            if (c0 == c1) continue;
-            const float ox = D.ox[t], oy = D.oy[t], oz = D.oz[t];
-            for (uint32_t j = c0 + lane; j < c1; j += 64) {
-                const size_t i = Wk.ray_list[base + j];
+        for (uint32_t j0 = 0; j0 < n; j0 += 64) {
+            const uint32_t j = j0 + lane;
+            const bool valid = j < n;
+            const float4 rc = valid ? Wk.rec[base + j] : make_float4(0.f, 0.f, 0.f, 0.f);
+            const uint32_t cnt_j = valid ? __float_as_uint(rc.w) : 0u;
+            // scan of ray j: the largest t < ns with cs_t <= j (lane t holds cs_t; cs_0 = 0).
+            // Branch-free search whose trip count depends on ns only, so every lane runs every
+            // __shfl (a shfl from a lane that left a divergent loop reads garbage).
+            uint32_t tj = 0;
+            for (uint32_t len = ns; len > 1;) {
+                const uint32_t half = len >> 1;
+                const uint32_t v = (uint32_t)__shfl(cs, (int)(tj + half), 64);
+                tj = (v <= j) ? tj + half : tj;
+                len -= half;
+            }
+            const uint32_t off = wave_excl_scan(cnt_j, lane);
+            if (valid && cnt_j) {
+                const float ox = D.ox[tj], oy = D.oy[tj], oz = D.oz[tj];
                 RayState r;
-                if (!ray_init(R, ox, oy, oz, xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2], r))
-                    continue;
-                for (int it = 0; it < MAX_DDA_STEPS; it++) {
-                    if ((r.vx >> 3) == bx && (r.vy >> 3) == by && (r.vz >> 3) == bz) {
-                        float s;
-                        if (voxel_sample(R, ox, oy, oz, r, s)) {
-                            const int l = ((r.vz & 7) << 6) | ((r.vy & 7) << 3) | (r.vx & 7);
-                            const long long q = (long long)(s * 4294967296.0f);
-                            atomicAdd(&A[l], (unsigned long long)q);
-                            atomicAdd(&B[l], 1u);
+                if (ray_init(R, ox, oy, oz, rc.x, rc.y, rc.z, r)) {
+                    uint32_t w = 0;
+                    for (int it = 0; it < MAX_DDA_STEPS; it++) {
+                        if ((r.vx >> 3) == bx && (r.vy >> 3) == by && (r.vz >> 3) == bz) {
+                            float s;
+                            if (voxel_sample(R, ox, oy, oz, r, s) && w < cnt_j) {
+                                smp_s[off + w] = s;
+                                smp_l[off + w] =
+                                    (uint16_t)(((r.vz & 7) << 6) | ((r.vy & 7) << 3) | (r.vx & 7));
+                                w++;
+                            }
+                        }
+                        if (!ray_step(r)) break;
+                    }
+                }
+            }
+            wave_sync_lds();
+            const uint32_t last_lane = min(63u, n - 1 - j0);
+            const uint32_t t_first = __shfl(tj, 0, 64);
+            const uint32_t t_last = __shfl(tj, (int)last_lane, 64);
+            for (uint32_t t = t_first; t <= t_last; t++) {
+                const unsigned long long m = __ballot(valid && tj == t);
+                if (!m) continue;
+                const int fl = __ffsll(m) - 1;
+                const int ll = 63 - __clzll(m);
+                const uint32_t sa = __shfl(off, fl, 64);
+                const uint32_t sb = __shfl(off + cnt_j, ll, 64);
+                for (uint32_t q = sa + lane; q < sb; q += 64) {
+                    const int l = smp_l[q];
+                    const long long fx = (long long)(smp_s[q] * 4294967296.0f);
+                    atomicAdd(&A[l], (unsigned long long)fx);
+                    atomicAdd(&B[l], 1u);
+                }
+                const uint32_t end_t = (t + 1 < ns) ? (uint32_t)__shfl(cs, (int)t + 1, 64) : n;
+                if (end_t <= j0 + 64) {  // every ray of scan t has been accumulated: fuse
+                    wave_sync_lds();
+                    const uint4 b0 = *reinterpret_cast<const uint4*>(&B[l0]);
+                    const uint4 b1 = *reinterpret_cast<const uint4*>(&B[l0 + 4]);
+                    const uint32_t bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+                    for (int k = 0; k < 8; k++) {
+                        if (bb[k]) {
+                            const float bf = (float)bb[k];
+                            const float af =
+                                (float)((double)(long long)A[l0 + k] * (1.0 / 4294967296.0));
+                            const float nw = wv[k] + bf;
+                            sv[k] = (sv[k] * wv[k] + af) / nw;
+                            wv[k] = nw;
+                            A[l0 + k] = 0ull;
+                            B[l0 + k] = 0u;
+                            dirty |= 1u << k;
+                            nvox++;
                         }
                     }
-                    if (!ray_step(r)) break;
                 }
+                wave_sync_lds();
             }
-            wave_sync_lds();
-#pragma unroll
-            for (int k = 0; k < BRICK_VOX / 64; k++) {
-                const int l = lane + 64 * k;
-                const uint32_t b = B[l];
-                if (b) {
-                    const float bf = (float)b;
-                    const float af = (float)((double)(long long)A[l] * (1.0 / 4294967296.0));
-                    const float nw = wv[k] + bf;
-                    sv[k] = (sv[k] * wv[k] + af) / nw;
-                    wv[k] = nw;
-                    A[l] = 0ull;
-                    B[l] = 0u;
-                    dirty |= 1u << k;
-                    nvox++;
-                }
-            }
-            wave_sync_lds();
         }
         if (has_slot) {
-#pragma unroll
-            for (int k = 0; k < BRICK_VOX / 64; k++) {
-                if (dirty & (1u << k)) {
-                    Sg[lane + 64 * k] = sv[k];
-                    Wg[lane + 64 * k] = wv[k];
-                }
+            if (dirty & 0x0Fu) {
+                Sg[0] = make_float4(sv[0], sv[1], sv[2], sv[3]);
+                Wg[0] = make_float4(wv[0], wv[1], wv[2], wv[3]);
+            }
+            if (dirty & 0xF0u) {
+                Sg[1] = make_float4(sv[4], sv[5], sv[6], sv[7]);
+                Wg[1] = make_float4(wv[4], wv[5], wv[6], wv[7]);
             }
         }
         ndirty += __popc(dirty);
-        if (lane == 0) T.cnt[h] = 0u;  // ready for the next batch
-        if ((uint32_t)lane < ns) T.cell[(size_t)h * T.cell_stride + lane] = 0u;
+        // zero every cell of the brick (k_compact prefixes whole uint4 groups) for the next batch
+        if ((uint32_t)lane < T.cell_stride) T.cell[(size_t)h * T.cell_stride + lane] = 0u;
     }
-    __shared__ unsigned long long red[2][INT_WAVES];
     const unsigned long long v = wave_sum<unsigned long long>(nvox);
     const unsigned long long d = wave_sum<unsigned long long>(ndirty);
-    if (lane == 0) { red[0][wid] = v; red[1][wid] = d; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const unsigned long long tv = red[0][0] + red[0][1] + red[0][2] + red[0][3];
-        const unsigned long long td = red[1][0] + red[1][1] + red[1][2] + red[1][3];
-        if (tv) {
-            atomicAdd(&C->n_vox[blockIdx.x & 7], tv);
-            atomicAdd(&G->tot_vox[blockIdx.x & 7], tv);
+    if (lane == 0) {
+        if (v) {
+            atomicAdd(&C->n_vox[blockIdx.x & 7], v);
+            atomicAdd(&G->tot_vox[blockIdx.x & 7], v);
         }
-        if (td) {
-            atomicAdd(&C->n_dirty[blockIdx.x & 7], td);
-            atomicAdd(&G->tot_dirty[blockIdx.x & 7], td);
+        if (d) {
+            atomicAdd(&C->n_dirty[blockIdx.x & 7], d);
+            atomicAdd(&G->tot_dirty[blockIdx.x & 7], d);
         }
     }
 }
@@ -656,22 +737,24 @@ static int grid_for(uint64_t items, int per_block, int cap) {
     return (int)(g < 1 ? 1 : (g > (uint64_t)cap ? (uint64_t)cap : g));
 }
 
+constexpr int INT_GRID = 2560;  // k_integrate: 256 CUs x 10 resident one-wave workgroups (LDS)
+
 hipError_t launch_batch(const float* d_xyz, const BatchDesc& D, const RayConst& R, const Table& T,
                         const Work& Wk, const Pool& Pl, Globals* G, int parity, hipStream_t st,
                         KernelTimer* timer) {
-    const uint32_t total = D.off[D.n_scans];
-    const uint32_t n_slots = total * Wk.maxp;
-    if (timer) timer->begin(KIND_RAYS, st);
-    k_rays<<<grid_for(total, 256, 2048), 256, 0, st>>>(d_xyz, D, R, T, Wk, G, parity);
-    if (timer) timer->end(KIND_RAYS, st);
-    if (timer) timer->begin(KIND_OFFSETS, st);
-    k_compact<<<64, CMP_THREADS, 0, st>>>(D.n_scans, T, Wk, G, parity);
-    if (timer) timer->end(KIND_OFFSETS, st);
-    if (timer) timer->begin(KIND_SCATTER, st);
-    k_scatter<<<grid_for(n_slots, 256, 8192), 256, 0, st>>>(n_slots, T, Wk);
-    if (timer) timer->end(KIND_SCATTER, st);
+    if (D.n_blocks == 0) return hipSuccess;
+    if (timer) timer->begin(KIND_COUNT, st);
+    k_count<<<D.n_blocks, CNT_THREADS, 0, st>>>(d_xyz, D, R, T, Wk, G, parity);
+    if (timer) timer->end(KIND_COUNT, st);
+    if (timer) timer->begin(KIND_COMPACT, st);
+    k_compact<<<grid_for(T.mask + 1, CMP_THREADS, 256), CMP_THREADS, 0, st>>>(D.n_scans, T, Wk,
+                                                                                G, parity);
+    if (timer) timer->end(KIND_COMPACT, st);
+    if (timer) timer->begin(KIND_PLACE, st);
+    k_place<<<D.n_blocks, CNT_THREADS, 0, st>>>(d_xyz, D, T, Wk);
+    if (timer) timer->end(KIND_PLACE, st);
     if (timer) timer->begin(KIND_INTEGRATE, st);
-    k_integrate<<<1536, 256, 0, st>>>(d_xyz, D, R, T, Wk, Pl, G, parity);
+    k_integrate<<<INT_GRID, 64, 0, st>>>(D, R, T, Wk, Pl, G, parity);
     if (timer) timer->end(KIND_INTEGRATE, st);
     return hipGetLastError();
 }
