@@ -134,6 +134,8 @@ struct KernelTimer {
 hipError_t launch_batch(const float* d_xyz, const BatchDesc& D, const RayConst& R, const Table& T,
                         const Work& Wk, const Pool& Pl, Globals* G, int parity, hipStream_t st,
                         KernelTimer* timer);
+hipError_t launch_integrate(const BatchDesc& D, const RayConst& R, const Table& T, const Work& Wk,
+                            const Pool& Pl, Globals* G, int parity, hipStream_t st);
 hipError_t launch_query_dense(const Table& T, const Pool& Pl, const int lo[3], const int dims[3],
                               float bg, float* d_sdf, float* d_w, hipStream_t st);
 hipError_t launch_import(const Table& T, const Pool& Pl, const int32_t* d_coords, uint32_t n,

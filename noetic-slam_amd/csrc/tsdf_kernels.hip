@@ -9,16 +9,14 @@
 //               atomicAdd on the brick's pair count and one on its (brick, scan) cell — global
 //               atomics per distinct brick per workgroup instead of per pair.
 //   k_compact   per active brick: block-wide scans give its contiguous ray-record segment, its pool
-//               slot if it is new, and the prefix of its per-scan cells (records scan-ordered)
+//               slot if it is new, and the prefix of its per-scan cells (records scan-ordered);
+//               it sweeps the table's `touched` words, so k_count needs no first-touch atomics
 //   k_place     same workgroups as k_count: coalesced read of the rays, one record
 //               (x, y, z, in-brick sample count) written per pair to its brick segment
-//   k_integrate one wave per active brick: the brick's (sdf, weight) live in registers (8 voxels
-//               per lane) for the whole batch.  The brick's records are read 64 at a time
-//               (coalesced); every lane walks its ray and writes its in-brick samples to an LDS
-//               buffer (positions from a wave prefix of the counts); then, for each scan of the
-//               chunk in order, the scan's samples are added as exact fixed point into an LDS tile
-//               and — once the scan is complete — each lane fuses its own voxels.  Each touched
-//               brick is read once and its dirty voxels written once per batch.
+//   k_integrate (tsdf_integrate.hip) one workgroup per active brick: brick in LDS for the whole
+//               batch, samples accumulated and fused scan by scan, touched voxels only.
+// (Global atomics in k_count: one cell atomicAdd per distinct brick per workgroup, plus the
+//  find-or-insert CAS of bricks new to the map.)
 //
 // Semantics: VDBFusion's VDBVolume::Integrate, restated in oracle/tsdf_oracle.c, which is the
 // bit-exact CPU twin of this file's arithmetic.  Ray arithmetic is fp32 with contraction off
@@ -30,165 +28,9 @@
 #include <stdint.h>
 
 #include "tsdf_device.h"
+#include "tsdf_ray.h"
 
 namespace tsdf {
-
-// ------------------------------------------------------------------------------------------------
-// ray setup and walk (same op order as oracle/tsdf_oracle.c walk_ray)
-
-struct RayState {
-    float px, py, pz;  // hit point (world)
-    float t1i;         // band end (index units)
-    float tnx, tny, tnz;
-    float tdx, tdy, tdz;
-    int vx, vy, vz;
-    int sx, sy, sz;
-};
-
-__device__ __forceinline__ void axis_init(float u, float s, float t0i, int v, float& tn, float& td,
-                                          int& st) {
-    if (u > 0.0f) {
-        const float inv = 1.0f / u;
-        st = 1;
-        td = inv;
-        tn = t0i + ((float)(v + 1) - s) * inv;
-    } else if (u < 0.0f) {
-        const float inv = 1.0f / u;
-        st = -1;
-        td = -inv;
-        tn = t0i + ((float)v - s) * inv;
-    } else {
-        st = 0;
-        td = __builtin_inff();
-        tn = __builtin_inff();
-    }
-}
-
-// Returns false when the ray is filtered out (zero/NaN length, outside [min_range, max_range]).
-__device__ __forceinline__ bool ray_init(const RayConst& R, float ox, float oy, float oz, float px,
-                                         float py, float pz, RayState& r) {
-    const float dx = px - ox, dy = py - oy, dz = pz - oz;
-    const float depth = __builtin_sqrtf(dx * dx + dy * dy + dz * dz);
-    if (!(depth > 0.0f)) return false;
-    if (!(depth >= R.min_range) || !(depth <= R.max_range)) return false;
-    const float ux = dx / depth, uy = dy / depth, uz = dz / depth;
-    const float t0 = R.carving ? 0.0f : depth - R.tau;
-    const float t1 = depth + R.tau;
-    const float t0i = t0 * R.inv_vs;
-    r.t1i = t1 * R.inv_vs;
-    const float sx = ox * R.inv_vs + ux * t0i;
-    const float sy = oy * R.inv_vs + uy * t0i;
-    const float sz = oz * R.inv_vs + uz * t0i;
-    r.vx = (int)__builtin_floorf(sx);
-    r.vy = (int)__builtin_floorf(sy);
-    r.vz = (int)__builtin_floorf(sz);
-    axis_init(ux, sx, t0i, r.vx, r.tnx, r.tdx, r.sx);
-    axis_init(uy, sy, t0i, r.vy, r.tny, r.tdy, r.sy);
-    axis_init(uz, sz, t0i, r.vz, r.tnz, r.tdz, r.sz);
-    r.px = px;
-    r.py = py;
-    r.pz = pz;
-    return true;
-}
-
-// ComputeSDF at the current voxel; true (and the truncated sample) when it passes sdf > -tau.
-__device__ __forceinline__ bool voxel_sample(const RayConst& R, float ox, float oy, float oz,
-                                             const RayState& r, float& s) {
-    if (!(r.vx > -VOX_LIMIT && r.vx < VOX_LIMIT && r.vy > -VOX_LIMIT && r.vy < VOX_LIMIT &&
-          r.vz > -VOX_LIMIT && r.vz < VOX_LIMIT))
-        return false;
-    const float cx = ((float)r.vx + 0.5f) * R.vs;
-    const float cy = ((float)r.vy + 0.5f) * R.vs;
-    const float cz = ((float)r.vz + 0.5f) * R.vs;
-    const float ax = cx - ox, ay = cy - oy, az = cz - oz;
-    const float bx = r.px - cx, by = r.py - cy, bz = r.pz - cz;
-    const float dist = __builtin_sqrtf(bx * bx + by * by + bz * bz);
-    const float proj = ax * bx + ay * by + az * bz;
-    if (!(proj > 0.0f || proj < 0.0f)) return false;
-    const float sdf = proj > 0.0f ? dist : -dist;
-    if (!(sdf > -R.tau)) return false;
-    s = sdf < R.tau ? sdf : R.tau;
-    return true;
-}
-
-// One DDA step (math::MinIndex tie-break: equal entries resolve to the higher axis).
-// Returns false when the next entry time is past the band end.
-// Written with selects only: an axis index would make hipcc spill the state to scratch.
-__device__ __forceinline__ bool ray_step(RayState& r) {
-    const bool mx = (r.tnx < r.tny) && (r.tnx < r.tnz);  // == oracle: a = 0
-    const bool my = !mx && (r.tny < r.tnz);              // == oracle: a = 1
-    const bool mz = !mx && !my;                          // == oracle: a = 2 (ties -> higher)
-    const float t = mx ? r.tnx : (my ? r.tny : r.tnz);
-    if (!(t <= r.t1i)) return false;
-    r.tnx = mx ? r.tnx + r.tdx : r.tnx;
-    r.tny = my ? r.tny + r.tdy : r.tny;
-    r.tnz = mz ? r.tnz + r.tdz : r.tnz;
-    r.vx += mx ? r.sx : 0;
-    r.vy += my ? r.sy : 0;
-    r.vz += mz ? r.sz : 0;
-    return true;
-}
-
-__device__ __forceinline__ uint64_t pack_brick(int bx, int by, int bz) {
-    return (uint64_t)(bx + BRICK_COORD_BIAS) | ((uint64_t)(by + BRICK_COORD_BIAS) << 21) |
-           ((uint64_t)(bz + BRICK_COORD_BIAS) << 42);
-}
-
-__device__ __forceinline__ uint64_t brick_key_of(int vx, int vy, int vz) {
-    return pack_brick(vx >> 3, vy >> 3, vz >> 3);
-}
-
-__device__ __forceinline__ uint64_t mix64(uint64_t k) {
-    k ^= k >> 33;
-    k *= 0xff51afd7ed558ccdull;
-    k ^= k >> 33;
-    k *= 0xc4ceb9fe1a85ec53ull;
-    k ^= k >> 33;
-    return k;
-}
-
-// Find-or-insert a brick key; returns the table index or -1 when the table is full.  Keys are
-// never removed, so a stale EMPTY read is resolved by the CAS and a non-EMPTY read is final.
-__device__ __forceinline__ int64_t table_insert(const Table& T, uint64_t key, uint32_t* overflow) {
-    uint64_t h = mix64(key) & T.mask;
-    for (uint64_t probe = 0; probe <= T.mask; probe++) {
-        const uint64_t k = T.keys[h];
-        if (k == key) return (int64_t)h;
-        if (k == EMPTY_KEY) {
-            const unsigned long long old =
-                atomicCAS((unsigned long long*)&T.keys[h], (unsigned long long)EMPTY_KEY,
-                          (unsigned long long)key);
-            if (old == EMPTY_KEY || old == key) return (int64_t)h;
-        }
-        h = (h + 1) & T.mask;
-    }
-    atomicOr(overflow, OVF_TABLE);
-    return -1;
-}
-
-__device__ __forceinline__ int64_t table_find(const Table& T, uint64_t key) {
-    uint64_t h = mix64(key) & T.mask;
-    for (uint64_t probe = 0; probe <= T.mask; probe++) {
-        const uint64_t k = T.keys[h];
-        if (k == key) return (int64_t)h;
-        if (k == EMPTY_KEY) return -1;
-        h = (h + 1) & T.mask;
-    }
-    return -1;
-}
-
-template <typename Tv>
-__device__ __forceinline__ Tv wave_sum(Tv v) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
-    return v;
-}
-
-__device__ __forceinline__ void wave_sync_lds() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 // ------------------------------------------------------------------------------------------------
 // shared helpers of the batch kernels
@@ -482,169 +324,6 @@ __global__ __launch_bounds__(CNT_THREADS) void k_place(const float* __restrict__
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_integrate: one wave per active brick; brick in registers, samples and tile in LDS
-
-constexpr int SBUF = 64 * MAX_IN_BRICK;
-
-__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t x, int lane) {
-    uint32_t v = x;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(v, d, 64);
-        if (lane >= d) v += y;
-    }
-    return v - x;
-}
-
-__global__ __launch_bounds__(64) void k_integrate(BatchDesc D, RayConst R, Table T, Work Wk,
-                                                 Pool Pl, Globals* G, int parity) {
-    __shared__ __attribute__((aligned(16))) unsigned long long A[BRICK_VOX];  // sum trunc(s*2^32)
-    __shared__ __attribute__((aligned(16))) uint32_t B[BRICK_VOX];            // sample count
-    __shared__ float smp_s[SBUF];
-    __shared__ uint16_t smp_l[SBUF];
-    Counters* C = &G->ctr[parity];
-    const int lane = threadIdx.x;
-    const int l0 = lane * 8;  // this lane owns voxels l0 .. l0 + 7
-    const uint32_t n_active = min(C->n_active, Wk.max_active);
-    const uint32_t ns = D.n_scans;
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-        A[l0 + k] = 0ull;
-        B[l0 + k] = 0u;
-    }
-    wave_sync_lds();
-    uint32_t nvox = 0, ndirty = 0;
-    for (uint32_t a = blockIdx.x; a < n_active; a += gridDim.x) {
-        const uint32_t h = Wk.active[a];
-        const uint32_t slot = T.slots[h];
-        const uint32_t n = T.cnt[h];
-        const uint32_t base = T.toff[h];
-        const uint32_t cs = (uint32_t)lane < ns ? T.cell[(size_t)h * T.cell_stride + lane] : n;
-        const uint64_t key = T.keys[h];
-        const int bx = (int)(key & 0x1FFFFF) - BRICK_COORD_BIAS;
-        const int by = (int)((key >> 21) & 0x1FFFFF) - BRICK_COORD_BIAS;
-        const int bz = (int)((key >> 42) & 0x1FFFFF) - BRICK_COORD_BIAS;
-        const bool has_slot = slot < T.max_bricks;
-        float4* Sg = reinterpret_cast<float4*>(Pl.sdf + (size_t)(has_slot ? slot : 0) * BRICK_VOX + l0);
-        float4* Wg = reinterpret_cast<float4*>(Pl.weight + (size_t)(has_slot ? slot : 0) * BRICK_VOX + l0);
-        float sv[8], wv[8];
-        {
-            const float4 s0 = has_slot ? Sg[0] : make_float4(R.tau, R.tau, R.tau, R.tau);
-            const float4 s1 = has_slot ? Sg[1] : make_float4(R.tau, R.tau, R.tau, R.tau);
-            const float4 w0 = has_slot ? Wg[0] : make_float4(0.f, 0.f, 0.f, 0.f);
-            const float4 w1 = has_slot ? Wg[1] : make_float4(0.f, 0.f, 0.f, 0.f);
-            sv[0] = s0.x; sv[1] = s0.y; sv[2] = s0.z; sv[3] = s0.w;
-            sv[4] = s1.x; sv[5] = s1.y; sv[6] = s1.z; sv[7] = s1.w;
-            wv[0] = w0.x; wv[1] = w0.y; wv[2] = w0.z; wv[3] = w0.w;
-            wv[4] = w1.x; wv[5] = w1.y; wv[6] = w1.z; wv[7] = w1.w;
-        }
-        uint32_t dirty = 0;
-        for (uint32_t j0 = 0; j0 < n; j0 += 64) {
-            const uint32_t j = j0 + lane;
-            const bool valid = j < n;
-            const float4 rc = valid ? Wk.rec[base + j] : make_float4(0.f, 0.f, 0.f, 0.f);
-            const uint32_t cnt_j = valid ? __float_as_uint(rc.w) : 0u;
-            // scan of ray j: the largest t < ns with cs_t <= j (lane t holds cs_t; cs_0 = 0).
-            // Branch-free search whose trip count depends on ns only, so every lane runs every
-            // __shfl (a shfl from a lane that left a divergent loop reads garbage).
-            uint32_t tj = 0;
-            for (uint32_t len = ns; len > 1;) {
-                const uint32_t half = len >> 1;
-                const uint32_t v = (uint32_t)__shfl(cs, (int)(tj + half), 64);
-                tj = (v <= j) ? tj + half : tj;
-                len -= half;
-            }
-            const uint32_t off = wave_excl_scan(cnt_j, lane);
-            if (valid && cnt_j) {
-                const float ox = D.ox[tj], oy = D.oy[tj], oz = D.oz[tj];
-                RayState r;
-                if (ray_init(R, ox, oy, oz, rc.x, rc.y, rc.z, r)) {
-                    uint32_t w = 0;
-                    for (int it = 0; it < MAX_DDA_STEPS; it++) {
-                        if ((r.vx >> 3) == bx && (r.vy >> 3) == by && (r.vz >> 3) == bz) {
-                            float s;
-                            if (voxel_sample(R, ox, oy, oz, r, s) && w < cnt_j) {
-                                smp_s[off + w] = s;
-                                smp_l[off + w] =
-                                    (uint16_t)(((r.vz & 7) << 6) | ((r.vy & 7) << 3) | (r.vx & 7));
-                                w++;
-                            }
-                        }
-                        if (!ray_step(r)) break;
-                    }
-                }
-            }
-            wave_sync_lds();
-            const uint32_t last_lane = min(63u, n - 1 - j0);
-            const uint32_t t_first = __shfl(tj, 0, 64);
-            const uint32_t t_last = __shfl(tj, (int)last_lane, 64);
-            for (uint32_t t = t_first; t <= t_last; t++) {
-                const unsigned long long m = __ballot(valid && tj == t);
-                if (!m) continue;
-                const int fl = __ffsll(m) - 1;
-                const int ll = 63 - __clzll(m);
-                const uint32_t sa = __shfl(off, fl, 64);
-                const uint32_t sb = __shfl(off + cnt_j, ll, 64);
-                for (uint32_t q = sa + lane; q < sb; q += 64) {
-                    const int l = smp_l[q];
-                    const long long fx = (long long)(smp_s[q] * 4294967296.0f);
-                    atomicAdd(&A[l], (unsigned long long)fx);
-                    atomicAdd(&B[l], 1u);
-                }
-                const uint32_t end_t = (t + 1 < ns) ? (uint32_t)__shfl(cs, (int)t + 1, 64) : n;
-                if (end_t <= j0 + 64) {  // every ray of scan t has been accumulated: fuse
-                    wave_sync_lds();
-                    const uint4 b0 = *reinterpret_cast<const uint4*>(&B[l0]);
-                    const uint4 b1 = *reinterpret_cast<const uint4*>(&B[l0 + 4]);
-                    const uint32_t bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-#pragma unroll
-                    for (int k = 0; k < 8; k++) {
-                        if (bb[k]) {
-                            const float bf = (float)bb[k];
-                            const float af =
-                                (float)((double)(long long)A[l0 + k] * (1.0 / 4294967296.0));
-                            const float nw = wv[k] + bf;
-                            sv[k] = (sv[k] * wv[k] + af) / nw;
-                            wv[k] = nw;
-                            A[l0 + k] = 0ull;
-                            B[l0 + k] = 0u;
-                            dirty |= 1u << k;
-                            nvox++;
-                        }
-                    }
-                }
-                wave_sync_lds();
-            }
-        }
-        if (has_slot) {
-            if (dirty & 0x0Fu) {
-                Sg[0] = make_float4(sv[0], sv[1], sv[2], sv[3]);
-                Wg[0] = make_float4(wv[0], wv[1], wv[2], wv[3]);
-            }
-            if (dirty & 0xF0u) {
-                Sg[1] = make_float4(sv[4], sv[5], sv[6], sv[7]);
-                Wg[1] = make_float4(wv[4], wv[5], wv[6], wv[7]);
-            }
-        }
-        ndirty += __popc(dirty);
-        // zero every cell of the brick (k_compact prefixes whole uint4 groups) for the next batch
-        if ((uint32_t)lane < T.cell_stride) T.cell[(size_t)h * T.cell_stride + lane] = 0u;
-    }
-    const unsigned long long v = wave_sum<unsigned long long>(nvox);
-    const unsigned long long d = wave_sum<unsigned long long>(ndirty);
-    if (lane == 0) {
-        if (v) {
-            atomicAdd(&C->n_vox[blockIdx.x & 7], v);
-            atomicAdd(&G->tot_vox[blockIdx.x & 7], v);
-        }
-        if (d) {
-            atomicAdd(&C->n_dirty[blockIdx.x & 7], d);
-            atomicAdd(&G->tot_dirty[blockIdx.x & 7], d);
-        }
-    }
-}
-
-// ------------------------------------------------------------------------------------------------
 // read-out / import
 
 __global__ void k_query_dense(Table T, Pool Pl, int lo0, int lo1, int lo2, int nx, int ny, int nz,
@@ -737,8 +416,6 @@ static int grid_for(uint64_t items, int per_block, int cap) {
     return (int)(g < 1 ? 1 : (g > (uint64_t)cap ? (uint64_t)cap : g));
 }
 
-constexpr int INT_GRID = 2560;  // k_integrate: 256 CUs x 10 resident one-wave workgroups (LDS)
-
 hipError_t launch_batch(const float* d_xyz, const BatchDesc& D, const RayConst& R, const Table& T,
                         const Work& Wk, const Pool& Pl, Globals* G, int parity, hipStream_t st,
                         KernelTimer* timer) {
@@ -754,9 +431,10 @@ hipError_t launch_batch(const float* d_xyz, const BatchDesc& D, const RayConst& 
     k_place<<<D.n_blocks, CNT_THREADS, 0, st>>>(d_xyz, D, T, Wk);
     if (timer) timer->end(KIND_PLACE, st);
     if (timer) timer->begin(KIND_INTEGRATE, st);
-    k_integrate<<<INT_GRID, 64, 0, st>>>(D, R, T, Wk, Pl, G, parity);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = launch_integrate(D, R, T, Wk, Pl, G, parity, st);  // tsdf_integrate.hip
     if (timer) timer->end(KIND_INTEGRATE, st);
-    return hipGetLastError();
+    return e;
 }
 
 hipError_t launch_query_dense(const Table& T, const Pool& Pl, const int lo[3], const int dims[3],

@@ -1,0 +1,169 @@
+// tsdf_ray.h — device helpers shared by the hot-path kernels: the fp32 ray model (the bit-exact
+// twin of oracle/tsdf_oracle.c walk_ray), brick keys, the global brick hash and wave utilities.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "tsdf_device.h"
+
+namespace tsdf {
+
+
+// ------------------------------------------------------------------------------------------------
+// ray setup and walk (same op order as oracle/tsdf_oracle.c walk_ray)
+
+struct RayState {
+    float px, py, pz;  // hit point (world)
+    float t1i;         // band end (index units)
+    float tnx, tny, tnz;
+    float tdx, tdy, tdz;
+    int vx, vy, vz;
+    int sx, sy, sz;
+};
+
+__device__ __forceinline__ void axis_init(float u, float s, float t0i, int v, float& tn, float& td,
+                                          int& st) {
+    if (u > 0.0f) {
+        const float inv = 1.0f / u;
+        st = 1;
+        td = inv;
+        tn = t0i + ((float)(v + 1) - s) * inv;
+    } else if (u < 0.0f) {
+        const float inv = 1.0f / u;
+        st = -1;
+        td = -inv;
+        tn = t0i + ((float)v - s) * inv;
+    } else {
+        st = 0;
+        td = __builtin_inff();
+        tn = __builtin_inff();
+    }
+}
+
+// Returns false when the ray is filtered out (zero/NaN length, outside [min_range, max_range]).
+__device__ __forceinline__ bool ray_init(const RayConst& R, float ox, float oy, float oz, float px,
+                                         float py, float pz, RayState& r) {
+    const float dx = px - ox, dy = py - oy, dz = pz - oz;
+    const float depth = __builtin_sqrtf(dx * dx + dy * dy + dz * dz);
+    if (!(depth > 0.0f)) return false;
+    if (!(depth >= R.min_range) || !(depth <= R.max_range)) return false;
+    const float ux = dx / depth, uy = dy / depth, uz = dz / depth;
+    const float t0 = R.carving ? 0.0f : depth - R.tau;
+    const float t1 = depth + R.tau;
+    const float t0i = t0 * R.inv_vs;
+    r.t1i = t1 * R.inv_vs;
+    const float sx = ox * R.inv_vs + ux * t0i;
+    const float sy = oy * R.inv_vs + uy * t0i;
+    const float sz = oz * R.inv_vs + uz * t0i;
+    r.vx = (int)__builtin_floorf(sx);
+    r.vy = (int)__builtin_floorf(sy);
+    r.vz = (int)__builtin_floorf(sz);
+    axis_init(ux, sx, t0i, r.vx, r.tnx, r.tdx, r.sx);
+    axis_init(uy, sy, t0i, r.vy, r.tny, r.tdy, r.sy);
+    axis_init(uz, sz, t0i, r.vz, r.tnz, r.tdz, r.sz);
+    r.px = px;
+    r.py = py;
+    r.pz = pz;
+    return true;
+}
+
+// ComputeSDF at the current voxel; true (and the truncated sample) when it passes sdf > -tau.
+__device__ __forceinline__ bool voxel_sample(const RayConst& R, float ox, float oy, float oz,
+                                             const RayState& r, float& s) {
+    if (!(r.vx > -VOX_LIMIT && r.vx < VOX_LIMIT && r.vy > -VOX_LIMIT && r.vy < VOX_LIMIT &&
+          r.vz > -VOX_LIMIT && r.vz < VOX_LIMIT))
+        return false;
+    const float cx = ((float)r.vx + 0.5f) * R.vs;
+    const float cy = ((float)r.vy + 0.5f) * R.vs;
+    const float cz = ((float)r.vz + 0.5f) * R.vs;
+    const float ax = cx - ox, ay = cy - oy, az = cz - oz;
+    const float bx = r.px - cx, by = r.py - cy, bz = r.pz - cz;
+    const float dist = __builtin_sqrtf(bx * bx + by * by + bz * bz);
+    const float proj = ax * bx + ay * by + az * bz;
+    if (!(proj > 0.0f || proj < 0.0f)) return false;
+    const float sdf = proj > 0.0f ? dist : -dist;
+    if (!(sdf > -R.tau)) return false;
+    s = sdf < R.tau ? sdf : R.tau;
+    return true;
+}
+
+// One DDA step (math::MinIndex tie-break: equal entries resolve to the higher axis).
+// Returns false when the next entry time is past the band end.
+// Written with selects only: an axis index would make hipcc spill the state to scratch.
+__device__ __forceinline__ bool ray_step(RayState& r) {
+    const bool mx = (r.tnx < r.tny) && (r.tnx < r.tnz);  // == oracle: a = 0
+    const bool my = !mx && (r.tny < r.tnz);              // == oracle: a = 1
+    const bool mz = !mx && !my;                          // == oracle: a = 2 (ties -> higher)
+    const float t = mx ? r.tnx : (my ? r.tny : r.tnz);
+    if (!(t <= r.t1i)) return false;
+    r.tnx = mx ? r.tnx + r.tdx : r.tnx;
+    r.tny = my ? r.tny + r.tdy : r.tny;
+    r.tnz = mz ? r.tnz + r.tdz : r.tnz;
+    r.vx += mx ? r.sx : 0;
+    r.vy += my ? r.sy : 0;
+    r.vz += mz ? r.sz : 0;
+    return true;
+}
+
+__device__ __forceinline__ uint64_t pack_brick(int bx, int by, int bz) {
+    return (uint64_t)(bx + BRICK_COORD_BIAS) | ((uint64_t)(by + BRICK_COORD_BIAS) << 21) |
+           ((uint64_t)(bz + BRICK_COORD_BIAS) << 42);
+}
+
+__device__ __forceinline__ uint64_t brick_key_of(int vx, int vy, int vz) {
+    return pack_brick(vx >> 3, vy >> 3, vz >> 3);
+}
+
+__device__ __forceinline__ uint64_t mix64(uint64_t k) {
+    k ^= k >> 33;
+    k *= 0xff51afd7ed558ccdull;
+    k ^= k >> 33;
+    k *= 0xc4ceb9fe1a85ec53ull;
+    k ^= k >> 33;
+    return k;
+}
+
+// Find-or-insert a brick key; returns the table index or -1 when the table is full.  Keys are
+// never removed, so a stale EMPTY read is resolved by the CAS and a non-EMPTY read is final.
+__device__ __forceinline__ int64_t table_insert(const Table& T, uint64_t key, uint32_t* overflow) {
+    uint64_t h = mix64(key) & T.mask;
+    for (uint64_t probe = 0; probe <= T.mask; probe++) {
+        const uint64_t k = T.keys[h];
+        if (k == key) return (int64_t)h;
+        if (k == EMPTY_KEY) {
+            const unsigned long long old =
+                atomicCAS((unsigned long long*)&T.keys[h], (unsigned long long)EMPTY_KEY,
+                          (unsigned long long)key);
+            if (old == EMPTY_KEY || old == key) return (int64_t)h;
+        }
+        h = (h + 1) & T.mask;
+    }
+    atomicOr(overflow, OVF_TABLE);
+    return -1;
+}
+
+__device__ __forceinline__ int64_t table_find(const Table& T, uint64_t key) {
+    uint64_t h = mix64(key) & T.mask;
+    for (uint64_t probe = 0; probe <= T.mask; probe++) {
+        const uint64_t k = T.keys[h];
+        if (k == key) return (int64_t)h;
+        if (k == EMPTY_KEY) return -1;
+        h = (h + 1) & T.mask;
+    }
+    return -1;
+}
+
+template <typename Tv>
+__device__ __forceinline__ Tv wave_sum(Tv v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+}  // namespace tsdf

@@ -18,7 +18,8 @@ def load_hip_library(path=None):
     global _hip
     if _hip is not None and path is None:
         return _hip
-    p = path or HIP_LIB
+    # TSDF_HIP_LIB: load another build of the same ABI (A/B kernel experiments, profiles/)
+    p = path or os.environ.get("TSDF_HIP_LIB") or HIP_LIB
     if not os.path.exists(p):
         raise RuntimeError("libtsdf_hip.so not built (%s); run `python -c 'import __graft_entry__ "
                            "as g; g.build()'` or `make -C noetic-slam_amd/csrc`" % p)
