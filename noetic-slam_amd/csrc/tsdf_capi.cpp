@@ -144,6 +144,15 @@ static uint32_t pairs_per_ray(const tsdf_params& p) {
     return (uint32_t)(1.0 + 3.0 * crossings);
 }
 
+// Sample slots per ray: a ray's gated voxels are among its DDA voxels, at most
+// 1 + 3 (floor(band) + 2) (5 cm / 15 cm: 25).
+static uint32_t samples_per_ray(const tsdf_params& p) {
+    double band;
+    if (p.space_carving) band = (p.max_range + p.sdf_trunc) / p.voxel_size;
+    else band = 2.0 * p.sdf_trunc / p.voxel_size;
+    return (uint32_t)(1.0 + 3.0 * (std::floor(band) + 2.0));
+}
+
 // Launch one batch (desc offsets relative to d_xyz); fills the workgroup prefix of D.
 static int launch(tsdf_ctx* c, const float* d_xyz, BatchDesc& D) {
     if (D.n_scans == 0) return TSDF_OK;
@@ -211,7 +220,7 @@ void tsdf_destroy(tsdf_ctx* c) {
                    c->T.touched,
                    c->T.cell,        c->T.brick_keys,    c->Pl.sdf,        c->Pl.weight,
                    c->Wk.pair,       c->Wk.blk,          c->Wk.blk_occ,    c->Wk.fb,
-                   c->Wk.rec,        c->Wk.active,
+                   c->Wk.smp,        c->Wk.active,
                    c->G,             c->d_stage};
     for (void* d : dev)
         if (d) (void)hipFree(d);
@@ -241,25 +250,36 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
     c->R.max_range = (float)p->max_range;
     c->R.carving = p->space_carving ? 1 : 0;
 
+    // Points one batch may hold: max_batch full scans, unless the per-ray worst cases (pair slots,
+    // sample slots — large with space carving) exceed the u32 index space or the sample budget;
+    // the host queue then cuts batches by points.  A single scan must always fit.
     const uint32_t maxp = pairs_per_ray(*p);
-    c->max_points = p->max_points;
+    const uint32_t spr = samples_per_ray(*p);
+    const uint64_t smp_budget = 1ull << 30;  // samples per batch (8 GiB of 8-byte records)
     c->max_batch = p->max_batch;
-    uint64_t slots = c->max_points * c->max_batch * maxp;
-    if (p->max_pairs && p->max_pairs < slots) slots = p->max_pairs;  // caller-imposed cap
-    if (slots >= 0xFFFFFFF0ull || slots < maxp)
-        return fail(c, TSDF_EINVAL, "max_batch * max_points * pairs_per_ray = %llu out of range",
-                    (unsigned long long)slots);
-    c->batch_points = slots / maxp;
-    if (c->max_points > c->batch_points) c->max_points = c->batch_points;
+    uint64_t bp = p->max_points * c->max_batch;
+    bp = std::min<uint64_t>(bp, 0xFFFFFFF0ull / maxp);
+    bp = std::min<uint64_t>(bp, smp_budget / spr);
+    if (p->max_pairs) bp = std::min<uint64_t>(bp, p->max_pairs / maxp);  // caller-imposed cap
+    if (bp < p->max_points)
+        return fail(c, TSDF_EINVAL,
+                    "max_points %llu exceeds what one batch can hold (%llu: %u pair and %u sample "
+                    "slots per ray)", (unsigned long long)p->max_points, (unsigned long long)bp,
+                    maxp, spr);
+    c->max_points = p->max_points;
+    c->batch_points = bp;
+    const uint64_t slots = bp * maxp;
     c->cap = next_pow2(2 * p->max_bricks);
     c->T.mask = c->cap - 1;
     c->T.max_bricks = (uint32_t)p->max_bricks;
     c->T.cell_stride = (c->max_batch + 3u) & ~3u;
     c->Wk.maxp = maxp;
     c->Wk.max_active = (uint32_t)std::min<uint64_t>(c->cap, slots);
-    c->Wk.max_rec = (uint32_t)slots;
+    c->Wk.max_smp = (uint32_t)std::min<uint64_t>(bp * spr, 0xFFFFFFF0ull);
     // fallback pairs (a workgroup's LDS brick hash is full): rare without carving, the rule with it
-    c->Wk.max_fb = (uint32_t)(p->space_carving ? slots : std::max<uint64_t>(slots / 16, 1u << 20));
+    // (the fallback index has 26 bits; past it pairs are dropped and OVF_FB reported)
+    c->Wk.max_fb = (uint32_t)std::min<uint64_t>(
+        p->space_carving ? slots : std::max<uint64_t>(slots / 16, 1u << 20), 1u << 26);
     c->max_blocks = (uint32_t)(c->batch_points / RPB + MAX_BATCH + 1);
 
     HIPCHK(c, hipMalloc(&c->T.keys, c->cap * sizeof(uint64_t)));
@@ -276,7 +296,7 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
     HIPCHK(c, hipMalloc(&c->Wk.blk, (size_t)c->max_blocks * HCAP * sizeof(uint2)));
     HIPCHK(c, hipMalloc(&c->Wk.blk_occ, (size_t)c->max_blocks * (HCAP / 32) * sizeof(uint32_t)));
     HIPCHK(c, hipMalloc(&c->Wk.fb, (size_t)c->Wk.max_fb * sizeof(uint4)));
-    HIPCHK(c, hipMalloc(&c->Wk.rec, slots * sizeof(float4)));
+    HIPCHK(c, hipMalloc(&c->Wk.smp, (size_t)c->Wk.max_smp * sizeof(uint2)));
     HIPCHK(c, hipMalloc(&c->Wk.active, (size_t)c->Wk.max_active * sizeof(uint32_t)));
     HIPCHK(c, hipMalloc(&c->G, sizeof(Globals)));
     HIPCHK(c, hipMalloc(&c->d_stage, c->batch_points * 3 * sizeof(float)));

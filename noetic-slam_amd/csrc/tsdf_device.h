@@ -12,14 +12,14 @@
 //           cnt[cap]   u32  this batch's (ray, brick) pair count (written by k_compact)
 //           toff[cap]  u32  this batch's ray-record segment offset
 //           touched[cap] u32  1 if the batch touches the brick (k_count sets, k_compact clears)
-//           cell[cap * cell_stride] u32  per (brick, scan) pair counts, then their prefix
+//           cell[cap * cell_stride] u32  per (brick, scan) SAMPLE counts, then their prefix
 //   Pool    sdf[max_bricks][512] f32, weight[max_bricks][512] f32 — voxel l = z*64 + y*8 + x;
 //           brick_keys[max_bricks] u64 (slot -> key, for export)
 //   Work    pair[max_batch_points * maxp] u32    per-ray pair codes (see PAIR_*)
 //           blk[n_blocks * HCAP] uint2          per-block local brick table (tidx, cell base)
 //           fb[..] uint4                        fallback pairs (block's LDS hash full)
-//           rec[pairs] float4                   per-brick, scan-ordered ray records:
-//                                               (x, y, z, in-brick sample count)
+//           smp[..] uint2                       the batch's samples: (sdf bits, scan << 9 | voxel),
+//                                               per brick contiguous and scan-ordered
 //           active[..] u32                      bricks touched by the batch
 #pragma once
 #include <hip/hip_runtime.h>
@@ -41,12 +41,19 @@ constexpr int HCAP = 2048;             // LDS brick-hash slots per k_count block
 constexpr int LDS_PROBES = 64;         // probe limit before a pair takes the global fallback
 constexpr int MAX_IN_BRICK = 22;       // a line visits at most 8+8+8-2 voxels of an 8^3 brick
 
-// pair codes (one u32 per (ray, k-th brick) slot)
-//   local:    bit 31 = 0 | count << 26 | lid << 10 | lrank   (lid < HCAP, lrank < RPB)
-//   fallback: bit 31 = 1 | count << 26 | fb index            (fb index < 2^26)
+// pair codes (one u32 per (ray, k-th brick) slot); count = the pair's in-brick samples
+//   local:    bit 31 = 0 | count << 26 | lid << 15 | local sample offset  (lid < HCAP,
+//             offset < RPB * MAX_IN_BRICK < 2^15)
+//   fallback: bit 31 = 1 | count << 26 | fb index                         (fb index < 2^26)
+//   dead:     PAIR_DEAD (the pair was dropped on a capacity overflow; keeps k_place's pair index
+//             aligned with k_count's)
 //   none:     NO_PAIR
 constexpr uint32_t PAIR_FB = 0x80000000u;
+constexpr uint32_t PAIR_DEAD = 0xFFFFFFFEu;  // count field 31: never a real pair
 constexpr int PAIR_CNT_SHIFT = 26;
+constexpr int PAIR_LID_SHIFT = 15;
+static_assert(RPB * MAX_IN_BRICK < (1 << PAIR_LID_SHIFT), "local sample offset overflows");
+static_assert(HCAP <= (1 << (PAIR_CNT_SHIFT - PAIR_LID_SHIFT)), "lid overflows");
 
 // overflow bits (sticky until tsdf_sync reads them)
 constexpr uint32_t OVF_TABLE = 1u, OVF_POOL = 2u, OVF_PAIRS = 4u, OVF_ACTIVE = 8u, OVF_FB = 16u;
@@ -90,12 +97,12 @@ struct Work {
     uint2* blk;      // n_blocks * HCAP
     uint32_t* blk_occ;  // n_blocks * HCAP/32 occupancy bits
     uint4* fb;       // fallback pairs: (tidx, scan, rank, 0)
-    float4* rec;
+    uint2* smp;  // x = truncated sdf (f32 bits), y = scan << 9 | local voxel
     uint32_t* active;
     uint32_t maxp;        // pair slots per ray
     uint32_t max_active;  // capacity of `active`
     uint32_t max_fb;      // capacity of `fb`
-    uint32_t max_rec;     // capacity of `rec`
+    uint32_t max_smp;     // capacity of smp
 };
 
 // per-batch counters, double-buffered by batch parity (k_count zeroes the other set)

@@ -107,22 +107,26 @@ __global__ __launch_bounds__(CNT_THREADS) void k_count(const float* __restrict__
                     return;
                 }
                 const int lid = lds_insert(s_key, bkey);
-                if (lid >= 0) {
-                    const uint32_t lr = atomicAdd(&s_cnt[lid], 1u);  // < RPB: one pair per ray
-                    pc[k++] = (cnt_in << PAIR_CNT_SHIFT) | ((uint32_t)lid << 10) | lr;
+                if (lid >= 0) {  // local sample offset < RPB * MAX_IN_BRICK
+                    const uint32_t lr = atomicAdd(&s_cnt[lid], cnt_in);
+                    pc[k++] = (cnt_in << PAIR_CNT_SHIFT) | ((uint32_t)lid << PAIR_LID_SHIFT) | lr;
                     return;
                 }
                 // LDS hash full: this pair takes the global path
                 const uint32_t f = atomicAdd(&C->n_fb, 1u);
                 if (f >= Wk.max_fb) {
                     atomicOr(&G->overflow, OVF_FB);
+                    pc[k++] = PAIR_DEAD;
                     return;
                 }
                 const int64_t hx = table_insert(T, bkey, &G->overflow);
-                if (hx < 0) return;
+                if (hx < 0) {
+                    pc[k++] = PAIR_DEAD;
+                    return;
+                }
                 const uint32_t h = (uint32_t)hx;
                 T.touched[h] = 1u;
-                const uint32_t rk = atomicAdd(&T.cell[(size_t)h * T.cell_stride + t], 1u);
+                const uint32_t rk = atomicAdd(&T.cell[(size_t)h * T.cell_stride + t], cnt_in);
                 Wk.fb[f] = make_uint4(h, t, rk, 0u);
                 pc[k++] = PAIR_FB | (cnt_in << PAIR_CNT_SHIFT) | f;
             };
@@ -259,6 +263,7 @@ __global__ __launch_bounds__(CMP_THREADS) void k_compact(uint32_t n_scans, Table
             base_a = tot_a ? atomicAdd(&C->n_active, tot_a) : 0u;
             base_c = tot_c ? atomicAdd(&C->cursor, tot_c) : 0u;
             base_n = tot_n ? atomicAdd(&G->pool_count, tot_n) : 0u;
+            if ((unsigned long long)base_c + tot_c > Wk.max_smp) atomicOr(&G->overflow, OVF_PAIRS);
         }
         __syncthreads();
         if (hit) {
@@ -281,10 +286,13 @@ __global__ __launch_bounds__(CMP_THREADS) void k_compact(uint32_t n_scans, Table
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_place: ray records into the bricks' scan-ordered segments
+// k_place: every ray walks its DDA once more (same workgroups as k_count, so rays are read
+// coalesced and lanes stay busy) and writes each gated sample (truncated sdf, local voxel) to its
+// brick's segment: segment start + (brick, scan) cell prefix + the workgroup's cell base + the
+// pair's local sample offset.  Samples are therefore per-brick contiguous and scan-ordered.
 
 __global__ __launch_bounds__(CNT_THREADS) void k_place(const float* __restrict__ xyz, BatchDesc D,
-                                                      Table T, Work Wk) {
+                                                      RayConst R, Table T, Work Wk) {
     __shared__ uint32_t s_base[HCAP];
     uint32_t t, r0, r1;
     block_range(D, blockIdx.x, t, r0, r1);
@@ -300,25 +308,46 @@ __global__ __launch_bounds__(CNT_THREADS) void k_place(const float* __restrict__
         s_base[slot] = b;
     }
     __syncthreads();
+    const float ox = D.ox[t], oy = D.oy[t], oz = D.oz[t];
     const uint32_t maxp = Wk.maxp;
     for (uint32_t i = r0 + threadIdx.x; i < r1; i += CNT_THREADS) {
         const uint32_t* pc = Wk.pair + (size_t)i * maxp;
-        const float px = xyz[3 * (size_t)i], py = xyz[3 * (size_t)i + 1],
-                    pz = xyz[3 * (size_t)i + 2];
-        for (uint32_t k = 0; k < maxp; k++) {
-            const uint32_t code = pc[k];
-            if (code == NO_PAIR) break;
-            const uint32_t cnt_in = (code >> PAIR_CNT_SHIFT) & 31u;
-            uint32_t pos;
-            if (code & PAIR_FB) {
-                const uint4 f = Wk.fb[code & ((1u << PAIR_CNT_SHIFT) - 1u)];
-                pos = T.toff[f.x] + T.cell[(size_t)f.x * T.cell_stride + f.y] + f.z;
-            } else {
-                const uint32_t b = s_base[(code >> 10) & (HCAP - 1)];
-                if (b == NO_PAIR) continue;
-                pos = b + (code & 1023u);
+        RayState r;
+        if (!ray_init(R, ox, oy, oz, xyz[3 * (size_t)i], xyz[3 * (size_t)i + 1],
+                      xyz[3 * (size_t)i + 2], r))
+            continue;
+        uint64_t cur = EMPTY_KEY;
+        uint32_t k = 0, pos = NO_PAIR, cnt = 0, w = 0;
+        for (int it = 0; it < MAX_DDA_STEPS; it++) {
+            float s;
+            if (voxel_sample(R, ox, oy, oz, r, s)) {
+                const uint64_t key = brick_key_of(r.vx, r.vy, r.vz);
+                if (key != cur) {  // the ray's next pair, in k_count's order
+                    cur = key;
+                    const uint32_t code = k < maxp ? pc[k] : NO_PAIR;
+                    k++;
+                    pos = NO_PAIR;
+                    cnt = 0;
+                    w = 0;
+                    if (code != NO_PAIR && code != PAIR_DEAD) {
+                        cnt = (code >> PAIR_CNT_SHIFT) & 31u;
+                        if (code & PAIR_FB) {
+                            const uint4 f = Wk.fb[code & ((1u << PAIR_CNT_SHIFT) - 1u)];
+                            pos = T.toff[f.x] + T.cell[(size_t)f.x * T.cell_stride + f.y] + f.z;
+                        } else {
+                            const uint32_t b =
+                                s_base[(code >> PAIR_LID_SHIFT) & (HCAP - 1)];
+                            if (b != NO_PAIR) pos = b + (code & ((1u << PAIR_LID_SHIFT) - 1u));
+                        }
+                    }
+                }
+                if (pos != NO_PAIR && w < cnt && pos + w < Wk.max_smp) {
+                    const uint32_t l = ((r.vz & 7) << 6) | ((r.vy & 7) << 3) | (r.vx & 7);
+                    Wk.smp[pos + w] = make_uint2(__float_as_uint(s), (t << 9) | l);
+                }
+                w++;
             }
-            if (pos < Wk.max_rec) Wk.rec[pos] = make_float4(px, py, pz, __uint_as_float(cnt_in));
+            if (!ray_step(r)) break;
         }
     }
 }
@@ -428,7 +457,7 @@ hipError_t launch_batch(const float* d_xyz, const BatchDesc& D, const RayConst& 
                                                                                 G, parity);
     if (timer) timer->end(KIND_COMPACT, st);
     if (timer) timer->begin(KIND_PLACE, st);
-    k_place<<<D.n_blocks, CNT_THREADS, 0, st>>>(d_xyz, D, T, Wk);
+    k_place<<<D.n_blocks, CNT_THREADS, 0, st>>>(d_xyz, D, R, T, Wk);
     if (timer) timer->end(KIND_PLACE, st);
     if (timer) timer->begin(KIND_INTEGRATE, st);
     hipError_t e = hipGetLastError();
