@@ -297,7 +297,7 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
     HIPCHK(c, hipMalloc(&c->Wk.blk_occ, (size_t)c->max_blocks * (HCAP / 32) * sizeof(uint32_t)));
     HIPCHK(c, hipMalloc(&c->Wk.fb, (size_t)c->Wk.max_fb * sizeof(uint4)));
     HIPCHK(c, hipMalloc(&c->Wk.smp, (size_t)c->Wk.max_smp * sizeof(uint2)));
-    HIPCHK(c, hipMalloc(&c->Wk.active, (size_t)c->Wk.max_active * sizeof(uint32_t)));
+    HIPCHK(c, hipMalloc(&c->Wk.active, (size_t)c->Wk.max_active * sizeof(uint4)));
     HIPCHK(c, hipMalloc(&c->G, sizeof(Globals)));
     HIPCHK(c, hipMalloc(&c->d_stage, c->batch_points * 3 * sizeof(float)));
     for (int i = 0; i < 2; i++) {

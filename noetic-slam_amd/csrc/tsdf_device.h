@@ -20,7 +20,8 @@
 //           fb[..] uint4                        fallback pairs (block's LDS hash full)
 //           smp[..] uint2                       the batch's samples: (sdf bits, scan << 9 | voxel),
 //                                               per brick contiguous and scan-ordered
-//           active[..] u32                      bricks touched by the batch
+//           active[..] uint4                    bricks touched by the batch: (table index, pool
+//                                               slot, sample segment offset, sample count)
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -98,7 +99,7 @@ struct Work {
     uint32_t* blk_occ;  // n_blocks * HCAP/32 occupancy bits
     uint4* fb;       // fallback pairs: (tidx, scan, rank, 0)
     uint2* smp;  // x = truncated sdf (f32 bits), y = scan << 9 | local voxel
-    uint32_t* active;
+    uint4* active;  // (h, slot, toff, cnt) per active brick (k_compact)
     uint32_t maxp;        // pair slots per ray
     uint32_t max_active;  // capacity of `active`
     uint32_t max_fb;      // capacity of `fb`

@@ -267,19 +267,20 @@ __global__ __launch_bounds__(CMP_THREADS) void k_compact(uint32_t n_scans, Table
         }
         __syncthreads();
         if (hit) {
-            if (base_a + ea < Wk.max_active) Wk.active[base_a + ea] = h;
-            else atomicOr(&G->overflow, OVF_ACTIVE);
             T.toff[h] = base_c + ec;
+            uint32_t slot = isnew ? base_n + en : T.slots[h];
             if (isnew) {
-                const uint32_t slot = base_n + en;
                 if (slot < T.max_bricks) {
-                    T.slots[h] = slot;
                     T.brick_keys[slot] = T.keys[h];
                 } else {
-                    T.slots[h] = INVALID_SLOT;
+                    slot = INVALID_SLOT;
                     atomicOr(&G->overflow, OVF_POOL);
                 }
+                T.slots[h] = slot;
             }
+            // k_integrate's whole per-brick header in one record
+            if (base_a + ea < Wk.max_active) Wk.active[base_a + ea] = make_uint4(h, slot, base_c + ec, n);
+            else atomicOr(&G->overflow, OVF_ACTIVE);
         }
         __syncthreads();
     }
@@ -341,6 +342,9 @@ __global__ __launch_bounds__(CNT_THREADS) void k_place(const float* __restrict__
                         }
                     }
                 }
+#ifdef TSDF_ABLATE_PLACE_NOWRITE
+                if (s == -1e30f)
+#endif
                 if (pos != NO_PAIR && w < cnt && pos + w < Wk.max_smp) {
                     const uint32_t l = ((r.vz & 7) << 6) | ((r.vy & 7) << 3) | (r.vx & 7);
                     Wk.smp[pos + w] = make_uint2(__float_as_uint(s), (t << 9) | l);

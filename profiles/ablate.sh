@@ -1,10 +1,10 @@
 #!/bin/bash
-# Timing shares of k_integrate's phases: the bench (kernel times from HIP events) on the real build
+# Timing shares of the batch kernels' phases: the bench (kernel times from HIP events) on the real build
 # and on the diagnostic builds of `make -C noetic-slam_amd/csrc ablate`.
 set -e
 OUT=${1:-gpurun_out/ablate}
 mkdir -p "$OUT"
-for v in real WALK OWN; do
+for v in ${VARIANTS:-real PLACE_NOWRITE INT_NOATOM INT_NOFUSE}; do
   lib=""
   [ "$v" != real ] && lib="noetic-slam_amd/lib/ablate/libtsdf_hip_$v.so"
   TSDF_HIP_LIB=$lib timeout -k 10 300 python3 bench.py --steps 4 --warmup 1 --no-cpu > "$OUT/$v.json"

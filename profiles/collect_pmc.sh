@@ -11,7 +11,8 @@ i=0
 for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS" \
            "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES" \
            "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum TCC_EA0_ATOMIC_sum" \
-           "SQ_INSTS_FLAT SQ_LDS_BANK_CONFLICT SQ_INSTS_SMEM"; do
+           "SQ_INSTS_FLAT SQ_LDS_BANK_CONFLICT SQ_INSTS_SMEM" \
+           "SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $grp --kernel-include-regex "tsdf::" --output-format csv -d "$OUT/p$i" -o pmc -- $CMD \
     > "$OUT/p$i.log" 2>&1 || { echo "pass $i ($grp) failed"; tail -5 "$OUT/p$i.log"; }
