@@ -293,7 +293,7 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
     HIPCHK(c, hipMalloc(&c->Pl.sdf, p->max_bricks * BRICK_VOX * sizeof(float)));
     HIPCHK(c, hipMalloc(&c->Pl.weight, p->max_bricks * BRICK_VOX * sizeof(float)));
     HIPCHK(c, hipMalloc(&c->Wk.pair, slots * sizeof(uint32_t)));
-    HIPCHK(c, hipMalloc(&c->Wk.blk, (size_t)c->max_blocks * HCAP * sizeof(uint2)));
+    HIPCHK(c, hipMalloc(&c->Wk.blk, (size_t)c->max_blocks * HCAP * sizeof(uint4)));
     HIPCHK(c, hipMalloc(&c->Wk.blk_occ, (size_t)c->max_blocks * (HCAP / 32) * sizeof(uint32_t)));
     HIPCHK(c, hipMalloc(&c->Wk.fb, (size_t)c->Wk.max_fb * sizeof(uint4)));
     HIPCHK(c, hipMalloc(&c->Wk.smp, (size_t)c->Wk.max_smp * sizeof(uint2)));

@@ -16,7 +16,8 @@
 //   Pool    sdf[max_bricks][512] f32, weight[max_bricks][512] f32 — voxel l = z*64 + y*8 + x;
 //           brick_keys[max_bricks] u64 (slot -> key, for export)
 //   Work    pair[max_batch_points * maxp] u32    per-ray pair codes (see PAIR_*)
-//           blk[n_blocks * HCAP] uint2          per-block local brick table (tidx, cell base)
+//           blk[n_blocks * HCAP] uint4          per-block local brick table (tidx, cell base,
+//                                               offset of the run in the block, run samples)
 //           fb[..] uint4                        fallback pairs (block's LDS hash full)
 //           smp[..] uint2                       the batch's samples: (sdf bits, scan << 9 | voxel),
 //                                               per brick contiguous and scan-ordered
@@ -95,7 +96,7 @@ struct Pool {
 
 struct Work {
     uint32_t* pair;
-    uint2* blk;      // n_blocks * HCAP
+    uint4* blk;      // n_blocks * HCAP: (table index, cell base, run offset, run samples)
     uint32_t* blk_occ;  // n_blocks * HCAP/32 occupancy bits
     uint4* fb;       // fallback pairs: (tidx, scan, rank, 0)
     uint2* smp;  // x = truncated sdf (f32 bits), y = scan << 9 | local voxel

@@ -77,6 +77,7 @@ __global__ __launch_bounds__(CNT_THREADS) void k_count(const float* __restrict__
     __shared__ uint32_t s_cnt[HCAP];
     __shared__ uint32_t s_occ[HCAP / 32];
     __shared__ unsigned long long red[2][CNT_THREADS / 64];
+    __shared__ uint32_t s_wsum[CNT_THREADS / 64];
     Counters* C = &G->ctr[parity];
     if (blockIdx.x == 0 && threadIdx.x < sizeof(Counters) / 4)
         reinterpret_cast<uint32_t*>(&G->ctr[parity ^ 1])[threadIdx.x] = 0u;  // next batch's set
@@ -153,19 +154,46 @@ __global__ __launch_bounds__(CNT_THREADS) void k_count(const float* __restrict__
     __syncthreads();
     // one global find-or-insert + one atomic per distinct brick of the workgroup: the cell
     // (brick, scan) count reserves the workgroup's ranks; `touched` (a plain store) lists the brick
-    // for k_compact, which also derives the brick's total from its cells
-    uint2* bt = Wk.blk + (size_t)blockIdx.x * HCAP;
-    for (int slot = threadIdx.x; slot < HCAP; slot += CNT_THREADS) {
+    // for k_compact, which also derives the brick's total from its cells.  Each thread takes
+    // HCAP / CNT_THREADS consecutive slots; a block scan over their sample counts gives every run
+    // its offset in the workgroup's sample order (k_place stages the samples in that order).
+    constexpr int SPT = HCAP / CNT_THREADS;
+    uint4* bt = Wk.blk + (size_t)blockIdx.x * HCAP;
+    uint32_t run_sum = 0;
+#pragma unroll
+    for (int j = 0; j < SPT; j++) {
+        const int slot = threadIdx.x * SPT + j;
+        run_sum += s_key[slot] != EMPTY_KEY ? s_cnt[slot] : 0u;
+    }
+    uint32_t run_off;
+    {
+        const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+        uint32_t incl = run_sum;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(incl, d, 64);
+            if (lane >= d) incl += y;
+        }
+        if (lane == 63) s_wsum[wid] = incl;
+        __syncthreads();
+        run_off = incl - run_sum;
+        for (int w = 0; w < wid; w++) run_off += s_wsum[w];
+    }
+#pragma unroll 1
+    for (int j = 0; j < SPT; j++) {
+        const int slot = threadIdx.x * SPT + j;
         const uint64_t key = s_key[slot];
         if (key == EMPTY_KEY) continue;
         const uint32_t n = s_cnt[slot];
         const int64_t hx = table_insert(T, key, &G->overflow);
-        uint2 e = make_uint2(NO_PAIR, 0u);
+        uint4 e = make_uint4(NO_PAIR, 0u, run_off, n);
         if (hx >= 0) {
             const uint32_t h = (uint32_t)hx;
             T.touched[h] = 1u;
-            e = make_uint2(h, atomicAdd(&T.cell[(size_t)h * T.cell_stride + t], n));
+            e.x = h;
+            e.y = atomicAdd(&T.cell[(size_t)h * T.cell_stride + t], n);
         }
+        run_off += n;
         bt[slot] = e;
         atomicOr(&s_occ[slot >> 5], 1u << (slot & 31));
     }
@@ -287,38 +315,54 @@ __global__ __launch_bounds__(CMP_THREADS) void k_compact(uint32_t n_scans, Table
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_place: every ray walks its DDA once more (same workgroups as k_count, so rays are read
-// coalesced and lanes stay busy) and writes each gated sample (truncated sdf, local voxel) to its
-// brick's segment: segment start + (brick, scan) cell prefix + the workgroup's cell base + the
-// pair's local sample offset.  Samples are therefore per-brick contiguous and scan-ordered.
+// k_place: every ray walks its DDA once more (one lane per ray, the same ray ranges as k_count's
+// workgroups) and produces each gated sample (truncated sdf, local voxel) for its brick's segment:
+// segment start + (brick, scan) cell prefix + the workgroup's run base + the pair's local offset.
+// Samples are therefore per-brick contiguous and scan-ordered.  Scattered 8-byte stores cost ~4x
+// their bytes in HBM writes, so the workgroup stages its samples in LDS in run order (run offsets
+// from k_count's block scan) and then copies each (brick) run out as one contiguous write; samples
+// past the staging capacity, and fallback pairs, are stored directly.
 
-__global__ __launch_bounds__(CNT_THREADS) void k_place(const float* __restrict__ xyz, BatchDesc D,
+constexpr int PLC_THREADS = RPB;      // one ray per lane
+constexpr int PLC_STAGE = 10112;      // staged samples per workgroup (6 B each; 2 workgroups per CU)
+
+__global__ __launch_bounds__(PLC_THREADS) void k_place(const float* __restrict__ xyz, BatchDesc D,
                                                       RayConst R, Table T, Work Wk) {
-    __shared__ uint32_t s_base[HCAP];
+    __shared__ uint32_t s_base[HCAP];    // run -> first sample of the run in the brick segment
+    __shared__ uint16_t s_loff[HCAP];    // run -> offset in the workgroup's sample order
+    __shared__ uint32_t s_runs[HCAP];    // occupied runs: slot | count << 11
+    __shared__ float st_s[PLC_STAGE];    // staged samples
+    __shared__ uint16_t st_l[PLC_STAGE];
+    __shared__ uint32_t s_nruns;
     uint32_t t, r0, r1;
     block_range(D, blockIdx.x, t, r0, r1);
-    const uint2* bt = Wk.blk + (size_t)blockIdx.x * HCAP;
+    const uint4* bt = Wk.blk + (size_t)blockIdx.x * HCAP;
     const uint32_t* occ = Wk.blk_occ + (size_t)blockIdx.x * (HCAP / 32);
-    for (int slot = threadIdx.x; slot < HCAP; slot += CNT_THREADS) {
-        uint32_t b = NO_PAIR;
+    if (threadIdx.x == 0) s_nruns = 0u;
+    __syncthreads();
+    for (int slot = threadIdx.x; slot < HCAP; slot += PLC_THREADS) {
         if ((occ[slot >> 5] >> (slot & 31)) & 1u) {
-            const uint2 e = bt[slot];
-            if (e.x != NO_PAIR)
-                b = T.toff[e.x] + T.cell[(size_t)e.x * T.cell_stride + t] + e.y;
+            const uint4 e = bt[slot];
+            uint32_t b = NO_PAIR;
+            if (e.x != NO_PAIR) b = T.toff[e.x] + T.cell[(size_t)e.x * T.cell_stride + t] + e.y;
+            s_base[slot] = b;
+            // runs starting past the staging capacity are stored directly (0xFFFF: not staged)
+            s_loff[slot] = e.z < (uint32_t)PLC_STAGE ? (uint16_t)e.z : (uint16_t)0xFFFFu;
+            if (b != NO_PAIR && e.z < (uint32_t)PLC_STAGE)
+                s_runs[atomicAdd(&s_nruns, 1u)] = (uint32_t)slot | (e.w << 11);
         }
-        s_base[slot] = b;
     }
     __syncthreads();
     const float ox = D.ox[t], oy = D.oy[t], oz = D.oz[t];
     const uint32_t maxp = Wk.maxp;
-    for (uint32_t i = r0 + threadIdx.x; i < r1; i += CNT_THREADS) {
+    const uint32_t i = r0 + threadIdx.x;
+    RayState r;
+    if (i < r1 && ray_init(R, ox, oy, oz, xyz[3 * (size_t)i], xyz[3 * (size_t)i + 1],
+                           xyz[3 * (size_t)i + 2], r)) {
         const uint32_t* pc = Wk.pair + (size_t)i * maxp;
-        RayState r;
-        if (!ray_init(R, ox, oy, oz, xyz[3 * (size_t)i], xyz[3 * (size_t)i + 1],
-                      xyz[3 * (size_t)i + 2], r))
-            continue;
         uint64_t cur = EMPTY_KEY;
-        uint32_t k = 0, pos = NO_PAIR, cnt = 0, w = 0;
+        // current pair: global position, or staging position (lpos < PLC_STAGE)
+        uint32_t k = 0, pos = NO_PAIR, lpos = NO_PAIR, cnt = 0, w = 0;
         for (int it = 0; it < MAX_DDA_STEPS; it++) {
             float s;
             if (voxel_sample(R, ox, oy, oz, r, s)) {
@@ -328,6 +372,7 @@ __global__ __launch_bounds__(CNT_THREADS) void k_place(const float* __restrict__
                     const uint32_t code = k < maxp ? pc[k] : NO_PAIR;
                     k++;
                     pos = NO_PAIR;
+                    lpos = NO_PAIR;
                     cnt = 0;
                     w = 0;
                     if (code != NO_PAIR && code != PAIR_DEAD) {
@@ -336,22 +381,41 @@ __global__ __launch_bounds__(CNT_THREADS) void k_place(const float* __restrict__
                             const uint4 f = Wk.fb[code & ((1u << PAIR_CNT_SHIFT) - 1u)];
                             pos = T.toff[f.x] + T.cell[(size_t)f.x * T.cell_stride + f.y] + f.z;
                         } else {
-                            const uint32_t b =
-                                s_base[(code >> PAIR_LID_SHIFT) & (HCAP - 1)];
-                            if (b != NO_PAIR) pos = b + (code & ((1u << PAIR_LID_SHIFT) - 1u));
+                            const uint32_t slot = (code >> PAIR_LID_SHIFT) & (HCAP - 1);
+                            const uint32_t b = s_base[slot];
+                            const uint32_t lr = code & ((1u << PAIR_LID_SHIFT) - 1u);
+                            if (b != NO_PAIR) {
+                                pos = b + lr;
+                                const uint32_t lo = s_loff[slot];
+                                if (lo != 0xFFFFu) lpos = lo + lr;
+                            }
                         }
                     }
                 }
-#ifdef TSDF_ABLATE_PLACE_NOWRITE
-                if (s == -1e30f)
-#endif
-                if (pos != NO_PAIR && w < cnt && pos + w < Wk.max_smp) {
+                if (w < cnt) {
                     const uint32_t l = ((r.vz & 7) << 6) | ((r.vy & 7) << 3) | (r.vx & 7);
-                    Wk.smp[pos + w] = make_uint2(__float_as_uint(s), (t << 9) | l);
+                    if (lpos != NO_PAIR && lpos + w < (uint32_t)PLC_STAGE) {
+                        st_s[lpos + w] = s;
+                        st_l[lpos + w] = (uint16_t)l;
+                    } else if (pos != NO_PAIR && pos + w < Wk.max_smp) {
+                        Wk.smp[pos + w] = make_uint2(__float_as_uint(s), (t << 9) | l);
+                    }
                 }
                 w++;
             }
             if (!ray_step(r)) break;
+        }
+    }
+    __syncthreads();
+    // copy-out: one wave per run, contiguous stores
+    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nr = s_nruns;
+    for (uint32_t q = wid; q < nr; q += PLC_THREADS / 64) {
+        const uint32_t e = s_runs[q], slot = e & (HCAP - 1), n = e >> 11;
+        const uint32_t b = s_base[slot], lo = s_loff[slot];
+        const uint32_t m = min(n, (uint32_t)PLC_STAGE - lo);  // the staged part of the run
+        for (uint32_t j = lane; j < m; j += 64) {
+            if (b + j < Wk.max_smp)
+                Wk.smp[b + j] = make_uint2(__float_as_uint(st_s[lo + j]), (t << 9) | st_l[lo + j]);
         }
     }
 }
@@ -461,7 +525,7 @@ hipError_t launch_batch(const float* d_xyz, const BatchDesc& D, const RayConst& 
                                                                                 G, parity);
     if (timer) timer->end(KIND_COMPACT, st);
     if (timer) timer->begin(KIND_PLACE, st);
-    k_place<<<D.n_blocks, CNT_THREADS, 0, st>>>(d_xyz, D, R, T, Wk);
+    k_place<<<D.n_blocks, PLC_THREADS, 0, st>>>(d_xyz, D, R, T, Wk);
     if (timer) timer->end(KIND_PLACE, st);
     if (timer) timer->begin(KIND_INTEGRATE, st);
     hipError_t e = hipGetLastError();
