@@ -122,33 +122,38 @@ def main():
     value = total_scans / elapsed
 
     # ---- roofline of the dominant kernel (per-launch means, this rank) -------------------------
-    # One launch = one batch of scans.  Algorithmic bytes of a batch: every valid
-    # ray's xyz read once (12 B) + every voxel the batch updates read and written once (8 + 8 B).
-    # The per-scan figure of SURVEY.md §8d (12 N + 16 U_vox per scan) is reported beside it.
+    # One launch = one batch of scans.  Algorithmic bytes: per scan
+    # B_scan = 12 N_valid + 16 U_vox (every valid ray's xyz read once, every voxel the scan updates
+    # read and written once as (S, W) f32), times the scans one launch integrates.  Also reported:
+    # the batch-deduplicated figure (a voxel updated by several scans of one batch counted once),
+    # which is what the batched pipeline must move at minimum.
     n_batches = max(1, st["n_batches"])
     n_scans_rank = max(1, st["n_scans"])
     rays_per_scan = st["n_rays_total"] / n_scans_rank
     uvox_per_scan = st["n_voxels_total"] / n_scans_rank
     bytes_per_scan = 12.0 * rays_per_scan + 16.0 * uvox_per_scan  # SURVEY.md §8d B_scan
-    bytes_per_batch = (12.0 * st["n_rays_total"] + 16.0 * st["n_dirty_total"]) / n_batches
+    scans_per_launch = n_scans_rank / n_batches
+    bytes_per_launch = bytes_per_scan * scans_per_launch
+    dedup_bytes_per_launch = (12.0 * st["n_rays_total"] + 16.0 * st["n_dirty_total"]) / n_batches
     kms = st["kernel_ms"]
     roofline = None
     kernel_ms_per_launch = {k: (kms[k] / max(1, st["kernel_launches"][k])) for k in kms}
     if not args.no_profile and sum(kms.values()) > 0:
         dom = max(kms, key=lambda k: kms[k])
         t_launch = kernel_ms_per_launch[dom] * 1e-3
-        achieved = bytes_per_batch / t_launch / 1e9
+        achieved = bytes_per_launch / t_launch / 1e9
         traffic = None
         try:
             with open(args.traffic_json) as f:
-                traffic = json.load(f).get(dom)
-        except (OSError, ValueError):
+                traffic = json.load(f)["bytes_per_launch"].get("k_" + dom)
+        except (OSError, ValueError, KeyError):
             traffic = None
         roofline = {"bound": "hbm", "kernel": "k_" + dom, "achieved": round(achieved, 2),
                     "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 5),
                     "traffic": traffic,
-                    "algorithmic_bytes_per_launch": round(bytes_per_batch),
-                    "scans_per_launch": round(n_scans_rank / n_batches, 2),
+                    "algorithmic_bytes_per_launch": round(bytes_per_launch),
+                    "dedup_bytes_per_launch": round(dedup_bytes_per_launch),
+                    "scans_per_launch": round(scans_per_launch, 2),
                     "avg_launch_ms": round(kernel_ms_per_launch[dom], 5)}
     path_ms_per_scan = sum(kernel_ms_per_launch.values()) * n_batches / n_scans_rank
 
@@ -168,18 +173,22 @@ def main():
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import oracle
         ov = oracle.OracleTSDFVolume(args.voxel, args.trunc)
-        x, offs, org = steps[args.warmup]
-        xs = x.cpu().numpy()
-        n_done, tc = 0, time.perf_counter()
-        for j in range(len(org)):
-            ov.integrate(xs[offs[j]:offs[j + 1]], org[j])
-            n_done += 1
+        n_done, tc, busy = 0, time.perf_counter(), 0.0
+        for i in range(args.warmup, n_steps):  # the timed steps' scans, in order, until the budget
+            x, offs, org = steps[i]
+            xs = x.cpu().numpy()
+            t1 = time.perf_counter()
+            for j in range(len(org)):
+                ov.integrate(xs[offs[j]:offs[j + 1]], org[j])
+                n_done += 1
+                if time.perf_counter() - tc > args.cpu_seconds:
+                    break
+            busy += time.perf_counter() - t1
             if time.perf_counter() - tc > args.cpu_seconds:
                 break
-        tc = time.perf_counter() - tc
-        cpu = {"value": round(n_done / tc, 4), "unit": "scans/s", "cores": 1, "kind": "port",
-               "sample": "%d scans of the first timed step, serial C oracle (scan-fused mode), "
-                         "same inputs" % n_done}
+        cpu = {"value": round(n_done / busy, 4), "unit": "scans/s", "cores": 1, "kind": "port",
+               "sample": "the first %d scans of the timed steps (%.1f s), serial C oracle "
+                         "(scan-fused mode), same inputs" % (n_done, busy)}
 
     if rank == 0:
         out = {

@@ -16,7 +16,7 @@ STATUS_NAMES = {
     TSDF_EHIP: "TSDF_EHIP", TSDF_ENODEV: "TSDF_ENODEV", TSDF_EOVERFLOW: "TSDF_EOVERFLOW",
 }
 
-KERNEL_KINDS = ("rays", "compact", "scatter", "integrate")
+KERNEL_KINDS = ("count", "compact", "place", "integrate")  # k_<kind>, KernelKind order
 
 
 class TsdfParams(C.Structure):
