@@ -90,10 +90,10 @@ typedef struct tsdf_stats {
 } tsdf_stats;
 
 /* kernel kinds reported in tsdf_stats.kernel_ms (profiling on) */
-#define TSDF_K_RAYS 0      /* ray walk + brick hash insert + (ray, brick) pair emission */
-#define TSDF_K_OFFSETS 1   /* per-brick ray-list segments, pool slots, per-scan cell prefix */
-#define TSDF_K_SCATTER 2   /* pair -> per-brick scan-ordered ray list */
-#define TSDF_K_INTEGRATE 3 /* per-brick LDS tile accumulate + in-order fuse into the field */
+#define TSDF_K_COUNT 0     /* k_count: ray walk, per-workgroup LDS brick hash, (ray, brick) pairs */
+#define TSDF_K_COMPACT 1   /* k_compact: per-brick sample segments, pool slots, per-scan prefix */
+#define TSDF_K_PLACE 2     /* k_place: second walk, samples staged in LDS, written per brick run */
+#define TSDF_K_INTEGRATE 3 /* k_integrate: per-brick live-cell accumulate + scan-ordered fuse */
 
 typedef struct tsdf_ctx tsdf_ctx;
 
