@@ -32,7 +32,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=32, help="scans per GPU per step")
+    ap.add_argument("--batch", type=int, default=64,
+                    help="scans per GPU per step (one GPU batch, <= 64; the field does not depend on it)")
     ap.add_argument("--voxel", type=float, default=0.05)
     ap.add_argument("--trunc", type=float, default=0.15)
     ap.add_argument("--cpu-seconds", type=float, default=15.0,

@@ -25,9 +25,13 @@
 namespace tsdf {
 
 constexpr int INT_THREADS = 256;
-constexpr int INT_PER = 8;                           // register-cached samples per thread
+#ifndef TSDF_INT_PER
+#define TSDF_INT_PER 4
+#endif
+constexpr int INT_PER = TSDF_INT_PER;                // register-cached samples per thread
 constexpr uint32_t INT_CAP = INT_PER * INT_THREADS;  // samples (>= live cells) per window
-constexpr int INT_BLOCKS_PER_CU = 4;                 // LDS ~34 KB per workgroup
+// LDS: 12 B per cell + ~9.5 KB per workgroup; residency as LDS allows
+constexpr int INT_BLOCKS_PER_CU = (160 * 1024) / (INT_CAP * 12 + 10 * 1024);
 constexpr uint32_t INT_MAX_WIN = 32;                 // scans per window (u32 masks)
 
 // Diagnostic build only (-DTSDF_PHASE_TIMING, never shipped): thread 0 of a few workgroups drains
@@ -58,7 +62,8 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchDesc D, Table T,
     // previous brick's prefix while another writes the next one
     __shared__ uint32_t s_csb[2][MAX_BATCH + 1];
     __shared__ uint32_t s_red[INT_THREADS / 64];
-    __shared__ uint32_t s_nlive, s_q;
+    __shared__ uint32_t s_nlive, s_q, s_ncell;
+    float2* cF = reinterpret_cast<float2*>(cA);  // P4: cells converted to (A 2^-32, B) as f32
     Counters* C = &G->ctr[parity];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const uint32_t n_active = min(C->n_active, Wk.max_active);
@@ -74,26 +79,62 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchDesc D, Table T,
     unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t_last = clock64();
     uint32_t nb = 0;
 #endif
-    for (uint32_t a = blockIdx.x; a < n_active; a += gridDim.x, par ^= 1u) {
+    // Software pipeline over the workgroup's bricks: while brick a is processed, brick a + G's
+    // cell row, (S, W) and first INT_CAP samples are in flight to registers (BrickRegs), and
+    // brick a + 2G's active record is loading.  A brick then starts with its data at hand.
+    struct BrickRegs {
+        uint2 c[INT_PER];
+        float s0, s1, w0, w1;
+        uint32_t cell;
+    };
+    auto load_brick = [&](const uint4& r, BrickRegs& B) {
+        const uint32_t n = r.w, base = r.z;
+        const bool has = r.y < T.max_bricks;
+#pragma unroll
+        for (int j = 0; j < INT_PER; j++) {
+            const uint32_t i = tid + j * INT_THREADS;
+            // base + i >= max_smp: capacity overflow (reported by k_compact)
+            B.c[j] = (i < n && base + i < Wk.max_smp) ? Wk.smp[base + i] : make_uint2(0u, ~0u);
+        }
+        B.cell = (uint32_t)tid < ns ? T.cell[(size_t)r.x * T.cell_stride + tid] : 0u;
+        const float* Sg = Pl.sdf + (size_t)(has ? r.y : 0) * BRICK_VOX;
+        const float* Wg = Pl.weight + (size_t)(has ? r.y : 0) * BRICK_VOX;
+        B.s0 = has ? Sg[tid] : tau;
+        B.s1 = has ? Sg[tid + 256] : tau;
+        B.w0 = has ? Wg[tid] : 0.0f;
+        B.w1 = has ? Wg[tid + 256] : 0.0f;
+    };
+    const uint32_t G0 = gridDim.x;
+    uint4 rec_next = blockIdx.x + G0 < n_active ? Wk.active[blockIdx.x + G0] : make_uint4(0u, 0u, 0u, 0u);
+    BrickRegs P;
+    if (blockIdx.x < n_active) load_brick(Wk.active[blockIdx.x], P);
+    uint4 rec = blockIdx.x < n_active ? Wk.active[blockIdx.x] : make_uint4(0u, 0u, 0u, 0u);
+    for (uint32_t a = blockIdx.x; a < n_active; a += G0, par ^= 1u) {
         uint32_t* s_cs = s_csb[par];
-        const uint4 rec = Wk.active[a];  // (h, slot, toff, n)
-        const uint32_t h = rec.x, n = rec.w, base = rec.z;
-        const bool has_slot = rec.y < T.max_bricks;
-        if ((uint32_t)tid < ns) s_cs[tid] = T.cell[(size_t)h * T.cell_stride + tid];
+        const uint4 cur = rec;  // (h, slot, toff, n)
+        const BrickRegs B = P;
+        rec = rec_next;
+        if (a + G0 < n_active) load_brick(rec, P);                     // brick a + G
+        if (a + 2 * G0 < n_active) rec_next = Wk.active[a + 2 * G0];  // record of a + 2G
+        const uint32_t h = cur.x, n = cur.w, base = cur.z;
+        uint2 c[INT_PER];
+#pragma unroll
+        for (int j = 0; j < INT_PER; j++) c[j] = B.c[j];
+        uint32_t cq = 0;  // samples [cq, cq + INT_CAP) are in c[] (uniform)
+        const bool has_slot = cur.y < T.max_bricks;
+        if ((uint32_t)tid < ns) s_cs[tid] = B.cell;
         if (tid == 0) s_cs[ns] = n;
-        float* Sg = Pl.sdf + (size_t)(has_slot ? rec.y : 0) * BRICK_VOX;
-        float* Wg = Pl.weight + (size_t)(has_slot ? rec.y : 0) * BRICK_VOX;
+        float* Sg = Pl.sdf + (size_t)(has_slot ? cur.y : 0) * BRICK_VOX;
+        float* Wg = Pl.weight + (size_t)(has_slot ? cur.y : 0) * BRICK_VOX;
         // sS / sW of voxels tid, tid + 256: the previous brick's last readers are past a barrier
-        sS[tid] = has_slot ? Sg[tid] : tau;
-        sS[tid + 256] = has_slot ? Sg[tid + 256] : tau;
-        sW[tid] = has_slot ? Wg[tid] : 0.0f;
-        sW[tid + 256] = has_slot ? Wg[tid + 256] : 0.0f;
+        sS[tid] = B.s0;
+        sS[tid + 256] = B.s1;
+        sW[tid] = B.w0;
+        sW[tid + 256] = B.w1;
         uint32_t dirty = 0;  // voxels 2 tid, 2 tid + 1 (bits 0, 1)
         PHASE(0);
         __syncthreads();  // s_cs, sS, sW visible
         PHASE(1);
-        uint2 c[INT_PER];
-        uint32_t cq = ~0u;  // samples [cq, cq + INT_CAP) are in c[] (uniform)
         for (uint32_t t0 = 0; t0 < ns;) {
             // window [t0, t1): as many scans as keep its samples <= INT_CAP (at least one)
             const uint32_t q0 = s_cs[t0];
@@ -111,7 +152,6 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchDesc D, Table T,
 #pragma unroll
                     for (int j = 0; j < INT_PER; j++) {
                         const uint32_t i = cq + tid + j * INT_THREADS;
-                        // base + i >= max_smp: capacity overflow (reported by k_compact)
                         c[j] = (i < n && base + i < Wk.max_smp) ? Wk.smp[base + i]
                                                                 : make_uint2(0u, ~0u);
                     }
@@ -120,7 +160,12 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchDesc D, Table T,
 #pragma unroll
                 for (int j = 0; j < INT_PER; j++) {
                     const uint32_t w = (c[j].y >> 9) - t0;
-                    if (w < nw) atomicOr(&sMask[c[j].y & 511u], 1u << w);
+#ifdef TSDF_ABLATE_INT_NOP1
+                    if (w < nw && c[j].x == 0x7FFFFFFFu)
+#else
+                    if (w < nw)
+#endif
+                        atomicOr(&sMask[c[j].y & 511u], 1u << w);
                 }
             }
             __syncthreads();
@@ -155,6 +200,7 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchDesc D, Table T,
                 if (v1) sLive[vb + v0] = (uint16_t)(2 * tid + 1);
                 if (tid == 0) {
                     s_nlive = tot >> 16;
+                    s_ncell = tot & 0xFFFFu;
                     s_q = 0u;
                     nvox += tot & 0xFFFFu;  // (voxel, scan) updates of the window
                 }
@@ -179,16 +225,37 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchDesc D, Table T,
                         const uint32_t l = c[j].y & 511u;
                         const uint32_t cell = sBase[l] + __popc(sMask[l] & ((1u << w) - 1u));
                         const long long fx = (long long)(__uint_as_float(c[j].x) * 4294967296.0f);
-                        atomicAdd(&cA[cell], (unsigned long long)fx);
-                        atomicAdd(&cB[cell], 1u);
+#ifdef TSDF_ABLATE_INT_NOP3
+                        if (fx == 12345)
+#endif
+                        {
+                            atomicAdd(&cA[cell], (unsigned long long)fx);
+                            atomicAdd(&cB[cell], 1u);
+                        }
                     }
                 }
             }
             __syncthreads();
             PHASE(5);
-            // P4: fuse, live voxels from a work queue; each lane runs one voxel's chain at a time
+            // P4a: convert every live cell to (A 2^-32, B) in f32, in parallel, so the serial
+            // per-voxel chains below are one LDS read, a multiply-add and a division per step
             {
+                const uint32_t ncell = s_ncell;
+                for (uint32_t j = tid; j < ncell; j += INT_THREADS) {
+                    const long long av = (long long)cA[j];
+                    const uint32_t bv = cB[j];
+                    cB[j] = 0u;
+                    cF[j] = make_float2((float)((double)av * (1.0 / 4294967296.0)), (float)bv);
+                }
+            }
+            __syncthreads();
+            // P4b: fuse, live voxels from a work queue; each lane runs one voxel's chain at a time
+            {
+#ifdef TSDF_ABLATE_INT_NOP4
+                const uint32_t nlive = 0;
+#else
                 const uint32_t nlive = s_nlive;
+#endif
                 uint32_t l = 0, cell = 0, rem = 0;
                 float s = 0.0f, wt = 0.0f;
                 while (true) {
@@ -203,12 +270,10 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchDesc D, Table T,
                         s = sS[l];
                         wt = sW[l];
                     }
-                    const float bf = (float)cB[cell];
-                    const float af = (float)((double)(long long)cA[cell] * (1.0 / 4294967296.0));
+                    const float2 v = cF[cell];
                     cA[cell] = 0ull;
-                    cB[cell] = 0u;
-                    const float nwt = wt + bf;
-                    s = (s * wt + af) / nwt;
+                    const float nwt = wt + v.y;
+                    s = (s * wt + v.x) / nwt;
                     wt = nwt;
                     cell++;
                     if (--rem == 0) {
@@ -260,9 +325,29 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchDesc D, Table T,
     }
 }
 
+// Grid = exactly the workgroups the device holds at once (CUs x resident workgroups per CU, from
+// the occupancy API: VGPRs or LDS, whichever binds): every workgroup of the grid-stride loop starts
+// at once, none waits for a second dispatch round.
+static int integrate_grid() {
+    static int grid = 0;
+    if (grid == 0) {
+        int dev = 0, cus = 0, per_cu = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_integrate, INT_THREADS, 0) !=
+                hipSuccess ||
+            cus <= 0 || per_cu <= 0) {
+            cus = 256;
+            per_cu = INT_BLOCKS_PER_CU;
+        }
+        grid = cus * per_cu;
+    }
+    return grid;
+}
+
 hipError_t launch_integrate(const BatchDesc& D, const RayConst& R, const Table& T, const Work& Wk,
                             const Pool& Pl, Globals* G, int parity, hipStream_t st) {
-    k_integrate<<<256 * INT_BLOCKS_PER_CU, INT_THREADS, 0, st>>>(D, T, Wk, Pl, G, parity, R.tau);
+    k_integrate<<<integrate_grid(), INT_THREADS, 0, st>>>(D, T, Wk, Pl, G, parity, R.tau);
     return hipGetLastError();
 }
 
