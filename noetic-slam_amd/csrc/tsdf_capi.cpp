@@ -249,6 +249,8 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
     c->R.min_range = (float)p->min_range;
     c->R.max_range = (float)p->max_range;
     c->R.carving = p->space_carving ? 1 : 0;
+    c->R.tau2_lo = (float)(((double)c->R.tau * (1.0 - 0x1p-20)) * ((double)c->R.tau * (1.0 - 0x1p-20)));
+    c->R.tau2_hi = (float)(((double)c->R.tau * (1.0 + 0x1p-20)) * ((double)c->R.tau * (1.0 + 0x1p-20)));
 
     // Points one batch may hold: max_batch full scans, unless the per-ray worst cases (pair slots,
     // sample slots — large with space carving) exceed the u32 index space or the sample budget;

@@ -64,6 +64,9 @@ constexpr uint32_t OVF_TABLE = 1u, OVF_POOL = 2u, OVF_PAIRS = 4u, OVF_ACTIVE = 8
 struct RayConst {
     float vs, inv_vs, tau, min_range, max_range;
     int carving;
+    // squared-distance bounds bracketing tau by 2^-20 relative: d2 < tau2_lo implies
+    // sqrt_rn(d2) < tau, d2 > tau2_hi implies sqrt_rn(d2) > tau (voxel_gate skips the sqrt)
+    float tau2_lo, tau2_hi;
 };
 
 // one batch: scan s = points [off[s], off[s+1]) seen from (ox[s], oy[s], oz[s]) (fp32);

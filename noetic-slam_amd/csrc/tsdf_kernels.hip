@@ -92,64 +92,113 @@ __global__ __launch_bounds__(CNT_THREADS) void k_count(const float* __restrict__
     const float ox = D.ox[t], oy = D.oy[t], oz = D.oz[t];
     const uint32_t maxp = Wk.maxp;
     uint32_t valid = 0, npairs = 0;
+    // The pair code of (ray, brick run): LDS-hash rank in the workgroup's run for the brick, or a
+    // fallback record when the LDS hash is full.  cnt_in = the pair's gated voxels (<= MAX_IN_BRICK).
+    auto pair_code = [&](uint64_t bkey, uint32_t cnt_in) -> uint32_t {
+        const int lid = lds_insert(s_key, bkey);
+        if (lid >= 0) {  // s_cnt: the run's samples; the pair's offset in it
+            const uint32_t lr = atomicAdd(&s_cnt[lid], cnt_in);
+            return (cnt_in << PAIR_CNT_SHIFT) | ((uint32_t)lid << PAIR_LID_SHIFT) | lr;
+        }
+        const uint32_t f = atomicAdd(&C->n_fb, 1u);  // LDS hash full: the global path
+        if (f >= Wk.max_fb) {
+            atomicOr(&G->overflow, OVF_FB);
+            return PAIR_DEAD;
+        }
+        const int64_t hx = table_insert(T, bkey, &G->overflow);
+        if (hx < 0) return PAIR_DEAD;
+        const uint32_t h = (uint32_t)hx;
+        T.touched[h] = 1u;
+        const uint32_t rk = atomicAdd(&T.cell[(size_t)h * T.cell_stride + t], cnt_in);
+        Wk.fb[f] = make_uint4(h, t, rk, 0u);
+        return PAIR_FB | (cnt_in << PAIR_CNT_SHIFT) | f;
+    };
     for (uint32_t i = r0 + threadIdx.x; i < r1; i += CNT_THREADS) {
         uint32_t* pc = Wk.pair + (size_t)i * maxp;
         uint32_t k = 0;
         RayState r;
-        if (ray_init(R, ox, oy, oz, xyz[3 * (size_t)i], xyz[3 * (size_t)i + 1],
-                     xyz[3 * (size_t)i + 2], r)) {
-            valid++;
-            // One pair per distinct brick; a line visits a brick in one contiguous run of DDA
-            // voxels, so the pair is closed when the next gated voxel's brick differs.  cnt_in =
-            // the pair's gated voxels (<= MAX_IN_BRICK), sizes k_integrate's sample buffer.
-            auto emit = [&](uint64_t bkey, uint32_t cnt_in) {
-                if (k >= maxp) {
-                    atomicOr(&G->overflow, OVF_PAIRS);
-                    return;
-                }
-                const int lid = lds_insert(s_key, bkey);
-                if (lid >= 0) {  // local sample offset < RPB * MAX_IN_BRICK
-                    const uint32_t lr = atomicAdd(&s_cnt[lid], cnt_in);
-                    pc[k++] = (cnt_in << PAIR_CNT_SHIFT) | ((uint32_t)lid << PAIR_LID_SHIFT) | lr;
-                    return;
-                }
-                // LDS hash full: this pair takes the global path
-                const uint32_t f = atomicAdd(&C->n_fb, 1u);
-                if (f >= Wk.max_fb) {
-                    atomicOr(&G->overflow, OVF_FB);
-                    pc[k++] = PAIR_DEAD;
-                    return;
-                }
-                const int64_t hx = table_insert(T, bkey, &G->overflow);
-                if (hx < 0) {
-                    pc[k++] = PAIR_DEAD;
-                    return;
-                }
-                const uint32_t h = (uint32_t)hx;
-                T.touched[h] = 1u;
-                const uint32_t rk = atomicAdd(&T.cell[(size_t)h * T.cell_stride + t], cnt_in);
-                Wk.fb[f] = make_uint4(h, t, rk, 0u);
-                pc[k++] = PAIR_FB | (cnt_in << PAIR_CNT_SHIFT) | f;
-            };
-            uint64_t cur = EMPTY_KEY;
-            uint32_t ccount = 0;
-            for (int it = 0; it < MAX_DDA_STEPS; it++) {
-                float s;
-                if (voxel_sample(R, ox, oy, oz, r, s)) {
-                    const uint64_t key = brick_key_of(r.vx, r.vy, r.vz);
-                    if (key != cur) {
-                        if (cur != EMPTY_KEY) emit(cur, ccount);
-                        cur = key;
-                        ccount = 0;
+        const bool ok = ray_init(R, ox, oy, oz, xyz[3 * (size_t)i], xyz[3 * (size_t)i + 1],
+                                 xyz[3 * (size_t)i + 2], r);
+        valid += ok ? 1u : 0u;
+        // One pair per distinct brick; a line visits a brick in one contiguous run of DDA voxels,
+        // so a pair closes when the next gated voxel's brick differs.
+        if (maxp <= 4) {
+            // Short rays (no carving): the walk only records its <= 4 pairs in registers; all lanes
+            // then emit pair j together, so the LDS hash work runs convergent, not once per lane.
+            uint64_t q0 = EMPTY_KEY, q1 = EMPTY_KEY, q2 = EMPTY_KEY, q3 = EMPTY_KEY;
+            uint32_t n0 = 0, n1 = 0, n2 = 0, n3 = 0, np = 0;
+            if (ok) {
+                uint64_t cur = EMPTY_KEY;
+                uint32_t ccount = 0;
+                for (int it = 0; it < MAX_DDA_STEPS; it++) {
+                    if (voxel_gate(R, ox, oy, oz, r)) {
+                        const uint64_t key = brick_key_of(r.vx, r.vy, r.vz);
+                        if (key != cur) {
+                            if (cur != EMPTY_KEY) {
+                                q0 = np == 0 ? cur : q0; n0 = np == 0 ? ccount : n0;
+                                q1 = np == 1 ? cur : q1; n1 = np == 1 ? ccount : n1;
+                                q2 = np == 2 ? cur : q2; n2 = np == 2 ? ccount : n2;
+                                q3 = np == 3 ? cur : q3; n3 = np == 3 ? ccount : n3;
+                                np++;
+                            }
+                            cur = key;
+                            ccount = 0;
+                        }
+                        ccount++;
                     }
-                    ccount++;
+                    if (!ray_step(r)) break;
                 }
-                if (!ray_step(r)) break;
+                if (cur != EMPTY_KEY) {
+                    q0 = np == 0 ? cur : q0; n0 = np == 0 ? ccount : n0;
+                    q1 = np == 1 ? cur : q1; n1 = np == 1 ? ccount : n1;
+                    q2 = np == 2 ? cur : q2; n2 = np == 2 ? ccount : n2;
+                    q3 = np == 3 ? cur : q3; n3 = np == 3 ? ccount : n3;
+                    np++;
+                }
             }
-            if (cur != EMPTY_KEY) emit(cur, ccount);
+            if (np > maxp) atomicOr(&G->overflow, OVF_PAIRS);  // beyond the geometric bound
+            k = min(np, maxp);
+            uint4 code = make_uint4(NO_PAIR, NO_PAIR, NO_PAIR, NO_PAIR);
+            if (k > 0) code.x = pair_code(q0, n0);
+            if (k > 1) code.y = pair_code(q1, n1);
+            if (k > 2) code.z = pair_code(q2, n2);
+            if (k > 3) code.w = pair_code(q3, n3);
+            if (maxp == 4) {
+                *reinterpret_cast<uint4*>(pc) = code;  // one 16-B store per ray
+            } else {
+                const uint32_t cv[4] = {code.x, code.y, code.z, code.w};
+#pragma unroll
+                for (uint32_t j = 0; j < 4; j++)
+                    if (j < maxp) pc[j] = cv[j];
+            }
+        } else {
+            if (ok) {
+                uint64_t cur = EMPTY_KEY;
+                uint32_t ccount = 0;
+                auto emit = [&](uint64_t bkey, uint32_t cnt_in) {
+                    if (k >= maxp) {
+                        atomicOr(&G->overflow, OVF_PAIRS);
+                        return;
+                    }
+                    pc[k++] = pair_code(bkey, cnt_in);
+                };
+                for (int it = 0; it < MAX_DDA_STEPS; it++) {
+                    if (voxel_gate(R, ox, oy, oz, r)) {
+                        const uint64_t key = brick_key_of(r.vx, r.vy, r.vz);
+                        if (key != cur) {
+                            if (cur != EMPTY_KEY) emit(cur, ccount);
+                            cur = key;
+                            ccount = 0;
+                        }
+                        ccount++;
+                    }
+                    if (!ray_step(r)) break;
+                }
+                if (cur != EMPTY_KEY) emit(cur, ccount);
+            }
+            for (uint32_t j = k; j < maxp; j++) pc[j] = NO_PAIR;
         }
         npairs += k;
-        for (uint32_t j = k; j < maxp; j++) pc[j] = NO_PAIR;
     }
     __syncthreads();
     // one global find-or-insert + one atomic per distinct brick of the workgroup: the cell
@@ -360,6 +409,47 @@ __global__ __launch_bounds__(PLC_THREADS) void k_place(const float* __restrict__
     if (i < r1 && ray_init(R, ox, oy, oz, xyz[3 * (size_t)i], xyz[3 * (size_t)i + 1],
                            xyz[3 * (size_t)i + 2], r)) {
         const uint32_t* pc = Wk.pair + (size_t)i * maxp;
+        // a pair code -> its samples' global position, staging position (lpos < PLC_STAGE), count
+        auto resolve = [&](uint32_t code, uint32_t& pos, uint32_t& lpos, uint32_t& cnt) {
+            pos = NO_PAIR;
+            lpos = NO_PAIR;
+            cnt = 0;
+            if (code == NO_PAIR || code == PAIR_DEAD) return;
+            cnt = (code >> PAIR_CNT_SHIFT) & 31u;
+            if (code & PAIR_FB) {
+                const uint4 f = Wk.fb[code & ((1u << PAIR_CNT_SHIFT) - 1u)];
+                pos = T.toff[f.x] + T.cell[(size_t)f.x * T.cell_stride + f.y] + f.z;
+            } else {
+                const uint32_t slot = (code >> PAIR_LID_SHIFT) & (HCAP - 1);
+                const uint32_t b = s_base[slot];
+                const uint32_t lr = code & ((1u << PAIR_LID_SHIFT) - 1u);
+                if (b != NO_PAIR) {
+                    pos = b + lr;
+                    const uint32_t lo = s_loff[slot];
+                    if (lo != 0xFFFFu) lpos = lo + lr;
+                }
+            }
+        };
+        // Short rays (maxp <= 4): all of the ray's pairs are resolved up front, convergent across
+        // lanes; the walk then only selects the k-th.
+        const bool fast = maxp <= 4;
+        uint32_t P0 = NO_PAIR, P1 = NO_PAIR, P2 = NO_PAIR, P3 = NO_PAIR;
+        uint32_t L0 = NO_PAIR, L1 = NO_PAIR, L2 = NO_PAIR, L3 = NO_PAIR;
+        uint32_t N0 = 0, N1 = 0, N2 = 0, N3 = 0;
+        if (fast) {
+            uint4 code = make_uint4(NO_PAIR, NO_PAIR, NO_PAIR, NO_PAIR);
+            if (maxp == 4) {
+                code = *reinterpret_cast<const uint4*>(pc);
+            } else {
+                code.x = pc[0];
+                if (maxp > 1) code.y = pc[1];
+                if (maxp > 2) code.z = pc[2];
+            }
+            resolve(code.x, P0, L0, N0);
+            resolve(code.y, P1, L1, N1);
+            resolve(code.z, P2, L2, N2);
+            resolve(code.w, P3, L3, N3);
+        }
         uint64_t cur = EMPTY_KEY;
         // current pair: global position, or staging position (lpos < PLC_STAGE)
         uint32_t k = 0, pos = NO_PAIR, lpos = NO_PAIR, cnt = 0, w = 0;
@@ -369,28 +459,15 @@ __global__ __launch_bounds__(PLC_THREADS) void k_place(const float* __restrict__
                 const uint64_t key = brick_key_of(r.vx, r.vy, r.vz);
                 if (key != cur) {  // the ray's next pair, in k_count's order
                     cur = key;
-                    const uint32_t code = k < maxp ? pc[k] : NO_PAIR;
-                    k++;
-                    pos = NO_PAIR;
-                    lpos = NO_PAIR;
-                    cnt = 0;
-                    w = 0;
-                    if (code != NO_PAIR && code != PAIR_DEAD) {
-                        cnt = (code >> PAIR_CNT_SHIFT) & 31u;
-                        if (code & PAIR_FB) {
-                            const uint4 f = Wk.fb[code & ((1u << PAIR_CNT_SHIFT) - 1u)];
-                            pos = T.toff[f.x] + T.cell[(size_t)f.x * T.cell_stride + f.y] + f.z;
-                        } else {
-                            const uint32_t slot = (code >> PAIR_LID_SHIFT) & (HCAP - 1);
-                            const uint32_t b = s_base[slot];
-                            const uint32_t lr = code & ((1u << PAIR_LID_SHIFT) - 1u);
-                            if (b != NO_PAIR) {
-                                pos = b + lr;
-                                const uint32_t lo = s_loff[slot];
-                                if (lo != 0xFFFFu) lpos = lo + lr;
-                            }
-                        }
+                    if (fast) {
+                        pos = k == 0 ? P0 : k == 1 ? P1 : k == 2 ? P2 : k == 3 ? P3 : NO_PAIR;
+                        lpos = k == 0 ? L0 : k == 1 ? L1 : k == 2 ? L2 : k == 3 ? L3 : NO_PAIR;
+                        cnt = k == 0 ? N0 : k == 1 ? N1 : k == 2 ? N2 : k == 3 ? N3 : 0u;
+                    } else {
+                        resolve(k < maxp ? pc[k] : NO_PAIR, pos, lpos, cnt);
                     }
+                    k++;
+                    w = 0;
                 }
                 if (w < cnt) {
                     const uint32_t l = ((r.vz & 7) << 6) | ((r.vy & 7) << 3) | (r.vx & 7);

@@ -87,6 +87,28 @@ __device__ __forceinline__ bool voxel_sample(const RayConst& R, float ox, float 
     return true;
 }
 
+// voxel_sample's verdict alone (k_count needs no sample value): the same fp32 ops up to the
+// projection; a voxel in front of the hit (proj > 0) always passes, and behind it the sqrt is only
+// evaluated when d2 lies within 2^-20 of tau^2, so the result equals voxel_sample's bit for bit.
+__device__ __forceinline__ bool voxel_gate(const RayConst& R, float ox, float oy, float oz,
+                                           const RayState& r) {
+    if (!(r.vx > -VOX_LIMIT && r.vx < VOX_LIMIT && r.vy > -VOX_LIMIT && r.vy < VOX_LIMIT &&
+          r.vz > -VOX_LIMIT && r.vz < VOX_LIMIT))
+        return false;
+    const float cx = ((float)r.vx + 0.5f) * R.vs;
+    const float cy = ((float)r.vy + 0.5f) * R.vs;
+    const float cz = ((float)r.vz + 0.5f) * R.vs;
+    const float ax = cx - ox, ay = cy - oy, az = cz - oz;
+    const float bx = r.px - cx, by = r.py - cy, bz = r.pz - cz;
+    const float proj = ax * bx + ay * by + az * bz;
+    if (proj > 0.0f) return true;       // sdf = +dist > -tau
+    if (!(proj < 0.0f)) return false;   // proj == 0 (or NaN): skipped
+    const float d2 = bx * bx + by * by + bz * bz;
+    if (d2 < R.tau2_lo) return true;    // dist < tau
+    if (!(d2 <= R.tau2_hi)) return false;
+    return __builtin_sqrtf(d2) < R.tau;  // -dist > -tau
+}
+
 // One DDA step (math::MinIndex tie-break: equal entries resolve to the higher axis).
 // Returns false when the next entry time is past the band end.
 // Written with selects only: an axis index would make hipcc spill the state to scratch.
