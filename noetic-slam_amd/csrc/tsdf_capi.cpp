@@ -216,7 +216,7 @@ void tsdf_destroy(tsdf_ctx* c) {
         }
     }
     delete c->timer;
-    void* dev[] = {c->T.keys,        c->T.slots,         c->T.cnt,         c->T.toff,
+    void* dev[] = {c->T.keys,        c->T.slots,
                    c->T.touched,
                    c->T.cell,        c->T.brick_keys,    c->Pl.sdf,        c->Pl.weight,
                    c->Wk.pair,       c->Wk.blk,          c->Wk.blk_occ,    c->Wk.fb,
@@ -286,8 +286,6 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
 
     HIPCHK(c, hipMalloc(&c->T.keys, c->cap * sizeof(uint64_t)));
     HIPCHK(c, hipMalloc(&c->T.slots, c->cap * sizeof(uint32_t)));
-    HIPCHK(c, hipMalloc(&c->T.cnt, c->cap * sizeof(uint32_t)));
-    HIPCHK(c, hipMalloc(&c->T.toff, c->cap * sizeof(uint32_t)));
     HIPCHK(c, hipMalloc(&c->T.touched, c->cap * sizeof(uint32_t)));
     HIPCHK(c, hipMemsetAsync(c->T.touched, 0, c->cap * sizeof(uint32_t), c->stream));
     HIPCHK(c, hipMalloc(&c->T.cell, c->cap * c->T.cell_stride * sizeof(uint32_t)));
@@ -310,7 +308,6 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
     // VDBFusion background: tsdf = sdf_trunc, weight = 0
     HIPCHK(c, launch_fill_u64(c->T.keys, EMPTY_KEY, c->cap, c->stream));
     HIPCHK(c, launch_fill_u32(c->T.slots, UNASSIGNED, c->cap, c->stream));
-    HIPCHK(c, hipMemsetAsync(c->T.cnt, 0, c->cap * sizeof(uint32_t), c->stream));
     HIPCHK(c, hipMemsetAsync(c->T.cell, 0, c->cap * c->T.cell_stride * sizeof(uint32_t),
                              c->stream));
     HIPCHK(c, launch_fill(c->Pl.sdf, (float)p->sdf_trunc, p->max_bricks * BRICK_VOX, c->stream));

@@ -9,10 +9,9 @@
 //   Table   open-addressing brick hash, capacity 2^k >= 2 * max_bricks, linear probing:
 //           keys[cap]  u64  packed brick coords (21 bits/axis, biased by 2^20); EMPTY = ~0
 //           slots[cap] u32  brick-pool slot (UNASSIGNED until the batch's compaction pass)
-//           cnt[cap]   u32  this batch's (ray, brick) pair count (written by k_compact)
-//           toff[cap]  u32  this batch's ray-record segment offset
 //           touched[cap] u32  1 if the batch touches the brick (k_count sets, k_compact clears)
-//           cell[cap * cell_stride] u32  per (brick, scan) SAMPLE counts, then their prefix
+//           cell[cap * cell_stride] u32  per (brick, scan) SAMPLE counts (k_count), then the
+//                                        absolute position of those samples (k_compact)
 //   Pool    sdf[max_bricks][512] f32, weight[max_bricks][512] f32 — voxel l = z*64 + y*8 + x;
 //           brick_keys[max_bricks] u64 (slot -> key, for export)
 //   Work    pair[max_batch_points * maxp] u32    per-ray pair codes (see PAIR_*)
@@ -82,8 +81,6 @@ struct BatchDesc {
 struct Table {
     uint64_t* keys;
     uint32_t* slots;
-    uint32_t* cnt;
-    uint32_t* toff;
     uint32_t* touched;  // set (plain store) by k_count for every brick the batch touches
     uint32_t* cell;
     uint64_t* brick_keys;  // pool slot -> key

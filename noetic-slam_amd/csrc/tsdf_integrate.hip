@@ -96,7 +96,8 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchDesc D, Table T,
             // base + i >= max_smp: capacity overflow (reported by k_compact)
             B.c[j] = (i < n && base + i < Wk.max_smp) ? Wk.smp[base + i] : make_uint2(0u, ~0u);
         }
-        B.cell = (uint32_t)tid < ns ? T.cell[(size_t)r.x * T.cell_stride + tid] : 0u;
+        // absolute position of the brick's scan-tid samples -> relative to its segment
+        B.cell = (uint32_t)tid < ns ? T.cell[(size_t)r.x * T.cell_stride + tid] - base : 0u;
         const float* Sg = Pl.sdf + (size_t)(has ? r.y : 0) * BRICK_VOX;
         const float* Wg = Pl.weight + (size_t)(has ? r.y : 0) * BRICK_VOX;
         B.s0 = has ? Sg[tid] : tau;

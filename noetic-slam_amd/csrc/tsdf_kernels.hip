@@ -302,9 +302,9 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t* s_w, u
 }
 
 // Sweeps the `touched` words of the whole table (coalesced, cap * 4 B) — cheaper than any
-// per-brick first-touch atomic in k_count.  For each touched brick: its per-scan cell counts
-// become their exclusive prefix (and their sum its pair count), it gets its record segment, a pool
-// slot if it is new, and an active-list entry; three atomics per CMP_THREADS table entries.
+// per-brick first-touch atomic in k_count.  For each touched brick: its sample segment, its
+// per-scan cells rewritten as absolute positions in it (segment start + exclusive prefix), a pool
+// slot if it is new, and an active record; three atomics per CMP_THREADS table entries.
 __global__ __launch_bounds__(CMP_THREADS) void k_compact(uint32_t n_scans, Table T, Work Wk,
                                                          Globals* G, int parity) {
     __shared__ uint32_t s_w[16];
@@ -316,21 +316,14 @@ __global__ __launch_bounds__(CMP_THREADS) void k_compact(uint32_t n_scans, Table
         const uint32_t h = chunk + threadIdx.x;
         const bool hit = T.touched[h] != 0u;
         uint32_t n = 0, isnew = 0;
+        uint4* cp = reinterpret_cast<uint4*>(T.cell + (size_t)h * T.cell_stride);
         if (hit) {
             T.touched[h] = 0u;
             isnew = T.slots[h] == UNASSIGNED ? 1u : 0u;
-            // exclusive prefix of the per-scan cell counts (cell_stride is a multiple of 4)
-            uint4* cp = reinterpret_cast<uint4*>(T.cell + (size_t)h * T.cell_stride);
-            for (uint32_t q = 0; q < (n_scans + 3) / 4; q++) {
-                uint4 v = cp[q];
-                const uint32_t x0 = v.x, x1 = v.y, x2 = v.z, x3 = v.w;
-                v.x = n; n += x0;
-                v.y = n; n += x1;
-                v.z = n; n += x2;
-                v.w = n; n += x3;
-                cp[q] = v;
+            for (uint32_t q = 0; q < (n_scans + 3) / 4; q++) {  // cell_stride is a multiple of 4
+                const uint4 v = cp[q];
+                n += v.x + v.y + v.z + v.w;
             }
-            T.cnt[h] = n;
         }
         uint32_t tot_a, tot_c, tot_n;
         const uint32_t ea = block_excl_scan(hit ? 1u : 0u, s_w, &tot_a);
@@ -344,7 +337,18 @@ __global__ __launch_bounds__(CMP_THREADS) void k_compact(uint32_t n_scans, Table
         }
         __syncthreads();
         if (hit) {
-            T.toff[h] = base_c + ec;
+            // the per-scan cells become absolute sample positions: segment start + exclusive
+            // prefix (k_place then finds a run's position with one gather)
+            uint32_t p = base_c + ec;
+            for (uint32_t q = 0; q < (n_scans + 3) / 4; q++) {
+                uint4 v = cp[q];
+                const uint32_t x0 = v.x, x1 = v.y, x2 = v.z, x3 = v.w;
+                v.x = p; p += x0;
+                v.y = p; p += x1;
+                v.z = p; p += x2;
+                v.w = p; p += x3;
+                cp[q] = v;
+            }
             uint32_t slot = isnew ? base_n + en : T.slots[h];
             if (isnew) {
                 if (slot < T.max_bricks) {
@@ -377,38 +381,90 @@ constexpr int PLC_STAGE = 10112;      // staged samples per workgroup (6 B each;
 
 __global__ __launch_bounds__(PLC_THREADS) void k_place(const float* __restrict__ xyz, BatchDesc D,
                                                       RayConst R, Table T, Work Wk) {
-    __shared__ uint32_t s_base[HCAP];    // run -> first sample of the run in the brick segment
-    __shared__ uint16_t s_loff[HCAP];    // run -> offset in the workgroup's sample order
-    __shared__ uint32_t s_runs[HCAP];    // occupied runs: slot | count << 11
-    __shared__ float st_s[PLC_STAGE];    // staged samples
+    constexpr int PLC_WORDS = (PLC_STAGE + 31) / 32;
+    __shared__ uint32_t s_base[HCAP];      // run -> first sample of the run in the brick segment
+    __shared__ uint16_t s_loff[HCAP];      // run -> offset in the workgroup's sample order
+    __shared__ uint16_t s_ord[HCAP];       // staged runs in staging order
+    __shared__ uint32_t s_bits[PLC_WORDS]; // staging positions where a run starts
+    __shared__ uint16_t s_wpre[PLC_WORDS]; // run starts in the words before
+    __shared__ float st_s[PLC_STAGE];      // staged samples
     __shared__ uint16_t st_l[PLC_STAGE];
-    __shared__ uint32_t s_nruns;
+    __shared__ uint32_t s_nst;             // staged samples (end of the last staged run)
     uint32_t t, r0, r1;
     block_range(D, blockIdx.x, t, r0, r1);
     const uint4* bt = Wk.blk + (size_t)blockIdx.x * HCAP;
     const uint32_t* occ = Wk.blk_occ + (size_t)blockIdx.x * (HCAP / 32);
-    if (threadIdx.x == 0) s_nruns = 0u;
-    __syncthreads();
-    for (int slot = threadIdx.x; slot < HCAP; slot += PLC_THREADS) {
-        if ((occ[slot >> 5] >> (slot & 31)) & 1u) {
-            const uint4 e = bt[slot];
-            uint32_t b = NO_PAIR;
-            if (e.x != NO_PAIR) b = T.toff[e.x] + T.cell[(size_t)e.x * T.cell_stride + t] + e.y;
-            s_base[slot] = b;
-            // runs starting past the staging capacity are stored directly (0xFFFF: not staged)
-            s_loff[slot] = e.z < (uint32_t)PLC_STAGE ? (uint16_t)e.z : (uint16_t)0xFFFFu;
-            if (b != NO_PAIR && e.z < (uint32_t)PLC_STAGE)
-                s_runs[atomicAdd(&s_nruns, 1u)] = (uint32_t)slot | (e.w << 11);
-        }
-    }
-    __syncthreads();
+    // the ray's own setup (point loads, divisions) overlaps the run-table gathers below
     const float ox = D.ox[t], oy = D.oy[t], oz = D.oz[t];
     const uint32_t maxp = Wk.maxp;
     const uint32_t i = r0 + threadIdx.x;
     RayState r;
-    if (i < r1 && ray_init(R, ox, oy, oz, xyz[3 * (size_t)i], xyz[3 * (size_t)i + 1],
-                           xyz[3 * (size_t)i + 2], r)) {
-        const uint32_t* pc = Wk.pair + (size_t)i * maxp;
+    const bool ok = i < r1 && ray_init(R, ox, oy, oz, xyz[3 * (size_t)i], xyz[3 * (size_t)i + 1],
+                                       xyz[3 * (size_t)i + 2], r);
+    const uint32_t* pc = Wk.pair + (size_t)i * maxp;
+    uint4 code4 = make_uint4(NO_PAIR, NO_PAIR, NO_PAIR, NO_PAIR);
+    if (ok && maxp == 4) code4 = *reinterpret_cast<const uint4*>(pc);
+    for (int j = threadIdx.x; j < PLC_WORDS; j += PLC_THREADS) s_bits[j] = 0u;
+    if (threadIdx.x == 0) s_nst = 0u;
+    __syncthreads();
+    // run table: global base and staging offset per run; staged runs mark their start
+    constexpr int SLOTS_PT = HCAP / PLC_THREADS;
+    uint32_t my_loff[SLOTS_PT];
+#pragma unroll
+    for (int q = 0; q < SLOTS_PT; q++) {
+        const int slot = threadIdx.x + q * PLC_THREADS;
+        my_loff[q] = 0xFFFFu;
+        if ((occ[slot >> 5] >> (slot & 31)) & 1u) {
+            const uint4 e = bt[slot];
+            uint32_t b = NO_PAIR;
+            if (e.x != NO_PAIR) b = T.cell[(size_t)e.x * T.cell_stride + t] + e.y;
+            s_base[slot] = b;
+            // runs starting past the staging capacity are stored directly (0xFFFF: not staged)
+            s_loff[slot] = e.z < (uint32_t)PLC_STAGE ? (uint16_t)e.z : (uint16_t)0xFFFFu;
+            if (e.z < (uint32_t)PLC_STAGE) {
+                my_loff[q] = e.z;
+                atomicOr(&s_bits[e.z >> 5], 1u << (e.z & 31));
+                atomicMax(&s_nst, min(e.z + e.w, (uint32_t)PLC_STAGE));
+            }
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {  // exclusive prefix of run starts per bitmap word (one wave)
+        constexpr int WPL = (PLC_WORDS + 63) / 64;
+        uint32_t cnt[WPL], sum = 0;
+#pragma unroll
+        for (int q = 0; q < WPL; q++) {
+            const int wd = threadIdx.x * WPL + q;
+            cnt[q] = wd < PLC_WORDS ? (uint32_t)__popc(s_bits[wd]) : 0u;
+            sum += cnt[q];
+        }
+        uint32_t incl = sum;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(incl, d, 64);
+            if ((int)threadIdx.x >= d) incl += y;
+        }
+        uint32_t pre = incl - sum;
+#pragma unroll
+        for (int q = 0; q < WPL; q++) {
+            const int wd = threadIdx.x * WPL + q;
+            if (wd < PLC_WORDS) s_wpre[wd] = (uint16_t)pre;
+            pre += cnt[q];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < SLOTS_PT; q++) {  // staged runs in staging order (read after the walk)
+        const uint32_t lo = my_loff[q];
+        if (lo != 0xFFFFu)
+            s_ord[s_wpre[lo >> 5] + __popc(s_bits[lo >> 5] & ((1u << (lo & 31)) - 1u))] =
+                (uint16_t)(threadIdx.x + q * PLC_THREADS);
+    }
+#ifdef TSDF_ABLATE_PL_NOWALK
+    if (ok && r.px == 1e30f) {
+#else
+    if (ok) {
+#endif
         // a pair code -> its samples' global position, staging position (lpos < PLC_STAGE), count
         auto resolve = [&](uint32_t code, uint32_t& pos, uint32_t& lpos, uint32_t& cnt) {
             pos = NO_PAIR;
@@ -418,7 +474,7 @@ __global__ __launch_bounds__(PLC_THREADS) void k_place(const float* __restrict__
             cnt = (code >> PAIR_CNT_SHIFT) & 31u;
             if (code & PAIR_FB) {
                 const uint4 f = Wk.fb[code & ((1u << PAIR_CNT_SHIFT) - 1u)];
-                pos = T.toff[f.x] + T.cell[(size_t)f.x * T.cell_stride + f.y] + f.z;
+                pos = T.cell[(size_t)f.x * T.cell_stride + f.y] + f.z;
             } else {
                 const uint32_t slot = (code >> PAIR_LID_SHIFT) & (HCAP - 1);
                 const uint32_t b = s_base[slot];
@@ -437,10 +493,8 @@ __global__ __launch_bounds__(PLC_THREADS) void k_place(const float* __restrict__
         uint32_t L0 = NO_PAIR, L1 = NO_PAIR, L2 = NO_PAIR, L3 = NO_PAIR;
         uint32_t N0 = 0, N1 = 0, N2 = 0, N3 = 0;
         if (fast) {
-            uint4 code = make_uint4(NO_PAIR, NO_PAIR, NO_PAIR, NO_PAIR);
-            if (maxp == 4) {
-                code = *reinterpret_cast<const uint4*>(pc);
-            } else {
+            uint4 code = code4;
+            if (maxp < 4) {
                 code.x = pc[0];
                 if (maxp > 1) code.y = pc[1];
                 if (maxp > 2) code.z = pc[2];
@@ -453,19 +507,40 @@ __global__ __launch_bounds__(PLC_THREADS) void k_place(const float* __restrict__
         uint64_t cur = EMPTY_KEY;
         // current pair: global position, or staging position (lpos < PLC_STAGE)
         uint32_t k = 0, pos = NO_PAIR, lpos = NO_PAIR, cnt = 0, w = 0;
+        if (fast) {
+            // Branch-free walk: lanes are at different steps of different pairs, so every
+            // data-dependent branch here would run for the whole wave; selects cost less.
+            for (int it = 0; it < MAX_DDA_STEPS; it++) {
+                float s;
+                const bool g = voxel_sample_sel(R, ox, oy, oz, r, s);
+                const uint64_t key = brick_key_of(r.vx, r.vy, r.vz);
+                const bool nb = g && key != cur;  // the ray's next pair, in k_count's order
+                cur = nb ? key : cur;
+                pos = nb ? (k == 0 ? P0 : k == 1 ? P1 : k == 2 ? P2 : k == 3 ? P3 : NO_PAIR) : pos;
+                lpos = nb ? (k == 0 ? L0 : k == 1 ? L1 : k == 2 ? L2 : k == 3 ? L3 : NO_PAIR) : lpos;
+                cnt = nb ? (k == 0 ? N0 : k == 1 ? N1 : k == 2 ? N2 : k == 3 ? N3 : 0u) : cnt;
+                k += nb ? 1u : 0u;
+                w = nb ? 0u : w;
+                const bool st = g && w < cnt;
+                const uint32_t l = ((r.vz & 7) << 6) | ((r.vy & 7) << 3) | (r.vx & 7);
+                const bool stage = st && lpos != NO_PAIR && lpos + w < (uint32_t)PLC_STAGE;
+                if (stage) {
+                    st_s[lpos + w] = s;
+                    st_l[lpos + w] = (uint16_t)l;
+                } else if (st && pos != NO_PAIR && pos + w < Wk.max_smp) {
+                    Wk.smp[pos + w] = make_uint2(__float_as_uint(s), (t << 9) | l);
+                }
+                w += g ? 1u : 0u;
+                if (!ray_step(r)) break;
+            }
+        } else
         for (int it = 0; it < MAX_DDA_STEPS; it++) {
             float s;
             if (voxel_sample(R, ox, oy, oz, r, s)) {
                 const uint64_t key = brick_key_of(r.vx, r.vy, r.vz);
                 if (key != cur) {  // the ray's next pair, in k_count's order
                     cur = key;
-                    if (fast) {
-                        pos = k == 0 ? P0 : k == 1 ? P1 : k == 2 ? P2 : k == 3 ? P3 : NO_PAIR;
-                        lpos = k == 0 ? L0 : k == 1 ? L1 : k == 2 ? L2 : k == 3 ? L3 : NO_PAIR;
-                        cnt = k == 0 ? N0 : k == 1 ? N1 : k == 2 ? N2 : k == 3 ? N3 : 0u;
-                    } else {
-                        resolve(k < maxp ? pc[k] : NO_PAIR, pos, lpos, cnt);
-                    }
+                    resolve(k < maxp ? pc[k] : NO_PAIR, pos, lpos, cnt);
                     k++;
                     w = 0;
                 }
@@ -484,15 +559,21 @@ __global__ __launch_bounds__(PLC_THREADS) void k_place(const float* __restrict__
         }
     }
     __syncthreads();
-    // copy-out: one wave per run, contiguous stores
-    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nr = s_nruns;
-    for (uint32_t q = wid; q < nr; q += PLC_THREADS / 64) {
-        const uint32_t e = s_runs[q], slot = e & (HCAP - 1), n = e >> 11;
-        const uint32_t b = s_base[slot], lo = s_loff[slot];
-        const uint32_t m = min(n, (uint32_t)PLC_STAGE - lo);  // the staged part of the run
-        for (uint32_t j = lane; j < m; j += 64) {
-            if (b + j < Wk.max_smp)
-                Wk.smp[b + j] = make_uint2(__float_as_uint(st_s[lo + j]), (t << 9) | st_l[lo + j]);
+    // copy-out: one lane per staged sample; its run = the last run start at or before it
+#ifdef TSDF_ABLATE_PL_NOCOPY
+    const uint32_t nst = 0;
+#else
+    const uint32_t nst = s_nst;
+#endif
+    for (uint32_t j = threadIdx.x; j < nst; j += PLC_THREADS) {
+        const uint32_t wd = j >> 5;
+        const uint32_t rank = s_wpre[wd] + __popc(s_bits[wd] & ((2u << (j & 31)) - 1u)) - 1u;
+        const uint32_t slot = s_ord[rank];
+        const uint32_t b = s_base[slot];
+        if (b != NO_PAIR) {
+            const uint32_t dst = b + (j - s_loff[slot]);
+            if (dst < Wk.max_smp)
+                Wk.smp[dst] = make_uint2(__float_as_uint(st_s[j]), (t << 9) | st_l[j]);
         }
     }
 }

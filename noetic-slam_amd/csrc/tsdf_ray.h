@@ -87,6 +87,24 @@ __device__ __forceinline__ bool voxel_sample(const RayConst& R, float ox, float 
     return true;
 }
 
+// voxel_sample without early exits (same fp32 ops, same verdict and sample): for walks whose lanes
+// diverge, where straight-line selects beat branches.
+__device__ __forceinline__ bool voxel_sample_sel(const RayConst& R, float ox, float oy, float oz,
+                                                 const RayState& r, float& s) {
+    const bool inl = r.vx > -VOX_LIMIT && r.vx < VOX_LIMIT && r.vy > -VOX_LIMIT &&
+                     r.vy < VOX_LIMIT && r.vz > -VOX_LIMIT && r.vz < VOX_LIMIT;
+    const float cx = ((float)r.vx + 0.5f) * R.vs;
+    const float cy = ((float)r.vy + 0.5f) * R.vs;
+    const float cz = ((float)r.vz + 0.5f) * R.vs;
+    const float ax = cx - ox, ay = cy - oy, az = cz - oz;
+    const float bx = r.px - cx, by = r.py - cy, bz = r.pz - cz;
+    const float dist = __builtin_sqrtf(bx * bx + by * by + bz * bz);
+    const float proj = ax * bx + ay * by + az * bz;
+    const float sdf = proj > 0.0f ? dist : -dist;
+    s = sdf < R.tau ? sdf : R.tau;
+    return inl && (proj > 0.0f || proj < 0.0f) && sdf > -R.tau;
+}
+
 // voxel_sample's verdict alone (k_count needs no sample value): the same fp32 ops up to the
 // projection; a voxel in front of the hit (proj > 0) always passes, and behind it the sqrt is only
 // evaluated when d2 lies within 2^-20 of tau^2, so the result equals voxel_sample's bit for bit.
