@@ -39,6 +39,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="budget of the CPU-oracle baseline sample (rank 0, N=1)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--pipeline", action="store_true",
+                    help="overlap consecutive batches on two HIP streams (tsdf_params.pipeline); "
+                         "per-kernel times then include the overlap")
     ap.add_argument("--no-profile", action="store_true",
                     help="do not record per-kernel HIP events in the timed region")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_r01.json"),
@@ -88,7 +91,8 @@ def main():
     max_pts = max(int(np.diff(o).max()) for _, o, _ in steps)
 
     vol = HipTSDFVolume(args.voxel, args.trunc, max_points=max(max_pts, 1 << 17),
-                        max_bricks=1 << 20, device_id=local, max_batch=min(args.batch, 64))
+                        max_bricks=1 << 20, device_id=local, max_batch=min(args.batch, 64),
+                        pipeline=args.pipeline)
 
     def run_step(i):
         x, offs, org = steps[i]
@@ -210,7 +214,7 @@ def main():
                        "voxel_size_m": args.voxel, "sdf_trunc_m": args.trunc,
                        "scans_per_step": scans_per_step, "global_batch": scans_per_step,
                        "points_per_scan": int(round(rays_per_scan * world)),
-                    "scans_per_gpu_batch": args.batch,
+                    "scans_per_gpu_batch": args.batch, "pipelined_batches": args.pipeline,
                        "parallelism": "azimuth-sector x%d" % world if world > 1 else "single"},
             "roofline": roofline,
             "cpu_baseline": cpu,

@@ -64,7 +64,10 @@ typedef struct tsdf_params {
     int32_t device_id;     /* HIP device ordinal */
     int32_t brick_side;    /* must be TSDF_BRICK_SIDE */
     uint32_t max_batch;    /* scans integrated per GPU batch, 1..TSDF_MAX_BATCH (default 32) */
-    uint32_t reserved;
+    uint32_t pipeline;     /* 1: overlap consecutive batches on two streams (count / compact /
+                              place of batch b+1 run beside batch b's place / integrate; same field,
+                              bit for bit); 0 (default): batches run one after another, so per-kernel
+                              timings (tsdf_stats.kernel_ms) are not shared with another batch */
 } tsdf_params;
 
 /* Batching.  Scans are integrated in call order and the field after any sequence of calls is

@@ -100,12 +100,22 @@ struct tsdf_ctx {
     uint32_t max_batch = 0;
     uint64_t batch_points = 0;  // pair-slot capacity / maxp: points one batch may hold
     uint32_t max_blocks = 0;    // k_count / k_place workgroups one batch may need
-    // host-pointer path: pinned double buffer per scan + device staging of the pending batch
+    // host-pointer path: pinned double buffer per scan; the pending batch's points are staged in
+    // stage2[batch parity]
     float* h_stage[2] = {nullptr, nullptr};
     hipEvent_t stage_done[2] = {nullptr, nullptr};
     int stage_cur = 0;
-    float* d_stage = nullptr;
-    BatchDesc pend{};  // pending host scans (points in d_stage)
+    // Batch pipeline: batch b runs on bst[b & 1] with its own work buffers (W2), per-scan cells
+    // (cell2) and device staging (stage2), so batch b + 1's count / compact / place overlap batch
+    // b's place / integrate.  Cross-batch order: k_count(b+1) after k_compact(b)
+    // (the table's `touched` words), k_integrate(b+1) after k_finish(b) (per-brick fuse order).
+    hipStream_t bst[2] = {nullptr, nullptr};
+    Work W2[2]{};
+    uint32_t* cell2[2] = {nullptr, nullptr};
+    float* stage2[2] = {nullptr, nullptr};
+    hipEvent_t ev_main = nullptr;
+    hipEvent_t ev_compact[2] = {nullptr, nullptr}, ev_integ[2] = {nullptr, nullptr};
+    BatchDesc pend{};  // pending host scans (points in stage2[batch_id & 1])
     uint64_t batch_id = 0;
     uint64_t n_scans = 0, n_batches = 0, n_points_in = 0;
     EventTimer* timer = nullptr;
@@ -162,25 +172,70 @@ static int launch(tsdf_ctx* c, const float* d_xyz, BatchDesc& D) {
     D.n_blocks = D.blk[D.n_scans];
     if (D.n_blocks > c->max_blocks)
         return fail(c, TSDF_EINVAL, "batch needs %u workgroups > %u", D.n_blocks, c->max_blocks);
-    const int parity = (int)(c->batch_id & 1);
-    HIPCHK(c, launch_batch(d_xyz, D, c->R, c->T, c->Wk, c->Pl, c->G, parity, c->stream,
-                           c->timer));
+    const int par = (int)(c->batch_id & 1);
+    hipStream_t st = c->bst[par];
+    Table T = c->T;
+    T.cell = c->cell2[par];
+    const Work& W = c->W2[par];
+    EventTimer* tm = c->timer;
+    HIPCHK(c, hipEventRecord(c->ev_main, c->stream));  // staging uploads, imports, ...
+    HIPCHK(c, hipStreamWaitEvent(st, c->ev_main, 0));
+    if (c->batch_id > 0)  // pipelined: after the previous batch's compact; else after all of it
+        HIPCHK(c, hipStreamWaitEvent(st, c->p.pipeline ? c->ev_compact[par ^ 1]
+                                                       : c->ev_integ[par ^ 1], 0));
+    if (D.n_blocks) {
+        if (tm) tm->begin(KIND_COUNT, st);
+        HIPCHK(c, launch_count(d_xyz, D, c->R, T, W, c->G, par, st));
+        if (tm) tm->end(KIND_COUNT, st);
+        if (tm) tm->begin(KIND_COMPACT, st);
+        HIPCHK(c, launch_compact(D, T, W, c->G, par, st));
+        if (tm) tm->end(KIND_COMPACT, st);
+    }
+    HIPCHK(c, hipEventRecord(c->ev_compact[par], st));
+    if (D.n_blocks) {
+        if (tm) tm->begin(KIND_PLACE, st);
+        HIPCHK(c, launch_place(d_xyz, D, c->R, T, W, st));
+        if (tm) tm->end(KIND_PLACE, st);
+    }
+    if (c->batch_id > 0) HIPCHK(c, hipStreamWaitEvent(st, c->ev_integ[par ^ 1], 0));
+    if (D.n_blocks) {
+        if (tm) tm->begin(KIND_INTEGRATE, st);
+        HIPCHK(c, launch_integrate(D, c->R, T, W, c->Pl, c->G, par, st));
+        if (tm) tm->end(KIND_INTEGRATE, st);
+    }
+    HIPCHK(c, launch_finish(c->G, par, st));
+    HIPCHK(c, hipEventRecord(c->ev_integ[par], st));
     c->batch_id++;
     c->n_batches++;
     c->n_scans += D.n_scans;
-    if (c->timer && c->timer->pending.size() > 8192) {
-        HIPCHK(c, hipStreamSynchronize(c->stream));
-        c->timer->harvest();
+    if (tm && tm->pending.size() > 8192) {
+        HIPCHK(c, hipStreamSynchronize(c->bst[0]));
+        HIPCHK(c, hipStreamSynchronize(c->bst[1]));
+        tm->harvest();
     }
     return TSDF_OK;
 }
 
+// The context stream waits for every launched batch (read-outs, imports, sync).
+static int join(tsdf_ctx* c) {
+    for (int q = 0; q < 2; q++)
+        if (c->batch_id > (uint64_t)q) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_integ[q], 0));
+    return TSDF_OK;
+}
+
+// Launch the queued host scans (integrate paths: no join, so batches keep overlapping).
 static int flush(tsdf_ctx* c) {
     if (c->pend.n_scans == 0) return TSDF_OK;
-    const int rc = launch(c, c->d_stage, c->pend);
+    const int rc = launch(c, c->stage2[c->batch_id & 1], c->pend);
     c->pend.n_scans = 0;
     c->pend.off[0] = 0;
     return rc;
+}
+
+// flush + make the context stream wait for every batch (read-out, import, sync paths)
+static int settle(tsdf_ctx* c) {
+    const int rc = flush(c);
+    return rc ? rc : join(c);
 }
 
 extern "C" {
@@ -211,23 +266,32 @@ void tsdf_destroy(tsdf_ctx* c) {
     if (c->device >= 0) {
         (void)hipSetDevice(c->device);
         if (c->stream) {
-            (void)flush(c);
+            (void)settle(c);
             (void)hipStreamSynchronize(c->stream);
+            for (int q = 0; q < 2; q++)
+                if (c->bst[q]) (void)hipStreamSynchronize(c->bst[q]);
         }
     }
     delete c->timer;
     void* dev[] = {c->T.keys,        c->T.slots,
                    c->T.touched,
-                   c->T.cell,        c->T.brick_keys,    c->Pl.sdf,        c->Pl.weight,
-                   c->Wk.pair,       c->Wk.blk,          c->Wk.blk_occ,    c->Wk.fb,
-                   c->Wk.smp,        c->Wk.active,
-                   c->G,             c->d_stage};
+                   c->T.brick_keys,  c->Pl.sdf,          c->Pl.weight,     c->G,
+                   c->cell2[0],      c->cell2[1],        c->stage2[0],     c->stage2[1],
+                   c->W2[0].pair,    c->W2[0].blk,       c->W2[0].blk_occ, c->W2[0].fb,
+                   c->W2[0].smp,     c->W2[0].active,    c->W2[1].pair,    c->W2[1].blk,
+                   c->W2[1].blk_occ, c->W2[1].fb,        c->W2[1].smp,     c->W2[1].active};
     for (void* d : dev)
         if (d) (void)hipFree(d);
     for (int i = 0; i < 2; i++) {
         if (c->h_stage[i]) (void)hipHostFree(c->h_stage[i]);
         if (c->stage_done[i]) (void)hipEventDestroy(c->stage_done[i]);
     }
+    for (int q = 0; q < 2; q++) {
+        if (c->bst[q]) (void)hipStreamDestroy(c->bst[q]);
+        if (c->ev_compact[q]) (void)hipEventDestroy(c->ev_compact[q]);
+        if (c->ev_integ[q]) (void)hipEventDestroy(c->ev_integ[q]);
+    }
+    if (c->ev_main) (void)hipEventDestroy(c->ev_main);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -242,6 +306,12 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
     c->device = p->device_id;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    for (int q = 0; q < 2; q++) {
+        HIPCHK(c, hipStreamCreateWithFlags(&c->bst[q], hipStreamNonBlocking));
+        HIPCHK(c, hipEventCreateWithFlags(&c->ev_compact[q], hipEventDisableTiming));
+        HIPCHK(c, hipEventCreateWithFlags(&c->ev_integ[q], hipEventDisableTiming));
+    }
+    HIPCHK(c, hipEventCreateWithFlags(&c->ev_main, hipEventDisableTiming));
 
     c->R.vs = (float)p->voxel_size;
     c->R.inv_vs = 1.0f / c->R.vs;
@@ -288,18 +358,25 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
     HIPCHK(c, hipMalloc(&c->T.slots, c->cap * sizeof(uint32_t)));
     HIPCHK(c, hipMalloc(&c->T.touched, c->cap * sizeof(uint32_t)));
     HIPCHK(c, hipMemsetAsync(c->T.touched, 0, c->cap * sizeof(uint32_t), c->stream));
-    HIPCHK(c, hipMalloc(&c->T.cell, c->cap * c->T.cell_stride * sizeof(uint32_t)));
     HIPCHK(c, hipMalloc(&c->T.brick_keys, p->max_bricks * sizeof(uint64_t)));
     HIPCHK(c, hipMalloc(&c->Pl.sdf, p->max_bricks * BRICK_VOX * sizeof(float)));
     HIPCHK(c, hipMalloc(&c->Pl.weight, p->max_bricks * BRICK_VOX * sizeof(float)));
-    HIPCHK(c, hipMalloc(&c->Wk.pair, slots * sizeof(uint32_t)));
-    HIPCHK(c, hipMalloc(&c->Wk.blk, (size_t)c->max_blocks * HCAP * sizeof(uint4)));
-    HIPCHK(c, hipMalloc(&c->Wk.blk_occ, (size_t)c->max_blocks * (HCAP / 32) * sizeof(uint32_t)));
-    HIPCHK(c, hipMalloc(&c->Wk.fb, (size_t)c->Wk.max_fb * sizeof(uint4)));
-    HIPCHK(c, hipMalloc(&c->Wk.smp, (size_t)c->Wk.max_smp * sizeof(uint2)));
-    HIPCHK(c, hipMalloc(&c->Wk.active, (size_t)c->Wk.max_active * sizeof(uint4)));
+    for (int q = 0; q < 2; q++) {  // one set per batch parity
+        Work& W = c->W2[q];
+        W = c->Wk;  // capacities
+        HIPCHK(c, hipMalloc(&W.pair, slots * sizeof(uint32_t)));
+        HIPCHK(c, hipMalloc(&W.blk, (size_t)c->max_blocks * HCAP * sizeof(uint4)));
+        HIPCHK(c, hipMalloc(&W.blk_occ, (size_t)c->max_blocks * (HCAP / 32) * sizeof(uint32_t)));
+        HIPCHK(c, hipMalloc(&W.fb, (size_t)W.max_fb * sizeof(uint4)));
+        HIPCHK(c, hipMalloc(&W.smp, (size_t)W.max_smp * sizeof(uint2)));
+        HIPCHK(c, hipMalloc(&W.active, (size_t)W.max_active * sizeof(uint4)));
+        HIPCHK(c, hipMalloc(&c->cell2[q], c->cap * c->T.cell_stride * sizeof(uint32_t)));
+        HIPCHK(c, hipMemsetAsync(c->cell2[q], 0, c->cap * c->T.cell_stride * sizeof(uint32_t),
+                                 c->stream));
+        HIPCHK(c, hipMalloc(&c->stage2[q], c->batch_points * 3 * sizeof(float)));
+    }
+    c->T.cell = c->cell2[0];
     HIPCHK(c, hipMalloc(&c->G, sizeof(Globals)));
-    HIPCHK(c, hipMalloc(&c->d_stage, c->batch_points * 3 * sizeof(float)));
     for (int i = 0; i < 2; i++) {
         HIPCHK(c, hipHostMalloc(&c->h_stage[i], c->max_points * 3 * sizeof(float),
                                 hipHostMallocDefault));
@@ -308,8 +385,6 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
     // VDBFusion background: tsdf = sdf_trunc, weight = 0
     HIPCHK(c, launch_fill_u64(c->T.keys, EMPTY_KEY, c->cap, c->stream));
     HIPCHK(c, launch_fill_u32(c->T.slots, UNASSIGNED, c->cap, c->stream));
-    HIPCHK(c, hipMemsetAsync(c->T.cell, 0, c->cap * c->T.cell_stride * sizeof(uint32_t),
-                             c->stream));
     HIPCHK(c, launch_fill(c->Pl.sdf, (float)p->sdf_trunc, p->max_bricks * BRICK_VOX, c->stream));
     HIPCHK(c, hipMemsetAsync(c->Pl.weight, 0, p->max_bricks * BRICK_VOX * sizeof(float),
                              c->stream));
@@ -383,8 +458,11 @@ int tsdf_integrate(tsdf_ctx* c, const void* pts, uint64_t n, uint32_t point_step
     }
     BatchDesc& D = c->pend;
     const uint32_t s = D.n_scans;
+    const int sp = (int)(c->batch_id & 1);  // the pending batch's parity
+    if (s == 0 && c->batch_id >= 2)  // stage2[sp] was last read by batch batch_id - 2
+        HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_integ[sp], 0));
     if (n) {
-        HIPCHK(c, hipMemcpyAsync(c->d_stage + 3 * (uint64_t)D.off[s], h, n * 12,
+        HIPCHK(c, hipMemcpyAsync(c->stage2[sp] + 3 * (uint64_t)D.off[s], h, n * 12,
                                  hipMemcpyHostToDevice, c->stream));
     }
     HIPCHK(c, hipEventRecord(c->stage_done[b], c->stream));
@@ -440,7 +518,7 @@ int tsdf_integrate_device(tsdf_ctx* c, const float* d_xyz, uint64_t n, const dou
 int tsdf_sync(tsdf_ctx* c) {
     if (!c) return TSDF_EINVAL;
     HIPCHK(c, hipSetDevice(c->device));
-    const int rc = flush(c);
+    const int rc = settle(c);
     if (rc) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (c->timer) c->timer->harvest();
@@ -460,7 +538,7 @@ int tsdf_sync(tsdf_ctx* c) {
 // flush + drain, ignoring (but keeping) the overflow flag for read-out calls
 static int drain(tsdf_ctx* c) {
     HIPCHK(c, hipSetDevice(c->device));
-    const int rc = flush(c);
+    const int rc = settle(c);
     if (rc) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (c->timer) c->timer->harvest();
@@ -604,7 +682,7 @@ int tsdf_get_stats(tsdf_ctx* c, tsdf_stats* out) {
     out->n_points_in = c->n_points_in;
     out->n_bricks = std::min<uint64_t>(g.pool_count, c->p.max_bricks);
     if (c->batch_id) {
-        const Counters& L = g.ctr[(c->batch_id - 1) & 1];
+        const Counters& L = g.last;
         out->n_active_last = L.n_active;
         for (int k = 0; k < 8; k++) {
             out->n_voxels_last += L.n_vox[k];

@@ -107,7 +107,7 @@ struct Work {
     uint32_t max_smp;     // capacity of smp
 };
 
-// per-batch counters, double-buffered by batch parity (k_count zeroes the other set)
+// per-batch counters, double-buffered by batch parity (zeroed by k_finish at the end of a batch)
 struct Counters {
     uint32_t n_active;
     uint32_t cursor;
@@ -129,6 +129,7 @@ struct Globals {
     unsigned long long tot_rays[8];
     unsigned long long tot_pairs[8];
     unsigned long long tot_dirty[8];
+    Counters last;  // the last finished batch's counters (k_finish)
 };
 
 enum KernelKind { KIND_COUNT = 0, KIND_COMPACT = 1, KIND_PLACE = 2, KIND_INTEGRATE = 3, KIND_N = 4 };
@@ -140,9 +141,13 @@ struct KernelTimer {
     virtual ~KernelTimer() {}
 };
 
-hipError_t launch_batch(const float* d_xyz, const BatchDesc& D, const RayConst& R, const Table& T,
-                        const Work& Wk, const Pool& Pl, Globals* G, int parity, hipStream_t st,
-                        KernelTimer* timer);
+hipError_t launch_count(const float* d_xyz, const BatchDesc& D, const RayConst& R, const Table& T,
+                        const Work& Wk, Globals* G, int parity, hipStream_t st);
+hipError_t launch_compact(const BatchDesc& D, const Table& T, const Work& Wk, Globals* G,
+                          int parity, hipStream_t st);
+hipError_t launch_place(const float* d_xyz, const BatchDesc& D, const RayConst& R, const Table& T,
+                        const Work& Wk, hipStream_t st);
+hipError_t launch_finish(Globals* G, int parity, hipStream_t st);
 hipError_t launch_integrate(const BatchDesc& D, const RayConst& R, const Table& T, const Work& Wk,
                             const Pool& Pl, Globals* G, int parity, hipStream_t st);
 hipError_t launch_query_dense(const Table& T, const Pool& Pl, const int lo[3], const int dims[3],

@@ -78,9 +78,7 @@ __global__ __launch_bounds__(CNT_THREADS) void k_count(const float* __restrict__
     __shared__ uint32_t s_occ[HCAP / 32];
     __shared__ unsigned long long red[2][CNT_THREADS / 64];
     __shared__ uint32_t s_wsum[CNT_THREADS / 64];
-    Counters* C = &G->ctr[parity];
-    if (blockIdx.x == 0 && threadIdx.x < sizeof(Counters) / 4)
-        reinterpret_cast<uint32_t*>(&G->ctr[parity ^ 1])[threadIdx.x] = 0u;  // next batch's set
+    Counters* C = &G->ctr[parity];  // zeroed by the previous batch of this parity (k_finish)
     for (int j = threadIdx.x; j < HCAP; j += CNT_THREADS) {
         s_key[j] = EMPTY_KEY;
         s_cnt[j] = 0u;
@@ -664,32 +662,49 @@ __global__ void k_fill(Tv* __restrict__ p, Tv v, uint64_t n) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// launchers (called from tsdf_capi.cpp; every kernel on the context's stream)
+// launchers (called from tsdf_capi.cpp)
 
 static int grid_for(uint64_t items, int per_block, int cap) {
     const uint64_t g = (items + per_block - 1) / per_block;
     return (int)(g < 1 ? 1 : (g > (uint64_t)cap ? (uint64_t)cap : g));
 }
 
-hipError_t launch_batch(const float* d_xyz, const BatchDesc& D, const RayConst& R, const Table& T,
-                        const Work& Wk, const Pool& Pl, Globals* G, int parity, hipStream_t st,
-                        KernelTimer* timer) {
-    if (D.n_blocks == 0) return hipSuccess;
-    if (timer) timer->begin(KIND_COUNT, st);
+// One batch is k_count -> k_compact -> k_place -> k_integrate -> k_finish on one stream; the host
+// (tsdf_capi.cpp) interleaves the cross-batch waits between them.
+hipError_t launch_count(const float* d_xyz, const BatchDesc& D, const RayConst& R, const Table& T,
+                        const Work& Wk, Globals* G, int parity, hipStream_t st) {
     k_count<<<D.n_blocks, CNT_THREADS, 0, st>>>(d_xyz, D, R, T, Wk, G, parity);
-    if (timer) timer->end(KIND_COUNT, st);
-    if (timer) timer->begin(KIND_COMPACT, st);
+    return hipGetLastError();
+}
+
+hipError_t launch_compact(const BatchDesc& D, const Table& T, const Work& Wk, Globals* G,
+                          int parity, hipStream_t st) {
     k_compact<<<grid_for(T.mask + 1, CMP_THREADS, 256), CMP_THREADS, 0, st>>>(D.n_scans, T, Wk,
                                                                                 G, parity);
-    if (timer) timer->end(KIND_COMPACT, st);
-    if (timer) timer->begin(KIND_PLACE, st);
+    return hipGetLastError();
+}
+
+hipError_t launch_place(const float* d_xyz, const BatchDesc& D, const RayConst& R, const Table& T,
+                        const Work& Wk, hipStream_t st) {
     k_place<<<D.n_blocks, PLC_THREADS, 0, st>>>(d_xyz, D, R, T, Wk);
-    if (timer) timer->end(KIND_PLACE, st);
-    if (timer) timer->begin(KIND_INTEGRATE, st);
-    hipError_t e = hipGetLastError();
-    if (e == hipSuccess) e = launch_integrate(D, R, T, Wk, Pl, G, parity, st);  // tsdf_integrate.hip
-    if (timer) timer->end(KIND_INTEGRATE, st);
-    return e;
+    return hipGetLastError();
+}
+
+// End of a batch: keep its counters as the "last batch" snapshot and zero them for the next batch
+// of the same parity (the same stream, so ordered after every reader of this batch).
+__global__ void k_finish(Globals* G, int parity) {
+    constexpr int NW = sizeof(Counters) / 4;
+    uint32_t* src = reinterpret_cast<uint32_t*>(&G->ctr[parity]);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(&G->last);
+    for (int j = threadIdx.x; j < NW; j += blockDim.x) {
+        dst[j] = src[j];
+        src[j] = 0u;
+    }
+}
+
+hipError_t launch_finish(Globals* G, int parity, hipStream_t st) {
+    k_finish<<<1, 64, 0, st>>>(G, parity);
+    return hipGetLastError();
 }
 
 hipError_t launch_query_dense(const Table& T, const Pool& Pl, const int lo[3], const int dims[3],

@@ -33,7 +33,7 @@ class TsdfParams(C.Structure):
         ("device_id", C.c_int32),
         ("brick_side", C.c_int32),
         ("max_batch", C.c_uint32),
-        ("reserved", C.c_uint32),
+        ("pipeline", C.c_uint32),
     ]
 
 

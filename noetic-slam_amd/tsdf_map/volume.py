@@ -45,13 +45,14 @@ class TSDFVolume:
 
     def __init__(self, lib, voxel_size, sdf_trunc, space_carving=False, min_range=0.0,
                  max_range=math.inf, max_bricks=1 << 20, max_points=1 << 18, device_id=0,
-                 max_batch=32):
+                 max_batch=32, pipeline=False):
         self._lib = lib
         self._ctx = C.c_void_p()
         p = _abi.default_params(lib)
         p.voxel_size = float(voxel_size)
         p.sdf_trunc = float(sdf_trunc)
         p.space_carving = 1 if space_carving else 0
+        p.pipeline = 1 if pipeline else 0
         p.min_range = float(min_range)
         p.max_range = float(max_range)
         p.max_bricks = int(max_bricks)

@@ -105,6 +105,37 @@ def test_batch_composition_is_invisible(sim):
         assert np.array_equal(x, y)
 
 
+def test_pipelined_and_64_scan_batches_bitwise(sim):
+    """Overlapped batches (tsdf_params.pipeline: batch b+1's count/compact/place beside batch b's
+    integrate, two streams) and 64-scan batches give the oracle's bits, through the host queue and
+    the device batch API, with read-outs interleaved between integrations."""
+    import torch
+    scans = [(decimate(p, 8), o) for p, o in (sim.scan(k) for k in range(70))]
+    o = ora()
+    for p, org in scans:
+        o.integrate(p, org)
+    ref = o.export_voxels()
+    for mb, pipe in ((2, True), (5, True), (64, False), (64, True)):
+        g = hip(max_batch=mb, pipeline=pipe)
+        for k, (p, org) in enumerate(scans):
+            g.integrate(p, org)
+            if k == 33:
+                assert g.num_bricks() > 0  # read-out in the middle joins both streams
+        for x, y in zip(g.export_voxels(), ref):
+            assert np.array_equal(x, y), (mb, pipe)
+    allp = np.concatenate([p for p, _ in scans])
+    offs = np.cumsum([0] + [p.shape[0] for p, _ in scans]).astype(np.uint64)
+    d = torch.from_numpy(allp).to("cuda:0")
+    torch.cuda.synchronize()
+    orgs = np.stack([org for _, org in scans])
+    g = hip(max_batch=7, pipeline=True)
+    for lo, hi in ((0, 20), (20, 21), (21, 70)):  # several calls, each several batches
+        g.integrate_batch_device(d.data_ptr() + 12 * int(offs[lo]),
+                                 (offs[lo:hi + 1] - offs[lo]).astype(np.uint64), orgs[lo:hi])
+    for x, y in zip(g.export_voxels(), ref):
+        assert np.array_equal(x, y)
+
+
 def test_queued_scans_flush_before_readout(sim):
     """A query right after queued host scans sees them (the queue is flushed first)."""
     p, org = sim.scan(0)
