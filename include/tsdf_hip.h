@@ -156,6 +156,17 @@ int tsdf_reset_stats(tsdf_ctx* ctx);
 /* Record HIP events around every kernel (per-kind device time in tsdf_stats.kernel_ms). */
 int tsdf_set_profiling(tsdf_ctx* ctx, int32_t on);
 
+/* Marching-cubes triangle mesh of the field (VDBFusion VDBVolume::extract_triangle_mesh; SURVEY
+ * §8f.1): every 2x2x2 voxel cube whose 8 voxels are observed (W > 0 and W >= min_weight) is
+ * meshed at S = 0.  Output: a triangle soup, 9 floats (3 vertices x, y, z, metres) per triangle,
+ * ordered by brick (z, y, x), then cube, then case-table order.  tri == NULL: only *n_tri is set;
+ * cap < *n_tri: TSDF_EOVERFLOW. */
+int tsdf_extract_mesh(tsdf_ctx* ctx, float min_weight, float* tri, uint64_t cap, uint64_t* n_tri);
+
+/* The generated marching-cubes case table (256 x 32 bytes: [case][0] = triangles, then 3 edge ids
+ * per triangle; corner c = (c & 1, c >> 1 & 1, c >> 2 & 1); edges axis-major). */
+int tsdf_mc_table(uint8_t* out);
+
 /* Azimuth-sector selection for multi-GPU sharding: keep the points whose azimuth around origin
  * (atan2(y-oy, x-ox) in [-pi, pi), offset by yaw0) falls in sector `sector` of `n_sectors`
  * equal sectors.  Writes the selected points packed to out_xyz (host, 3 f32 each). */

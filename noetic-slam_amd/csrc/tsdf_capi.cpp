@@ -238,6 +238,89 @@ static int settle(tsdf_ctx* c) {
     return rc ? rc : join(c);
 }
 
+// Marching-cubes case table, generated (the same construction as the oracle's
+// mc_build): per cube face the sign-change edges are paired into segments (ambiguous faces pair the
+// crossings around their inside corners, so neighbouring cubes agree), each directed with the
+// face's inside corners (S < 0) on its right seen from outside; the segments chain into cycles,
+// fanned into triangles.  Corner c = (c & 1, c >> 1 & 1, c >> 2 & 1); edges axis-major.
+struct McTable {
+    uint8_t tab[256][32];  // [case][0] = triangles, then 3 edge ids each
+    uint8_t edge[12][2];   // edge -> (a, b), b = a | axis bit
+};
+
+static McTable build_mc_table() {
+    McTable M{};
+    int ne = 0;
+    for (int d = 0; d < 3; d++)
+        for (int base = 0; base < 8; base++)
+            if (!(base & (1 << d))) {
+                M.edge[ne][0] = (uint8_t)base;
+                M.edge[ne][1] = (uint8_t)(base | (1 << d));
+                ne++;
+            }
+    auto edge_of = [&](int a, int b) {
+        for (int e = 0; e < 12; e++)
+            if ((M.edge[e][0] == a && M.edge[e][1] == b) || (M.edge[e][0] == b && M.edge[e][1] == a))
+                return e;
+        return -1;
+    };
+    for (int k = 0; k < 256; k++) {
+        int next[12];
+        std::fill(next, next + 12, -1);
+        for (int d = 0; d < 3; d++) {
+            const int u = (d + 1) % 3, w = (d + 2) % 3;
+            for (int side = 0; side < 2; side++) {
+                // face corners counter-clockwise seen from outside (outward normal (2 side - 1) e_d)
+                const int ou[4] = {0, 1, 1, 0}, ow[4] = {0, 0, 1, 1};
+                int q[4], in[4];
+                for (int i = 0; i < 4; i++) {
+                    const int cu = side ? ou[i] : ow[i], cw = side ? ow[i] : ou[i];
+                    q[i] = (side << d) | (cu << u) | (cw << w);
+                    in[i] = (k >> q[i]) & 1;
+                }
+                int cr[4], ncr = 0;
+                for (int i = 0; i < 4; i++)
+                    if (in[i] != in[(i + 1) & 3]) cr[ncr++] = i;
+                std::vector<std::pair<int, int>> pairs;
+                if (ncr == 2) pairs.push_back({cr[0], cr[1]});
+                if (ncr == 4) {
+                    if (in[0]) pairs = {{3, 0}, {1, 2}};
+                    else pairs = {{0, 1}, {2, 3}};
+                }
+                for (auto [i, j] : pairs) {
+                    const int ei = edge_of(q[i], q[(i + 1) & 3]), ej = edge_of(q[j], q[(j + 1) & 3]);
+                    // the corners q[i+1 .. j] are on the right of the segment i -> j
+                    if (in[(i + 1) & 3]) next[ei] = ej;
+                    else next[ej] = ei;
+                }
+            }
+        }
+        bool used[12] = {};
+        int nt = 0;
+        for (int e0 = 0; e0 < 12; e0++) {
+            if (next[e0] < 0 || used[e0]) continue;
+            int poly[12], n = 0;
+            for (int e = e0; !used[e] && n < 12; e = next[e]) {
+                used[e] = true;
+                poly[n++] = e;
+            }
+            for (int m = 1; m + 1 < n; m++) {
+                M.tab[k][1 + 3 * nt] = (uint8_t)poly[0];
+                M.tab[k][2 + 3 * nt] = (uint8_t)poly[m];
+                M.tab[k][3 + 3 * nt] = (uint8_t)poly[m + 1];
+                nt++;
+            }
+        }
+        M.tab[k][0] = (uint8_t)nt;
+    }
+    return M;
+}
+
+static const McTable& mc_table() {
+    static const McTable M = build_mc_table();
+    return M;
+}
+
 extern "C" {
 
 void tsdf_default_params(tsdf_params* p) {
@@ -390,6 +473,7 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
                              c->stream));
     HIPCHK(c, hipMemsetAsync(c->G, 0, sizeof(Globals), c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, upload_mc_table(mc_table().tab, mc_table().edge));
     return TSDF_OK;
 }
 
@@ -623,6 +707,70 @@ int tsdf_export_bricks(tsdf_ctx* c, int32_t* coords, float* sdf, float* weight, 
         if (sdf) std::memcpy(sdf + i * BRICK_VOX, s.data() + k * BRICK_VOX, BRICK_VOX * 4);
         if (weight) std::memcpy(weight + i * BRICK_VOX, w.data() + k * BRICK_VOX, BRICK_VOX * 4);
     }
+    return TSDF_OK;
+}
+
+int tsdf_mc_table(uint8_t* out) {
+    if (!out) return TSDF_EINVAL;
+    std::memcpy(out, mc_table().tab, sizeof(mc_table().tab));
+    return TSDF_OK;
+}
+
+int tsdf_extract_mesh(tsdf_ctx* c, float min_weight, float* tri, uint64_t cap, uint64_t* n_tri) {
+    if (!c || !n_tri) return TSDF_EINVAL;
+    uint64_t nb = 0;
+    int rc = pool_bricks(c, &nb);
+    if (rc) return rc;
+    *n_tri = 0;
+    if (!nb) return TSDF_OK;
+    if (nb >= 0xFFFFFFFFull) return fail(c, TSDF_EINVAL, "too many bricks");
+    // bricks in (z, y, x) order: the triangle soup's order (and the oracle's)
+    std::vector<uint64_t> keys(nb);
+    HIPCHK(c, hipMemcpy(keys.data(), c->T.brick_keys, nb * 8, hipMemcpyDeviceToHost));
+    std::sort(keys.begin(), keys.end(), [](uint64_t a, uint64_t b) {
+        for (int ax = 2; ax >= 0; ax--) {
+            const uint64_t x = (a >> (21 * ax)) & 0x1FFFFF, y = (b >> (21 * ax)) & 0x1FFFFF;
+            if (x != y) return x < y;
+        }
+        return false;
+    });
+    uint64_t* dk = nullptr;
+    uint32_t* dc = nullptr;
+    uint64_t* doff = nullptr;
+    float* dt = nullptr;
+    std::vector<uint32_t> cnt(nb);
+    std::vector<uint64_t> off(nb);
+    uint64_t total = 0;
+    hipError_t e = hipMalloc(&dk, nb * 8);
+    if (e == hipSuccess) e = hipMalloc(&dc, nb * 4);
+    if (e == hipSuccess) e = hipMemcpyAsync(dk, keys.data(), nb * 8, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess)
+        e = launch_mesh_count(c->T, c->Pl, dk, (uint32_t)nb, min_weight, dc, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(cnt.data(), dc, nb * 4, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess) {
+        for (uint64_t i = 0; i < nb; i++) {
+            off[i] = total;
+            total += cnt[i];
+        }
+        *n_tri = total;
+    }
+    if (e == hipSuccess && tri && total <= cap && total) {
+        e = hipMalloc(&doff, nb * 8);
+        if (e == hipSuccess) e = hipMalloc(&dt, total * 36);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(doff, off.data(), nb * 8, hipMemcpyHostToDevice, c->stream);
+        if (e == hipSuccess)
+            e = launch_mesh_emit(c->T, c->Pl, dk, (uint32_t)nb, min_weight, c->R.vs, doff, dt,
+                                 c->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(tri, dt, total * 36, hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    }
+    for (void* p : {(void*)dk, (void*)dc, (void*)doff, (void*)dt})
+        if (p) (void)hipFree(p);
+    if (e != hipSuccess) return fail(c, TSDF_EHIP, "extract_mesh: %s", hipGetErrorString(e));
+    if (tri && total > cap)
+        return fail(c, TSDF_EOVERFLOW, "mesh has %llu triangles", (unsigned long long)total);
     return TSDF_OK;
 }
 

@@ -156,6 +156,13 @@ hipError_t launch_import(const Table& T, const Pool& Pl, const int32_t* d_coords
                          const float* d_sdf, const float* d_w, uint32_t* d_tidx, Globals* G,
                          hipStream_t st);
 hipError_t launch_fill(float* p, float v, uint64_t n, hipStream_t st);
+// marching cubes (tsdf_mesh.hip)
+hipError_t upload_mc_table(const uint8_t tab[256][32], const uint8_t edge[12][2]);
+hipError_t launch_mesh_count(const Table& T, const Pool& Pl, const uint64_t* d_keys, uint32_t nb,
+                             float min_weight, uint32_t* d_counts, hipStream_t st);
+hipError_t launch_mesh_emit(const Table& T, const Pool& Pl, const uint64_t* d_keys, uint32_t nb,
+                            float min_weight, float vs, const uint64_t* d_offsets, float* d_tri,
+                            hipStream_t st);
 hipError_t launch_fill_u32(uint32_t* p, uint32_t v, uint64_t n, hipStream_t st);
 hipError_t launch_fill_u64(uint64_t* p, uint64_t v, uint64_t n, hipStream_t st);
 

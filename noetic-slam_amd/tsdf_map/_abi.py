@@ -86,6 +86,8 @@ SIGNATURES = {
     "tsdf_set_profiling": (C.c_int, [P, C.c_int32]),
     "tsdf_select_sector": (C.c_int, [FP, C.c_uint64, D3, C.c_double, C.c_uint32, C.c_uint32, FP,
                                      U64P]),
+    "tsdf_extract_mesh": (C.c_int, [P, C.c_float, FP, C.c_uint64, U64P]),
+    "tsdf_mc_table": (C.c_int, [C.POINTER(C.c_uint8)]),
 }
 
 

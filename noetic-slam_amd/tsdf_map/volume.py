@@ -137,6 +137,21 @@ class TSDFVolume:
                                                w.ctypes.data_as(_abi.FP)), "query_dense")
         return s, w
 
+    def extract_triangle_mesh(self, fill_holes=True, min_weight=0.0):
+        """VDBVolume.extract_triangle_mesh: (vertices (3T, 3) float32, triangles (T, 3) int64) —
+        marching cubes over every cube of 8 observed voxels (W > 0, W >= min_weight), as a soup
+        (each triangle owns its 3 vertices).  fill_holes is accepted for API compatibility; cubes
+        with an unobserved voxel are never meshed."""
+        n = C.c_uint64()
+        self._check(self._lib.tsdf_extract_mesh(self._ctx, float(min_weight), None, 0,
+                                                C.byref(n)), "extract_mesh")
+        t = np.empty((n.value, 9), np.float32)
+        if n.value:
+            self._check(self._lib.tsdf_extract_mesh(self._ctx, float(min_weight),
+                                                    t.ctypes.data_as(_abi.FP), n.value,
+                                                    C.byref(n)), "extract_mesh")
+        return t.reshape(-1, 3), np.arange(3 * t.shape[0], dtype=np.int64).reshape(-1, 3)
+
     def num_bricks(self):
         n = C.c_uint64()
         self._check(self._lib.tsdf_num_bricks(self._ctx, C.byref(n)), "num_bricks")

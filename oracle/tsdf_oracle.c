@@ -564,3 +564,138 @@ int tsdf_select_sector(const float* xyz, uint64_t n, const double origin[3], dou
     *n_out = k;
     return TSDF_OK;
 }
+
+/* ---- marching cubes (mesh extraction over the field) --------------------
+ *
+ * Semantics (the GPU's tsdf_extract_mesh restates the same):
+ *   A cube is the 2x2x2 voxels v + {0,1}^3; it is meshed when all 8 voxels are observed
+ *   (W > 0 and W >= min_weight).  Corner c = (c & 1, c >> 1 & 1, c >> 2 & 1) is INSIDE when S < 0.
+ *   The case table is built, not transcribed: on every cube face the sign-change edges are paired
+ *   into segments (an ambiguous face pairs the crossings around its inside corners, so the two
+ *   cubes sharing a face agree), each segment directed with the face's inside corners on its right
+ *   (seen from outside the cube), segments chained into cycles, cycles fan-triangulated.
+ *   A vertex on edge (a, b) (b = a + axis bit) is corner a's centre + t vs along the axis,
+ *   t = S_a / (S_a - S_b), corner centres at (i + 1/2) vs (fp32).
+ *   Output: triangle soup, 9 floats per triangle, bricks in (z, y, x) order, cubes by their min
+ *   voxel's in-brick index z*64 + y*8 + x, triangles in table order. */
+
+static uint8_t mc_tab[256][32]; /* [case][0] = triangles, then 3 edge ids each */
+static int mc_edge_a[12], mc_edge_b[12];
+static int mc_ready = 0;
+
+static int mc_edge_of(int a, int b) {
+    for (int e = 0; e < 12; e++)
+        if ((mc_edge_a[e] == a && mc_edge_b[e] == b) || (mc_edge_a[e] == b && mc_edge_b[e] == a))
+            return e;
+    return -1;
+}
+
+static void mc_build(void) {
+    int ne = 0;
+    for (int d = 0; d < 3; d++)
+        for (int base = 0; base < 8; base++)
+            if (!(base & (1 << d))) { mc_edge_a[ne] = base; mc_edge_b[ne] = base | (1 << d); ne++; }
+    for (int k = 0; k < 256; k++) {
+        int nxt[12];
+        for (int e = 0; e < 12; e++) nxt[e] = -1;
+        for (int d = 0; d < 3; d++) {
+            const int u = (d + 1) % 3, w = (d + 2) % 3;
+            for (int s = 0; s < 2; s++) {
+                /* face corners, counter-clockwise seen from outside (normal (2s-1) e_d) */
+                static const int cu_p[4] = {0, 1, 1, 0}, cw_p[4] = {0, 0, 1, 1};
+                int q[4];
+                for (int i = 0; i < 4; i++) {
+                    const int iu = s ? cu_p[i] : cw_p[i], iw = s ? cw_p[i] : cu_p[i];
+                    q[i] = (s << d) | (iu << u) | (iw << w);
+                }
+                int in[4], cr[4], ncr = 0;
+                for (int i = 0; i < 4; i++) in[i] = (k >> q[i]) & 1;
+                for (int i = 0; i < 4; i++)
+                    if (in[i] != in[(i + 1) & 3]) cr[ncr++] = i;
+                int pi[2], pj[2], np = 0;
+                if (ncr == 2) { pi[0] = cr[0]; pj[0] = cr[1]; np = 1; }
+                else if (ncr == 4) {
+                    if (in[0]) { pi[0] = 3; pj[0] = 0; pi[1] = 1; pj[1] = 2; }
+                    else { pi[0] = 0; pj[0] = 1; pi[1] = 2; pj[1] = 3; }
+                    np = 2;
+                }
+                for (int t = 0; t < np; t++) {
+                    const int i = pi[t], j = pj[t];
+                    const int ei = mc_edge_of(q[i], q[(i + 1) & 3]);
+                    const int ej = mc_edge_of(q[j], q[(j + 1) & 3]);
+                    /* corners q[i+1 .. j] lie on the right of the segment i -> j */
+                    const int arc_in = in[(i + 1) & 3];
+                    if (arc_in) nxt[ei] = ej; else nxt[ej] = ei;
+                }
+            }
+        }
+        int used[12] = {0}, nt = 0;
+        for (int e0 = 0; e0 < 12; e0++) {
+            if (nxt[e0] < 0 || used[e0]) continue;
+            int poly[12], n = 0, e = e0;
+            while (!used[e] && n < 12) { used[e] = 1; poly[n++] = e; e = nxt[e]; }
+            for (int m = 1; m + 1 < n; m++) {
+                mc_tab[k][1 + 3 * nt] = (uint8_t)poly[0];
+                mc_tab[k][2 + 3 * nt] = (uint8_t)poly[m];
+                mc_tab[k][3 + 3 * nt] = (uint8_t)poly[m + 1];
+                nt++;
+            }
+        }
+        mc_tab[k][0] = (uint8_t)nt;
+    }
+    mc_ready = 1;
+}
+
+int tsdf_mc_table(uint8_t* out) {
+    if (!out) return TSDF_EINVAL;
+    if (!mc_ready) mc_build();
+    memcpy(out, mc_tab, sizeof mc_tab);
+    return TSDF_OK;
+}
+
+int tsdf_extract_mesh(tsdf_ctx* c, float min_weight, float* tri, uint64_t cap, uint64_t* n_tri) {
+    if (!c || !n_tri) return TSDF_EINVAL;
+    if (!mc_ready) mc_build();
+    uint64_t nb = 0;
+    brick_ent* e = list_bricks(c, &nb);
+    if (!e) return TSDF_ENOMEM;
+    const float vs = c->vs;
+    uint64_t nt = 0;
+    for (uint64_t b = 0; b < nb; b++) {
+        for (int l = 0; l < 512; l++) {
+            const int32_t x = e[b].b[0] * 8 + (l & 7), y = e[b].b[1] * 8 + ((l >> 3) & 7),
+                          z = e[b].b[2] * 8 + (l >> 6);
+            float S[8];
+            int ok = 1, k = 0;
+            for (int q = 0; q < 8 && ok; q++) {
+                const vox_t* v = vox_find(c, x + (q & 1), y + ((q >> 1) & 1), z + ((q >> 2) & 1));
+                if (!v || !(v->W > 0.0f) || !(v->W >= min_weight)) { ok = 0; break; }
+                S[q] = v->S;
+                if (v->S < 0.0f) k |= 1 << q;
+            }
+            if (!ok) continue;
+            const int ntc = mc_tab[k][0];
+            for (int t = 0; t < ntc; t++) {
+                if (nt < cap && tri) {
+                    for (int j = 0; j < 3; j++) {
+                        const int ed = mc_tab[k][1 + 3 * t + j];
+                        const int a = mc_edge_a[ed], bb = mc_edge_b[ed];
+                        const int ax = (a ^ bb) == 1 ? 0 : ((a ^ bb) == 2 ? 1 : 2);
+                        const float tt = S[a] / (S[a] - S[bb]);
+                        float p[3] = {((float)(x + (a & 1)) + 0.5f) * vs,
+                                      ((float)(y + ((a >> 1) & 1)) + 0.5f) * vs,
+                                      ((float)(z + ((a >> 2) & 1)) + 0.5f) * vs};
+                        p[ax] = p[ax] + tt * vs;
+                        tri[9 * nt + 3 * j] = p[0];
+                        tri[9 * nt + 3 * j + 1] = p[1];
+                        tri[9 * nt + 3 * j + 2] = p[2];
+                    }
+                }
+                nt++;
+            }
+        }
+    }
+    free(e);
+    *n_tri = nt;
+    return (tri && nt > cap) ? TSDF_EOVERFLOW : TSDF_OK;  /* tri == NULL: count only */
+}
