@@ -167,6 +167,41 @@ int tsdf_extract_mesh(tsdf_ctx* ctx, float min_weight, float* tri, uint64_t cap,
  * per triangle; corner c = (c & 1, c >> 1 & 1, c >> 2 & 1); edges axis-major). */
 int tsdf_mc_table(uint8_t* out);
 
+/* ---- Ouster sensor input ------------------------------------------------------
+ * The reference's sensor path is the Ouster SDK (src/ouster/ouster-sdk/ouster_client): UDP lidar
+ * packets -> LidarScan field images (parsing.cpp, lidar_scan.cpp ScanBatcher) -> xyz via the
+ * make_xyz_lut LUT (lidar_scan.cpp:297-382, cartesian.h).  These entry points run that path on the
+ * GPU so a frame's raw packets can go straight to tsdf_integrate_device. */
+#define TSDF_OS_LEGACY 0
+#define TSDF_OS_RNG19_RFL8_SIG16_NIR16 1
+#define TSDF_OS_RNG19_RFL8_SIG16_NIR16_DUAL 2 /* first return only */
+#define TSDF_OS_RNG15_RFL8_NIR8 3
+
+typedef struct tsdf_os_format {
+    uint32_t profile;            /* TSDF_OS_* (metadata data_format.udp_profile_lidar) */
+    uint32_t pixels_per_column;  /* h */
+    uint32_t columns_per_packet;
+    uint32_t columns_per_frame;  /* w */
+} tsdf_os_format;
+
+/* Bytes of one lidar packet of this format (the UDP payload). */
+int tsdf_os_packet_bytes(const tsdf_os_format* fmt, uint32_t* bytes);
+
+/* Decode n_packets lidar packets of ONE frame (device memory, packed back to back) into staggered
+ * h x w row-major u32 images (device; any may be NULL): column = measurement_id, columns with
+ * status bit 0 clear are dropped, absent columns are 0 (the SDK's ScanBatcher).  Values are the
+ * SDK's field values (RANGE in mm, masked / shifted per profile). */
+int tsdf_os_decode_device(tsdf_ctx* ctx, const tsdf_os_format* fmt, const uint8_t* d_packets,
+                          uint32_t n_packets, uint32_t* d_range, uint32_t* d_signal,
+                          uint32_t* d_reflectivity, uint32_t* d_near_ir);
+
+/* World points of a range image: xyz = r dir + off (dir, off: the xyz LUT, n x 3 float32, device;
+ * r = 0 gives the sensor origin, dropped by the integrate), then x_world = pose * [xyz; 1] with
+ * pose a 3x4 row-major matrix.  d_xyz: n x 3 float32 (device), ready for tsdf_integrate_device
+ * with origin = the pose's translation. */
+int tsdf_os_cartesian_device(tsdf_ctx* ctx, const uint32_t* d_range, uint64_t n, const float* d_dir,
+                             const float* d_off, const double pose[12], float* d_xyz);
+
 /* Azimuth-sector selection for multi-GPU sharding: keep the points whose azimuth around origin
  * (atan2(y-oy, x-ox) in [-pi, pi), offset by yaw0) falls in sector `sector` of `n_sectors`
  * equal sectors.  Writes the selected points packed to out_xyz (host, 3 f32 each). */

@@ -710,6 +710,92 @@ int tsdf_export_bricks(tsdf_ctx* c, int32_t* coords, float* sdf, float* weight, 
     return TSDF_OK;
 }
 
+// Ouster packet layouts per UDP profile (ouster_client/src/parsing.cpp:42-175): header / column /
+// footer sizes and, for RANGE, SIGNAL, REFLECTIVITY, NEAR_IR: (bytes, offset, mask, shift).
+static bool os_layout(const tsdf_os_format* f, OsLayout& L) {
+    if (!f || f->pixels_per_column == 0 || f->columns_per_packet == 0 || f->columns_per_frame == 0 ||
+        f->pixels_per_column > 4096)
+        return false;
+    L = OsLayout{};
+    L.h = f->pixels_per_column;
+    L.w = f->columns_per_frame;
+    L.cols_per_packet = f->columns_per_packet;
+    switch (f->profile) {
+        case TSDF_OS_LEGACY:
+            L.pixel_bytes = 12;
+            L.f[0] = {4, 0, 0x000FFFFFu, 0};
+            L.f[1] = {2, 6, 0, 0};
+            L.f[2] = {2, 4, 0, 0};
+            L.f[3] = {2, 8, 0, 0};
+            break;
+        case TSDF_OS_RNG19_RFL8_SIG16_NIR16:
+            L.pixel_bytes = 12;
+            L.f[0] = {4, 0, 0x0007FFFFu, 0};
+            L.f[1] = {2, 6, 0, 0};
+            L.f[2] = {1, 4, 0, 0};
+            L.f[3] = {2, 8, 0, 0};
+            break;
+        case TSDF_OS_RNG19_RFL8_SIG16_NIR16_DUAL:
+            L.pixel_bytes = 16;
+            L.f[0] = {4, 0, 0x0007FFFFu, 0};
+            L.f[1] = {2, 8, 0, 0};
+            L.f[2] = {1, 3, 0, 0};
+            L.f[3] = {2, 12, 0, 0};
+            break;
+        case TSDF_OS_RNG15_RFL8_NIR8:
+            L.pixel_bytes = 4;
+            L.f[0] = {2, 0, 0x7FFFu, -3};
+            L.f[1] = {0, 0, 0, 0};
+            L.f[2] = {1, 2, 0, 0};
+            L.f[3] = {1, 3, 0, -4};
+            break;
+        default:
+            return false;
+    }
+    L.legacy = f->profile == TSDF_OS_LEGACY ? 1u : 0u;
+    L.packet_header = L.legacy ? 0u : 32u;
+    L.col_header = L.legacy ? 16u : 12u;
+    const uint32_t col_footer = L.legacy ? 4u : 0u, packet_footer = L.legacy ? 0u : 32u;
+    L.col_bytes = L.col_header + L.h * L.pixel_bytes + col_footer;
+    L.packet_bytes = L.packet_header + L.cols_per_packet * L.col_bytes + packet_footer;
+    return true;
+}
+
+int tsdf_os_packet_bytes(const tsdf_os_format* fmt, uint32_t* bytes) {
+    OsLayout L;
+    if (!bytes || !os_layout(fmt, L)) return TSDF_EINVAL;
+    *bytes = L.packet_bytes;
+    return TSDF_OK;
+}
+
+int tsdf_os_decode_device(tsdf_ctx* c, const tsdf_os_format* fmt, const uint8_t* d_packets,
+                          uint32_t n_packets, uint32_t* d_range, uint32_t* d_signal,
+                          uint32_t* d_reflectivity, uint32_t* d_near_ir) {
+    if (!c) return TSDF_EINVAL;
+    OsLayout L;
+    if (!os_layout(fmt, L)) return fail(c, TSDF_EINVAL, "bad Ouster packet format");
+    if (n_packets && !d_packets) return fail(c, TSDF_EINVAL, "null packets");
+    HIPCHK(c, hipSetDevice(c->device));
+    uint32_t* out[4] = {d_range, d_signal, d_reflectivity, d_near_ir};
+    const size_t img = (size_t)L.h * L.w * sizeof(uint32_t);
+    for (int k = 0; k < 4; k++)
+        if (out[k]) HIPCHK(c, hipMemsetAsync(out[k], 0, img, c->stream));
+    HIPCHK(c, launch_os_decode(d_packets, n_packets, L, out, c->stream));
+    return TSDF_OK;
+}
+
+int tsdf_os_cartesian_device(tsdf_ctx* c, const uint32_t* d_range, uint64_t n, const float* d_dir,
+                             const float* d_off, const double pose[12], float* d_xyz) {
+    if (!c) return TSDF_EINVAL;
+    if (n && (!d_range || !d_dir || !d_off || !d_xyz)) return fail(c, TSDF_EINVAL, "null argument");
+    if (!pose) return fail(c, TSDF_EINVAL, "null pose");
+    HIPCHK(c, hipSetDevice(c->device));
+    OsPose P;
+    for (int k = 0; k < 12; k++) P.m[k] = (float)pose[k];
+    HIPCHK(c, launch_os_xyz(d_range, n, d_dir, d_off, P, d_xyz, c->stream));
+    return TSDF_OK;
+}
+
 int tsdf_mc_table(uint8_t* out) {
     if (!out) return TSDF_EINVAL;
     std::memcpy(out, mc_table().tab, sizeof(mc_table().tab));

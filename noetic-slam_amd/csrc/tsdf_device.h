@@ -156,6 +156,25 @@ hipError_t launch_import(const Table& T, const Pool& Pl, const int32_t* d_coords
                          const float* d_sdf, const float* d_w, uint32_t* d_tidx, Globals* G,
                          hipStream_t st);
 hipError_t launch_fill(float* p, float v, uint64_t n, hipStream_t st);
+// Ouster packets (tsdf_ouster.hip)
+struct OsField {
+    uint32_t nbytes;  // little-endian source bytes (0: the profile has no such field)
+    uint32_t offset;  // byte offset in the pixel
+    uint32_t mask;    // 0: none
+    int32_t shift;    // > 0: right, < 0: left
+};
+struct OsLayout {
+    uint32_t h, w, cols_per_packet, packet_bytes, packet_header, col_header, col_bytes,
+        pixel_bytes, legacy;
+    OsField f[4];  // RANGE, SIGNAL, REFLECTIVITY, NEAR_IR
+};
+struct OsPose {
+    float m[12];  // 3x4 row-major (rotation | translation), fp32
+};
+hipError_t launch_os_decode(const uint8_t* d_packets, uint32_t n_packets, const OsLayout& L,
+                            uint32_t* const out[4], hipStream_t st);
+hipError_t launch_os_xyz(const uint32_t* d_range, uint64_t n, const float* d_dir,
+                         const float* d_off, const OsPose& P, float* d_xyz, hipStream_t st);
 // marching cubes (tsdf_mesh.hip)
 hipError_t upload_mc_table(const uint8_t tab[256][32], const uint8_t edge[12][2]);
 hipError_t launch_mesh_count(const Table& T, const Pool& Pl, const uint64_t* d_keys, uint32_t nb,

@@ -67,6 +67,16 @@ D3 = C.POINTER(C.c_double)
 I3 = C.POINTER(C.c_int32)
 FP = C.POINTER(C.c_float)
 U64P = C.POINTER(C.c_uint64)
+class OsFormat(C.Structure):
+    """tsdf_os_format (include/tsdf_hip.h)."""
+    _fields_ = [("profile", C.c_uint32), ("pixels_per_column", C.c_uint32),
+                ("columns_per_packet", C.c_uint32), ("columns_per_frame", C.c_uint32)]
+
+
+OS_PROFILES = {"LEGACY": 0, "RNG19_RFL8_SIG16_NIR16": 1, "RNG19_RFL8_SIG16_NIR16_DUAL": 2,
+               "RNG15_RFL8_NIR8": 3}
+
+
 SIGNATURES = {
     "tsdf_default_params": (None, [C.POINTER(TsdfParams)]),
     "tsdf_abi_version": (C.c_int, []),
@@ -88,6 +98,9 @@ SIGNATURES = {
                                      U64P]),
     "tsdf_extract_mesh": (C.c_int, [P, C.c_float, FP, C.c_uint64, U64P]),
     "tsdf_mc_table": (C.c_int, [C.POINTER(C.c_uint8)]),
+    "tsdf_os_packet_bytes": (C.c_int, [C.POINTER(OsFormat), C.POINTER(C.c_uint32)]),
+    "tsdf_os_decode_device": (C.c_int, [P, C.POINTER(OsFormat), P, C.c_uint32, P, P, P, P]),
+    "tsdf_os_cartesian_device": (C.c_int, [P, P, C.c_uint64, P, P, C.POINTER(C.c_double), P]),
 }
 
 

@@ -22,7 +22,8 @@ from tsdf_map.volume import TSDFVolume  # noqa: E402
 LIB_PATH = os.path.join(HERE, "build", "libtsdf_oracle.so")
 MODE_SCAN_FUSED = 0
 MODE_SEQUENTIAL = 1
-HOST_ONLY = ("tsdf_integrate_device", "tsdf_integrate_batch_device", "tsdf_set_profiling")
+HOST_ONLY = ("tsdf_integrate_device", "tsdf_integrate_batch_device", "tsdf_set_profiling",
+             "tsdf_os_packet_bytes", "tsdf_os_decode_device", "tsdf_os_cartesian_device")
 
 _lib = None
 
