@@ -26,14 +26,27 @@ namespace tsdf {
 
 constexpr int INT_THREADS = 256;
 #ifndef TSDF_INT_PER
-#define TSDF_INT_PER 4
+#define TSDF_INT_PER 6
 #endif
 constexpr int INT_PER = TSDF_INT_PER;                // register-cached samples per thread
 constexpr uint32_t INT_CAP = INT_PER * INT_THREADS;  // samples (>= live cells) per window
 // LDS: 12 B per cell + ~9.5 KB per workgroup; residency as LDS allows
 constexpr int INT_BLOCKS_PER_CU = (160 * 1024) / (INT_CAP * 12 + 10 * 1024);
-constexpr uint32_t INT_MAX_WIN = 32;                 // scans per window (u32 masks)
+#ifndef TSDF_INT_WIN
+#define TSDF_INT_WIN 64
+#endif
+#if TSDF_INT_WIN == 64
+typedef unsigned long long MaskT;  // a voxel's scans in the window, one bit per scan
+#define MASK_POPC(m) __popcll(m)
+#else
+typedef uint32_t MaskT;
+#define MASK_POPC(m) __popc(m)
+#endif
+constexpr uint32_t INT_MAX_WIN = TSDF_INT_WIN;       // scans per window (mask bits)
 
+#ifdef TSDF_ABLATE_PHASE  // `make ablate ABLATE=PHASE`
+#define TSDF_PHASE_TIMING
+#endif
 // Diagnostic build only (-DTSDF_PHASE_TIMING, never shipped): thread 0 of a few workgroups drains
 // its memory counters at each phase boundary and prints the cycles spent per phase.
 #ifdef TSDF_PHASE_TIMING
@@ -54,7 +67,7 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchDesc D, Table T,
                                                           Globals* G, int parity, float tau) {
     __shared__ unsigned long long cA[INT_CAP];  // live cell: sum of trunc(s * 2^32)
     __shared__ uint32_t cB[INT_CAP];            // live cell: sample count
-    __shared__ uint32_t sMask[BRICK_VOX];       // voxel: scans (bit t - t0) observed in the window
+    __shared__ MaskT sMask[BRICK_VOX];          // voxel: scans (bit t - t0) observed in the window
     __shared__ uint32_t sBase[BRICK_VOX];       // voxel: first live cell
     __shared__ float sS[BRICK_VOX], sW[BRICK_VOX];
     __shared__ uint16_t sLive[BRICK_VOX];  // live voxels of the window
@@ -62,18 +75,14 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchDesc D, Table T,
     // previous brick's prefix while another writes the next one
     __shared__ uint32_t s_csb[2][MAX_BATCH + 1];
     __shared__ uint32_t s_red[INT_THREADS / 64];
-    __shared__ uint32_t s_nlive, s_q, s_ncell;
+    __shared__ uint32_t s_nlive, s_ncell;
     float2* cF = reinterpret_cast<float2*>(cA);  // P4: cells converted to (A 2^-32, B) as f32
     Counters* C = &G->ctr[parity];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const uint32_t n_active = min(C->n_active, Wk.max_active);
     const uint32_t ns = D.n_scans;
-    for (uint32_t j = tid; j < INT_CAP; j += INT_THREADS) {
-        cA[j] = 0ull;
-        cB[j] = 0u;
-    }
-    sMask[tid] = 0u;
-    sMask[tid + 256] = 0u;
+    sMask[tid] = 0;
+    sMask[tid + 256] = 0;
     uint32_t nvox = 0, ndirty = 0, par = 0;
 #ifdef TSDF_PHASE_TIMING
     unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t_last = clock64();
@@ -138,9 +147,11 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchDesc D, Table T,
         PHASE(1);
         for (uint32_t t0 = 0; t0 < ns;) {
             // window [t0, t1): as many scans as keep its samples <= INT_CAP (at least one)
+            // (the extension test is monotone in the scan: one lane per candidate, one ballot)
             const uint32_t q0 = s_cs[t0];
-            uint32_t t1 = t0 + 1;
-            while (t1 < ns && t1 - t0 < INT_MAX_WIN && s_cs[t1 + 1] - q0 <= INT_CAP) t1++;
+            const uint32_t tt = t0 + 1 + lane;
+            const bool ext = tt < ns && tt - t0 < INT_MAX_WIN && s_cs[min(tt + 1, ns)] - q0 <= INT_CAP;
+            const uint32_t t1 = t0 + 1 + (uint32_t)__popcll(__ballot(ext));
             const uint32_t q1 = s_cs[t1], nw = t1 - t0;
             if (q0 == q1) {  // uniform: no sample of this brick in the window
                 t0 = t1;
@@ -166,15 +177,15 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchDesc D, Table T,
 #else
                     if (w < nw)
 #endif
-                        atomicOr(&sMask[c[j].y & 511u], 1u << w);
+                        atomicOr(&sMask[c[j].y & 511u], (MaskT)1 << w);
                 }
             }
             __syncthreads();
             PHASE(3);
             // P2: live cells and live voxels (packed block scan: cells | voxels << 16)
             {
-                const uint32_t m0 = sMask[2 * tid], m1 = sMask[2 * tid + 1];
-                const uint32_t c0 = __popc(m0), c1 = __popc(m1);
+                const MaskT m0 = sMask[2 * tid], m1 = sMask[2 * tid + 1];
+                const uint32_t c0 = MASK_POPC(m0), c1 = MASK_POPC(m1);
                 const uint32_t v0 = m0 ? 1u : 0u, v1 = m1 ? 1u : 0u;
                 dirty |= v0 | (v1 << 1);
                 const uint32_t x = (c0 + c1) | ((v0 + v1) << 16);
@@ -202,8 +213,12 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchDesc D, Table T,
                 if (tid == 0) {
                     s_nlive = tot >> 16;
                     s_ncell = tot & 0xFFFFu;
-                    s_q = 0u;
                     nvox += tot & 0xFFFFu;  // (voxel, scan) updates of the window
+                }
+                // the window's cells start at zero (the previous window's P4 is past a barrier)
+                for (uint32_t j = tid; j < (tot & 0xFFFFu); j += INT_THREADS) {
+                    cA[j] = 0ull;
+                    cB[j] = 0u;
                 }
             }
             __syncthreads();
@@ -224,7 +239,7 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchDesc D, Table T,
                     const uint32_t w = (c[j].y >> 9) - t0;
                     if (w < nw) {
                         const uint32_t l = c[j].y & 511u;
-                        const uint32_t cell = sBase[l] + __popc(sMask[l] & ((1u << w) - 1u));
+                        const uint32_t cell = sBase[l] + MASK_POPC(sMask[l] & (((MaskT)1 << w) - 1));
                         const long long fx = (long long)(__uint_as_float(c[j].x) * 4294967296.0f);
 #ifdef TSDF_ABLATE_INT_NOP3
                         if (fx == 12345)
@@ -245,42 +260,47 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchDesc D, Table T,
                 for (uint32_t j = tid; j < ncell; j += INT_THREADS) {
                     const long long av = (long long)cA[j];
                     const uint32_t bv = cB[j];
-                    cB[j] = 0u;
                     cF[j] = make_float2((float)((double)av * (1.0 / 4294967296.0)), (float)bv);
                 }
             }
             __syncthreads();
-            // P4b: fuse, live voxels from a work queue; each lane runs one voxel's chain at a time
+            // P4b: fuse.  Lane tid takes live voxels tid, tid + 256 and runs each one's chain in scan
+            // order; the next cell is read from LDS while the current step divides, so a step costs
+            // the arithmetic only (the critical path of a window is its longest chain).
             {
 #ifdef TSDF_ABLATE_INT_NOP4
                 const uint32_t nlive = 0;
 #else
                 const uint32_t nlive = s_nlive;
 #endif
-                uint32_t l = 0, cell = 0, rem = 0;
-                float s = 0.0f, wt = 0.0f;
-                while (true) {
-                    if (rem == 0) {
-                        const uint32_t vi = atomicAdd(&s_q, 1u);
-                        if (vi >= nlive) break;
-                        l = sLive[vi];
-                        cell = sBase[l];
-                        const uint32_t m = sMask[l];
-                        sMask[l] = 0u;
-                        rem = __popc(m);
-                        s = sS[l];
-                        wt = sW[l];
+                for (uint32_t vi = tid; vi < nlive; vi += INT_THREADS) {
+                    const uint32_t l = sLive[vi];
+                    const uint32_t cell = sBase[l];
+                    const uint32_t rem = MASK_POPC(sMask[l]);
+                    sMask[l] = 0;
+                    float s = sS[l], wt = sW[l];
+                    // two cells in flight: a step's operand was read one step earlier
+                    float2 va = cF[cell], vb = cF[min(cell + 1u, INT_CAP - 1u)];
+                    // branch-free body (one basic block, so the reads stay ahead of their use);
+                    // the second step of a pair is dropped past the chain's end
+                    typedef const volatile __attribute__((address_space(3))) uint64_t lds_u64;
+                    lds_u64* cV = (lds_u64*)(cA);
+                    for (uint32_t k = 0; k < rem; k += 2) {
+                        const uint64_t na = cV[min(cell + k + 2, INT_CAP - 1u)];
+                        float nwt = wt + va.y;
+                        s = (s * wt + va.x) / nwt;
+                        wt = nwt;
+                        const uint64_t nb = cV[min(cell + k + 3, INT_CAP - 1u)];
+                        nwt = wt + vb.y;
+                        const float s2 = (s * wt + vb.x) / nwt;
+                        const bool more = k + 1 < rem;
+                        s = more ? s2 : s;
+                        wt = more ? nwt : wt;
+                        va = make_float2(__uint_as_float((uint32_t)na), __uint_as_float((uint32_t)(na >> 32)));
+                        vb = make_float2(__uint_as_float((uint32_t)nb), __uint_as_float((uint32_t)(nb >> 32)));
                     }
-                    const float2 v = cF[cell];
-                    cA[cell] = 0ull;
-                    const float nwt = wt + v.y;
-                    s = (s * wt + v.x) / nwt;
-                    wt = nwt;
-                    cell++;
-                    if (--rem == 0) {
-                        sS[l] = s;
-                        sW[l] = wt;
-                    }
+                    sS[l] = s;
+                    sW[l] = wt;
                 }
             }
             __syncthreads();

@@ -23,6 +23,14 @@ def load_hip_library(path=None):
     if not os.path.exists(p):
         raise RuntimeError("libtsdf_hip.so not built (%s); run `python -c 'import __graft_entry__ "
                            "as g; g.build()'` or `make -C noetic-slam_amd/csrc`" % p)
+    # One HIP runtime per process: torch ships its own libamdhip64 (SONAME libamdhip64.so.7, but
+    # needed as "libamdhip64.so"), so it is loaded first and the library's libamdhip64.so.7 then
+    # resolves to that copy.  Loaded the other way round, the process holds two runtimes and
+    # torch finds no GPU.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = _abi.declare(ctypes.CDLL(p))
     if lib.tsdf_abi_version() != ABI_VERSION:
         raise RuntimeError("libtsdf_hip.so ABI version mismatch")
