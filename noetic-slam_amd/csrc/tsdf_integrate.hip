@@ -47,12 +47,15 @@ constexpr uint32_t INT_MAX_WIN = TSDF_INT_WIN;       // scans per window (mask b
 #ifdef TSDF_ABLATE_PHASE  // `make ablate ABLATE=PHASE`
 #define TSDF_PHASE_TIMING
 #endif
-// Diagnostic build only (-DTSDF_PHASE_TIMING, never shipped): thread 0 of a few workgroups drains
-// its memory counters at each phase boundary and prints the cycles spent per phase.
+#ifdef TSDF_ABLATE_PHASE  // `make ablate ABLATE=PHASE`
+#define TSDF_PHASE_TIMING
+#endif
+// Diagnostic build only (-DTSDF_PHASE_TIMING, never shipped): thread 0 of a few workgroups reads
+// the clock at each phase boundary (no counter drain: outstanding loads stay in flight) and
+// prints the cycles spent per phase.
 #ifdef TSDF_PHASE_TIMING
 #define PHASE(k)                                 \
     do {                                         \
-        __builtin_amdgcn_s_waitcnt(0);           \
         const unsigned long long t_ = clock64(); \
         ph[k] += t_ - t_last;                    \
         t_last = t_;                             \
@@ -85,8 +88,8 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchDesc D, Table T,
     sMask[tid + 256] = 0;
     uint32_t nvox = 0, ndirty = 0, par = 0;
 #ifdef TSDF_PHASE_TIMING
-    unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t_last = clock64();
-    uint32_t nb = 0;
+    unsigned long long ph[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, t_last = clock64();
+    uint32_t nb = 0, nwin = 0;
 #endif
     // Software pipeline over the workgroup's bricks: while brick a is processed, brick a + G's
     // cell row, (S, W) and first INT_CAP samples are in flight to registers (BrickRegs), and
@@ -131,6 +134,14 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchDesc D, Table T,
 #pragma unroll
         for (int j = 0; j < INT_PER; j++) c[j] = B.c[j];
         uint32_t cq = 0;  // samples [cq, cq + INT_CAP) are in c[] (uniform)
+        auto load_chunk = [&](uint32_t q) {
+            cq = q;
+#pragma unroll
+            for (int j = 0; j < INT_PER; j++) {
+                const uint32_t i = q + tid + j * INT_THREADS;
+                c[j] = (i < n && base + i < Wk.max_smp) ? Wk.smp[base + i] : make_uint2(0u, ~0u);
+            }
+        };
         const bool has_slot = cur.y < T.max_bricks;
         if ((uint32_t)tid < ns) s_cs[tid] = B.cell;
         if (tid == 0) s_cs[ns] = n;
@@ -157,16 +168,13 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchDesc D, Table T,
                 t0 = t1;
                 continue;
             }
+#ifdef TSDF_PHASE_TIMING
+            nwin++;
+#endif
             // P1: scan masks (a one-scan window may exceed INT_CAP samples: chunked)
             for (uint32_t qc = q0; qc < q1; qc += INT_CAP) {
                 if (cq != qc) {
-                    cq = qc;
-#pragma unroll
-                    for (int j = 0; j < INT_PER; j++) {
-                        const uint32_t i = cq + tid + j * INT_THREADS;
-                        c[j] = (i < n && base + i < Wk.max_smp) ? Wk.smp[base + i]
-                                                                : make_uint2(0u, ~0u);
-                    }
+                    load_chunk(qc);
                     PHASE(2);
                 }
 #pragma unroll
@@ -226,13 +234,7 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchDesc D, Table T,
             // P3: accumulate into the live cells
             for (uint32_t qc = q0; qc < q1; qc += INT_CAP) {
                 if (cq != qc) {
-                    cq = qc;
-#pragma unroll
-                    for (int j = 0; j < INT_PER; j++) {
-                        const uint32_t i = cq + tid + j * INT_THREADS;
-                        c[j] = (i < n && base + i < Wk.max_smp) ? Wk.smp[base + i]
-                                                                : make_uint2(0u, ~0u);
-                    }
+                    load_chunk(qc);
                 }
 #pragma unroll
                 for (int j = 0; j < INT_PER; j++) {
@@ -251,6 +253,8 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchDesc D, Table T,
                     }
                 }
             }
+            // the next window starts at q1: its samples load while this one converts and fuses
+            if (q1 < n) load_chunk(q1);
             __syncthreads();
             PHASE(5);
             // P4a: convert every live cell to (A 2^-32, B) in f32, in parallel, so the serial
@@ -264,6 +268,7 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchDesc D, Table T,
                 }
             }
             __syncthreads();
+            PHASE(8);
             // P4b: fuse.  Lane tid takes live voxels tid, tid + 256 and runs each one's chain in scan
             // order; the next cell is read from LDS while the current step divides, so a step costs
             // the arithmetic only (the critical path of a window is its longest chain).
@@ -328,9 +333,9 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchDesc D, Table T,
     }
 #ifdef TSDF_PHASE_TIMING
     if (tid == 0 && (blockIdx.x % 97) == 0)
-        printf("phase blk %u bricks %u meta %llu bar0 %llu load %llu mask %llu scan %llu acc %llu "
-               "fuse %llu tail %llu\n", blockIdx.x, nb, ph[0], ph[1], ph[2], ph[3], ph[4], ph[5],
-               ph[6], ph[7]);
+        printf("phase blk %u bricks %u windows %u meta %llu bar0 %llu load %llu mask %llu scan %llu "
+               "acc %llu conv %llu fuse %llu tail %llu\n", blockIdx.x, nb, nwin, ph[0], ph[1], ph[2],
+               ph[3], ph[4], ph[5], ph[8], ph[6], ph[7]);
 #endif
     const unsigned long long v = wave_sum<unsigned long long>(nvox);
     const unsigned long long d = wave_sum<unsigned long long>(ndirty);
