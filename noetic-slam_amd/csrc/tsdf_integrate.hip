@@ -109,7 +109,9 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchDesc D, Table T,
             B.c[j] = (i < n && base + i < Wk.max_smp) ? Wk.smp[base + i] : make_uint2(0u, ~0u);
         }
         // absolute position of the brick's scan-tid samples -> relative to its segment
-        B.cell = (uint32_t)tid < ns ? T.cell[(size_t)r.x * T.cell_stride + tid] - base : 0u;
+        // (made relative to the segment where it is consumed: a use here, or a load inside a
+        // branch, would make the compiler wait for this prefetch at once)
+        B.cell = T.cell[(size_t)r.x * T.cell_stride + min((uint32_t)tid, T.cell_stride - 1u)];
         const float* Sg = Pl.sdf + (size_t)(has ? r.y : 0) * BRICK_VOX;
         const float* Wg = Pl.weight + (size_t)(has ? r.y : 0) * BRICK_VOX;
         B.s0 = has ? Sg[tid] : tau;
@@ -143,7 +145,7 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchDesc D, Table T,
             }
         };
         const bool has_slot = cur.y < T.max_bricks;
-        if ((uint32_t)tid < ns) s_cs[tid] = B.cell;
+        if ((uint32_t)tid < ns) s_cs[tid] = B.cell - base;
         if (tid == 0) s_cs[ns] = n;
         float* Sg = Pl.sdf + (size_t)(has_slot ? cur.y : 0) * BRICK_VOX;
         float* Wg = Pl.weight + (size_t)(has_slot ? cur.y : 0) * BRICK_VOX;

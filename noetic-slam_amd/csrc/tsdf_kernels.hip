@@ -514,10 +514,23 @@ __global__ __launch_bounds__(PLC_THREADS) void k_place(const float* __restrict__
                 const uint64_t key = brick_key_of(r.vx, r.vy, r.vz);
                 const bool nb = g && key != cur;  // the ray's next pair, in k_count's order
                 cur = nb ? key : cur;
-                pos = nb ? (k == 0 ? P0 : k == 1 ? P1 : k == 2 ? P2 : k == 3 ? P3 : NO_PAIR) : pos;
-                lpos = nb ? (k == 0 ? L0 : k == 1 ? L1 : k == 2 ? L2 : k == 3 ? L3 : NO_PAIR) : lpos;
-                cnt = nb ? (k == 0 ? N0 : k == 1 ? N1 : k == 2 ? N2 : k == 3 ? N3 : 0u) : cnt;
-                k += nb ? 1u : 0u;
+                // take the head of the ray's pair queue (P0, L0, N0) and shift the queue: plain
+                // selects (a select on the pair index k compiles to branches)
+                pos = nb ? P0 : pos;
+                lpos = nb ? L0 : lpos;
+                cnt = nb ? N0 : cnt;
+                P0 = nb ? P1 : P0;
+                P1 = nb ? P2 : P1;
+                P2 = nb ? P3 : P2;
+                P3 = nb ? NO_PAIR : P3;
+                L0 = nb ? L1 : L0;
+                L1 = nb ? L2 : L1;
+                L2 = nb ? L3 : L2;
+                L3 = nb ? NO_PAIR : L3;
+                N0 = nb ? N1 : N0;
+                N1 = nb ? N2 : N1;
+                N2 = nb ? N3 : N2;
+                N3 = nb ? 0u : N3;
                 w = nb ? 0u : w;
                 const bool st = g && w < cnt;
                 const uint32_t l = ((r.vz & 7) << 6) | ((r.vy & 7) << 3) | (r.vx & 7);

@@ -7,6 +7,6 @@ mkdir -p "$OUT"
 for v in ${VARIANTS:-real PLACE_NOWRITE INT_NOATOM INT_NOFUSE}; do
   lib=""
   [ "$v" != real ] && lib="noetic-slam_amd/lib/ablate/libtsdf_hip_$v.so"
-  TSDF_HIP_LIB=$lib timeout -k 10 300 python3 bench.py --steps 4 --warmup 1 --no-cpu > "$OUT/$v.json"
+  TSDF_HIP_LIB=$lib timeout -k 10 300 python3 bench.py --steps ${STEPS:-16} --warmup 2 --no-cpu > "$OUT/$v.json"
   python3 -c "import json,sys; d=json.load(open('$OUT/$v.json')); print('$v', d['value'], d['kernel_ms_per_launch'])"
 done
