@@ -487,9 +487,11 @@ __global__ __launch_bounds__(PLC_THREADS) void k_place(const float* __restrict__
         // Short rays (maxp <= 4): all of the ray's pairs are resolved up front, convergent across
         // lanes; the walk then only selects the k-th.
         const bool fast = maxp <= 4;
+        // pair queue: global position P, and (staging position | count << 16) Q; a staging
+        // position of 0xFFFF (>= PLC_STAGE) means not staged
         uint32_t P0 = NO_PAIR, P1 = NO_PAIR, P2 = NO_PAIR, P3 = NO_PAIR;
-        uint32_t L0 = NO_PAIR, L1 = NO_PAIR, L2 = NO_PAIR, L3 = NO_PAIR;
-        uint32_t N0 = 0, N1 = 0, N2 = 0, N3 = 0;
+        uint32_t Q0 = 0xFFFFu, Q1 = 0xFFFFu, Q2 = 0xFFFFu, Q3 = 0xFFFFu;
+        static_assert(PLC_STAGE < 0xFFFF, "staging positions are 16-bit");
         if (fast) {
             uint4 code = code4;
             if (maxp < 4) {
@@ -497,10 +499,15 @@ __global__ __launch_bounds__(PLC_THREADS) void k_place(const float* __restrict__
                 if (maxp > 1) code.y = pc[1];
                 if (maxp > 2) code.z = pc[2];
             }
-            resolve(code.x, P0, L0, N0);
-            resolve(code.y, P1, L1, N1);
-            resolve(code.z, P2, L2, N2);
-            resolve(code.w, P3, L3, N3);
+            auto resolve_q = [&](uint32_t c, uint32_t& P, uint32_t& Q) {
+                uint32_t lp, n;
+                resolve(c, P, lp, n);
+                Q = min(lp, 0xFFFFu) | (n << 16);
+            };
+            resolve_q(code.x, P0, Q0);
+            resolve_q(code.y, P1, Q1);
+            resolve_q(code.z, P2, Q2);
+            resolve_q(code.w, P3, Q3);
         }
         uint64_t cur = EMPTY_KEY;
         // current pair: global position, or staging position (lpos < PLC_STAGE)
@@ -508,6 +515,7 @@ __global__ __launch_bounds__(PLC_THREADS) void k_place(const float* __restrict__
         if (fast) {
             // Branch-free walk: lanes are at different steps of different pairs, so every
             // data-dependent branch here would run for the whole wave; selects cost less.
+            uint32_t lq = 0xFFFFu;  // current pair's (staging position | count << 16)
             for (int it = 0; it < MAX_DDA_STEPS; it++) {
                 float s;
                 const bool g = voxel_sample_sel(R, ox, oy, oz, r, s);
@@ -517,24 +525,20 @@ __global__ __launch_bounds__(PLC_THREADS) void k_place(const float* __restrict__
                 // take the head of the ray's pair queue (P0, L0, N0) and shift the queue: plain
                 // selects (a select on the pair index k compiles to branches)
                 pos = nb ? P0 : pos;
-                lpos = nb ? L0 : lpos;
-                cnt = nb ? N0 : cnt;
+                lq = nb ? Q0 : lq;
                 P0 = nb ? P1 : P0;
                 P1 = nb ? P2 : P1;
                 P2 = nb ? P3 : P2;
                 P3 = nb ? NO_PAIR : P3;
-                L0 = nb ? L1 : L0;
-                L1 = nb ? L2 : L1;
-                L2 = nb ? L3 : L2;
-                L3 = nb ? NO_PAIR : L3;
-                N0 = nb ? N1 : N0;
-                N1 = nb ? N2 : N1;
-                N2 = nb ? N3 : N2;
-                N3 = nb ? 0u : N3;
+                Q0 = nb ? Q1 : Q0;
+                Q1 = nb ? Q2 : Q1;
+                Q2 = nb ? Q3 : Q2;
+                Q3 = nb ? 0xFFFFu : Q3;
                 w = nb ? 0u : w;
+                const uint32_t lpos = lq & 0xFFFFu, cnt = lq >> 16;
                 const bool st = g && w < cnt;
                 const uint32_t l = ((r.vz & 7) << 6) | ((r.vy & 7) << 3) | (r.vx & 7);
-                const bool stage = st && lpos != NO_PAIR && lpos + w < (uint32_t)PLC_STAGE;
+                const bool stage = st && lpos + w < (uint32_t)PLC_STAGE;
                 if (stage) {
                     st_s[lpos + w] = s;
                     st_l[lpos + w] = (uint16_t)l;
