@@ -236,9 +236,11 @@ __global__ __launch_bounds__(CNT_THREADS) void k_count(const float* __restrict__
         uint4 e = make_uint4(NO_PAIR, 0u, run_off, n);
         if (hx >= 0) {
             const uint32_t h = (uint32_t)hx;
-            T.touched[h] = 1u;
             e.x = h;
             e.y = atomicAdd(&T.cell[(size_t)h * T.cell_stride + t], n);
+            // the brick's first run of this scan marks it (one store per (brick, scan), not one
+            // per (workgroup, brick): partial-line stores from every XCD cost HBM writes)
+            if (e.y == 0u) T.touched[h] = 1u;
         }
         run_off += n;
         bt[slot] = e;
