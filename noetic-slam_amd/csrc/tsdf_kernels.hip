@@ -226,21 +226,44 @@ __global__ __launch_bounds__(CNT_THREADS) void k_count(const float* __restrict__
         run_off = incl - run_sum;
         for (int w = 0; w < wid; w++) run_off += s_wsum[w];
     }
-#pragma unroll 1
+    // The thread's SPT slots go to the global table in three batched stages, so their round trips
+    // overlap instead of running one slot after another: (1) first-probe loads of all keys,
+    // (2) resolve (a hit needs nothing more; an empty or taken first slot takes the probing path),
+    // (3) the cell atomics of all found bricks.
+    uint64_t key[SPT], h0[SPT], k0[SPT];
+#pragma unroll
     for (int j = 0; j < SPT; j++) {
         const int slot = threadIdx.x * SPT + j;
-        const uint64_t key = s_key[slot];
-        if (key == EMPTY_KEY) continue;
+        key[j] = s_key[slot];
+        h0[j] = mix64(key[j]) & T.mask;
+        k0[j] = key[j] != EMPTY_KEY ? T.keys[h0[j]] : EMPTY_KEY;
+    }
+    int64_t hx[SPT];
+#pragma unroll
+    for (int j = 0; j < SPT; j++) {
+        hx[j] = -1;
+        if (key[j] != EMPTY_KEY)
+            hx[j] = k0[j] == key[j] ? (int64_t)h0[j] : table_insert(T, key[j], &G->overflow);
+    }
+    uint32_t old[SPT];
+#pragma unroll
+    for (int j = 0; j < SPT; j++) {
+        const int slot = threadIdx.x * SPT + j;
+        old[j] = hx[j] >= 0 ? atomicAdd(&T.cell[(size_t)hx[j] * T.cell_stride + t], s_cnt[slot])
+                            : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < SPT; j++) {
+        const int slot = threadIdx.x * SPT + j;
+        if (key[j] == EMPTY_KEY) continue;
         const uint32_t n = s_cnt[slot];
-        const int64_t hx = table_insert(T, key, &G->overflow);
         uint4 e = make_uint4(NO_PAIR, 0u, run_off, n);
-        if (hx >= 0) {
-            const uint32_t h = (uint32_t)hx;
-            e.x = h;
-            e.y = atomicAdd(&T.cell[(size_t)h * T.cell_stride + t], n);
+        if (hx[j] >= 0) {
+            e.x = (uint32_t)hx[j];
+            e.y = old[j];
             // the brick's first run of this scan marks it (one store per (brick, scan), not one
             // per (workgroup, brick): partial-line stores from every XCD cost HBM writes)
-            if (e.y == 0u) T.touched[h] = 1u;
+            if (old[j] == 0u) T.touched[e.x] = 1u;
         }
         run_off += n;
         bt[slot] = e;
