@@ -362,7 +362,8 @@ void tsdf_destroy(tsdf_ctx* c) {
                    c->cell2[0],      c->cell2[1],        c->stage2[0],     c->stage2[1],
                    c->W2[0].pair,    c->W2[0].blk,       c->W2[0].blk_occ, c->W2[0].fb,
                    c->W2[0].smp,     c->W2[0].active,    c->W2[1].pair,    c->W2[1].blk,
-                   c->W2[1].blk_occ, c->W2[1].fb,        c->W2[1].smp,     c->W2[1].active};
+                   c->W2[1].blk_occ, c->W2[1].fb,        c->W2[1].smp,     c->W2[1].active,
+                   c->W2[0].cagg,    c->W2[1].cagg};
     for (void* d : dev)
         if (d) (void)hipFree(d);
     for (int i = 0; i < 2; i++) {
@@ -453,6 +454,7 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
         HIPCHK(c, hipMalloc(&W.fb, (size_t)W.max_fb * sizeof(uint4)));
         HIPCHK(c, hipMalloc(&W.smp, (size_t)W.max_smp * sizeof(uint2)));
         HIPCHK(c, hipMalloc(&W.active, (size_t)W.max_active * sizeof(uint4)));
+        HIPCHK(c, hipMalloc(&W.cagg, compact_chunks(c->cap) * 2 * sizeof(uint4)));
         HIPCHK(c, hipMalloc(&c->cell2[q], c->cap * c->T.cell_stride * sizeof(uint32_t)));
         HIPCHK(c, hipMemsetAsync(c->cell2[q], 0, c->cap * c->T.cell_stride * sizeof(uint32_t),
                                  c->stream));

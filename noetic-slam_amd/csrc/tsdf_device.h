@@ -101,6 +101,7 @@ struct Work {
     uint4* fb;       // fallback pairs: (tidx, scan, rank, 0)
     uint2* smp;  // x = truncated sdf (f32 bits), y = scan << 9 | local voxel
     uint4* active;  // (h, slot, toff, cnt) per active brick (k_compact)
+    uint4* cagg;    // k_compact: per table chunk (touched bricks, samples, new bricks), then bases
     uint32_t maxp;        // pair slots per ray
     uint32_t max_active;  // capacity of `active`
     uint32_t max_fb;      // capacity of `fb`
@@ -143,6 +144,9 @@ struct KernelTimer {
 
 hipError_t launch_count(const float* d_xyz, const BatchDesc& D, const RayConst& R, const Table& T,
                         const Work& Wk, Globals* G, int parity, hipStream_t st);
+// table chunks of k_compact (Work::cagg holds two uint4 per chunk)
+constexpr uint32_t CMP_CHUNK = 1024;
+inline uint64_t compact_chunks(uint64_t cap) { return (cap + CMP_CHUNK - 1) / CMP_CHUNK; }
 hipError_t launch_compact(const BatchDesc& D, const Table& T, const Work& Wk, Globals* G,
                           int parity, hipStream_t st);
 hipError_t launch_place(const float* d_xyz, const BatchDesc& D, const RayConst& R, const Table& T,

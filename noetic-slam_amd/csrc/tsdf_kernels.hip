@@ -296,9 +296,15 @@ __global__ __launch_bounds__(CNT_THREADS) void k_count(const float* __restrict__
 // ------------------------------------------------------------------------------------------------
 // k_compact: per active brick — record segment, new pool slot, per-scan cell prefix
 
-constexpr int CMP_THREADS = 1024;
+constexpr int CMP_THREADS = 256;
+constexpr int CMP_PER = CMP_CHUNK / CMP_THREADS;  // table entries per thread
+constexpr int CMP_GROUP = 16;  // lanes per touched brick: one uint4 of its cell row each (<= 64 scans)
+constexpr int CMP_SCAN_THREADS = 1024;
+static_assert(MAX_BATCH <= 4 * CMP_GROUP, "a cell row is at most CMP_GROUP uint4");
 
+template <int NT>
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t* s_w, uint32_t* total) {
+    constexpr int NW = NT / 64;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     uint32_t v = x;
 #pragma unroll
@@ -308,72 +314,156 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t* s_w, u
     }
     if (lane == 63) s_w[wid] = v;
     __syncthreads();
-    if (threadIdx.x < 16) {
-        uint32_t u = s_w[threadIdx.x];
+    uint32_t off = 0, tot = 0;
 #pragma unroll
-        for (int d = 1; d < 16; d <<= 1) {
-            const uint32_t y = __shfl_up(u, d, 16);
-            if ((int)threadIdx.x >= d) u += y;
-        }
-        s_w[threadIdx.x] = u;
+    for (int k = 0; k < NW; k++) {
+        const uint32_t r = s_w[k];
+        off += k < wid ? r : 0u;
+        tot += r;
     }
-    __syncthreads();
-    *total = s_w[15];
-    const uint32_t r = v - x + (wid ? s_w[wid - 1] : 0u);
-    __syncthreads();
-    return r;
+    *total = tot;
+    __syncthreads();  // s_w reusable
+    return v - x + off;
 }
 
-// Sweeps the `touched` words of the whole table (coalesced, cap * 4 B) — cheaper than any
-// per-brick first-touch atomic in k_count.  For each touched brick: its sample segment, its
-// per-scan cells rewritten as absolute positions in it (segment start + exclusive prefix), a pool
-// slot if it is new, and an active record; three atomics per CMP_THREADS table entries.
-__global__ __launch_bounds__(CMP_THREADS) void k_compact(uint32_t n_scans, Table T, Work Wk,
-                                                         Globals* G, int parity) {
-    __shared__ uint32_t s_w[16];
-    __shared__ uint32_t base_a, base_c, base_n;
-    Counters* C = &G->ctr[parity];
-    const uint32_t cap = (uint32_t)(T.mask + 1);
-    for (uint32_t chunk = blockIdx.x * CMP_THREADS; chunk < cap;
-         chunk += gridDim.x * CMP_THREADS) {
-        const uint32_t h = chunk + threadIdx.x;
-        const bool hit = T.touched[h] != 0u;
-        uint32_t n = 0, isnew = 0;
-        uint4* cp = reinterpret_cast<uint4*>(T.cell + (size_t)h * T.cell_stride);
-        if (hit) {
-            T.touched[h] = 0u;
-            isnew = T.slots[h] == UNASSIGNED ? 1u : 0u;
-            for (uint32_t q = 0; q < (n_scans + 3) / 4; q++) {  // cell_stride is a multiple of 4
-                const uint4 v = cp[q];
-                n += v.x + v.y + v.z + v.w;
-            }
+// k_compact gives every brick touched by the batch its sample segment (a global prefix over the
+// bricks), a pool slot if new and an active record, and rewrites its per-scan cells as absolute
+// sample positions.  The global prefix is taken over table chunks in three launches, without any
+// atomic (a counter shared by thousands of workgroups serializes at ~11 ns per add):
+//   k_compact_sum    per chunk of CMP_CHUNK table entries: touched bricks, their samples (16 lanes
+//                    per brick read its cell row, one uint4 each) and new bricks -> cagg[chunk];
+//   k_compact_scan   one workgroup: exclusive prefix of the chunk totals -> cagg[nch + chunk], the
+//                    batch's counters and the pool count;
+//   k_compact_write  per chunk again: records, slots and the rewritten cell rows.
+// The chunk's touched bricks, listed in LDS in table order (<= CMP_CHUNK of them).
+__device__ __forceinline__ uint32_t compact_list(const Table& T, uint32_t chunk, uint32_t* s_h,
+                                                 uint32_t* s_w, bool clear) {
+    uint32_t hit[CMP_PER], cnt = 0;
+#pragma unroll
+    for (int j = 0; j < CMP_PER; j++) {  // thread-consecutive entries keep the list in table order
+        const uint32_t h = chunk + threadIdx.x * CMP_PER + j;
+        hit[j] = h <= T.mask && T.touched[h] != 0u ? 1u : 0u;
+        cnt += hit[j];
+    }
+    uint32_t nh;
+    uint32_t e = block_excl_scan<CMP_THREADS>(cnt, s_w, &nh);
+#pragma unroll
+    for (int j = 0; j < CMP_PER; j++) {
+        if (hit[j]) {
+            const uint32_t h = chunk + threadIdx.x * CMP_PER + j;
+            s_h[e++] = h;
+            if (clear) T.touched[h] = 0u;
         }
-        uint32_t tot_a, tot_c, tot_n;
-        const uint32_t ea = block_excl_scan(hit ? 1u : 0u, s_w, &tot_a);
-        const uint32_t ec = block_excl_scan(n, s_w, &tot_c);
-        const uint32_t en = block_excl_scan(isnew, s_w, &tot_n);
+    }
+    __syncthreads();
+    return nh;
+}
+
+__global__ __launch_bounds__(CMP_THREADS) void k_compact_sum(uint32_t n_scans, Table T, Work Wk) {
+    __shared__ uint32_t s_w[CMP_THREADS / 64];
+    __shared__ uint32_t s_h[CMP_CHUNK];
+    __shared__ uint32_t s_acc[2];  // samples, new bricks
+    if (threadIdx.x == 0) {
+        s_acc[0] = 0u;
+        s_acc[1] = 0u;
+    }
+    const uint32_t nh = compact_list(T, blockIdx.x * CMP_CHUNK, s_h, s_w, false);
+    const uint32_t nq = (n_scans + 3) / 4;  // cell_stride is a multiple of 4
+    const uint32_t grp = threadIdx.x / CMP_GROUP, li = threadIdx.x % CMP_GROUP;
+    uint32_t samples = 0, nnew = 0;
+    for (uint32_t k = grp; k < nh; k += CMP_THREADS / CMP_GROUP) {
+        const uint32_t h = s_h[k];
+        const uint4* cp = reinterpret_cast<const uint4*>(T.cell + (size_t)h * T.cell_stride);
+        const uint4 v = li < nq ? cp[li] : make_uint4(0u, 0u, 0u, 0u);
+        samples += v.x + v.y + v.z + v.w;
+        if (li == 0 && T.slots[h] == UNASSIGNED) nnew++;
+    }
+    samples = wave_sum<uint32_t>(samples);
+    nnew = wave_sum<uint32_t>(nnew);
+    if ((threadIdx.x & 63) == 0) {
+        if (samples) atomicAdd(&s_acc[0], samples);
+        if (nnew) atomicAdd(&s_acc[1], nnew);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) Wk.cagg[blockIdx.x] = make_uint4(nh, s_acc[0], s_acc[1], 0u);
+}
+
+__global__ __launch_bounds__(CMP_SCAN_THREADS) void k_compact_scan(uint32_t nch, Work Wk,
+                                                                   Globals* G, int parity) {
+    __shared__ uint32_t s_w[3][CMP_SCAN_THREADS / 64];
+    __shared__ uint32_t s_carry[3];
+    Counters* C = &G->ctr[parity];
+    if (threadIdx.x == 0) {
+        s_carry[0] = 0u;
+        s_carry[1] = 0u;
+        s_carry[2] = G->pool_count;
+    }
+    __syncthreads();
+    for (uint32_t b0 = 0; b0 < nch; b0 += CMP_SCAN_THREADS) {
+        const uint32_t i = b0 + threadIdx.x;
+        const uint4 a = i < nch ? Wk.cagg[i] : make_uint4(0u, 0u, 0u, 0u);
+        uint32_t ta, tc, tn;
+        const uint32_t ea = block_excl_scan<CMP_SCAN_THREADS>(a.x, s_w[0], &ta);
+        const uint32_t ec = block_excl_scan<CMP_SCAN_THREADS>(a.y, s_w[1], &tc);
+        const uint32_t en = block_excl_scan<CMP_SCAN_THREADS>(a.z, s_w[2], &tn);
+        if (i < nch) Wk.cagg[nch + i] = make_uint4(s_carry[0] + ea, s_carry[1] + ec, s_carry[2] + en, 0u);
+        __syncthreads();
         if (threadIdx.x == 0) {
-            base_a = tot_a ? atomicAdd(&C->n_active, tot_a) : 0u;
-            base_c = tot_c ? atomicAdd(&C->cursor, tot_c) : 0u;
-            base_n = tot_n ? atomicAdd(&G->pool_count, tot_n) : 0u;
-            if ((unsigned long long)base_c + tot_c > Wk.max_smp) atomicOr(&G->overflow, OVF_PAIRS);
+            s_carry[0] += ta;
+            s_carry[1] += tc;
+            s_carry[2] += tn;
         }
         __syncthreads();
-        if (hit) {
-            // the per-scan cells become absolute sample positions: segment start + exclusive
-            // prefix (k_place then finds a run's position with one gather)
-            uint32_t p = base_c + ec;
-            for (uint32_t q = 0; q < (n_scans + 3) / 4; q++) {
-                uint4 v = cp[q];
-                const uint32_t x0 = v.x, x1 = v.y, x2 = v.z, x3 = v.w;
-                v.x = p; p += x0;
-                v.y = p; p += x1;
-                v.z = p; p += x2;
-                v.w = p; p += x3;
-                cp[q] = v;
-            }
-            uint32_t slot = isnew ? base_n + en : T.slots[h];
-            if (isnew) {
+    }
+    if (threadIdx.x == 0) {
+        C->n_active = s_carry[0];
+        C->cursor = s_carry[1];
+        G->pool_count = s_carry[2];
+        if (s_carry[1] > Wk.max_smp) atomicOr(&G->overflow, OVF_PAIRS);
+        if (s_carry[0] > Wk.max_active) atomicOr(&G->overflow, OVF_ACTIVE);
+    }
+}
+
+__global__ __launch_bounds__(CMP_THREADS) void k_compact_write(uint32_t n_scans, uint32_t nch,
+                                                               Table T, Work Wk, Globals* G) {
+    __shared__ uint32_t s_w[CMP_THREADS / 64];
+    __shared__ uint32_t s_h[CMP_CHUNK];
+    __shared__ uint32_t s_n[CMP_CHUNK];  // the bricks' samples, then their segment starts
+    const uint32_t chunk = blockIdx.x * CMP_CHUNK;
+    const uint32_t nh = compact_list(T, chunk, s_h, s_w, true);
+    if (nh == 0) return;  // uniform
+    const uint32_t nq = (n_scans + 3) / 4;
+    const uint32_t grp = threadIdx.x / CMP_GROUP, li = threadIdx.x % CMP_GROUP;
+    for (uint32_t k = grp; k < nh; k += CMP_THREADS / CMP_GROUP) {
+        const uint4* cp = reinterpret_cast<const uint4*>(T.cell + (size_t)s_h[k] * T.cell_stride);
+        const uint4 v = li < nq ? cp[li] : make_uint4(0u, 0u, 0u, 0u);
+        uint32_t sum = v.x + v.y + v.z + v.w;
+#pragma unroll
+        for (int d = CMP_GROUP / 2; d >= 1; d >>= 1) sum += __shfl_xor(sum, d, CMP_GROUP);
+        if (li == 0) s_n[k] = sum;
+    }
+    __syncthreads();
+    const uint4 base = Wk.cagg[nch + blockIdx.x];  // (active, sample, pool) bases of the chunk
+    // per brick, in table order: CMP_PER consecutive bricks per thread
+    uint32_t n[CMP_PER], isnew[CMP_PER], sn = 0, snew = 0;
+#pragma unroll
+    for (int j = 0; j < CMP_PER; j++) {
+        const uint32_t k = threadIdx.x * CMP_PER + j;
+        n[j] = k < nh ? s_n[k] : 0u;
+        isnew[j] = k < nh && T.slots[s_h[k]] == UNASSIGNED ? 1u : 0u;
+        sn += n[j];
+        snew += isnew[j];
+    }
+    uint32_t tc, tn;
+    uint32_t ec = block_excl_scan<CMP_THREADS>(sn, s_w, &tc);
+    uint32_t en = block_excl_scan<CMP_THREADS>(snew, s_w, &tn);
+#pragma unroll
+    for (int j = 0; j < CMP_PER; j++) {
+        const uint32_t k = threadIdx.x * CMP_PER + j;
+        if (k < nh) {
+            const uint32_t h = s_h[k];
+            uint32_t slot = isnew[j] ? base.z + en : T.slots[h];
+            if (isnew[j]) {
                 if (slot < T.max_bricks) {
                     T.brick_keys[slot] = T.keys[h];
                 } else {
@@ -383,10 +473,33 @@ __global__ __launch_bounds__(CMP_THREADS) void k_compact(uint32_t n_scans, Table
                 T.slots[h] = slot;
             }
             // k_integrate's whole per-brick header in one record
-            if (base_a + ea < Wk.max_active) Wk.active[base_a + ea] = make_uint4(h, slot, base_c + ec, n);
-            else atomicOr(&G->overflow, OVF_ACTIVE);
+            if (base.x + k < Wk.max_active)
+                Wk.active[base.x + k] = make_uint4(h, slot, base.y + ec, n[j]);
+            s_n[k] = base.y + ec;
         }
-        __syncthreads();
+        ec += n[j];
+        en += isnew[j];
+    }
+    __syncthreads();
+    // the per-scan cells become absolute sample positions: segment start + exclusive prefix
+    // (k_place then finds a run's position with one gather)
+    for (uint32_t k = grp; k < nh; k += CMP_THREADS / CMP_GROUP) {
+        uint4* cp = reinterpret_cast<uint4*>(T.cell + (size_t)s_h[k] * T.cell_stride);
+        uint4 v = li < nq ? cp[li] : make_uint4(0u, 0u, 0u, 0u);
+        const uint32_t s4 = v.x + v.y + v.z + v.w;
+        uint32_t incl = s4;
+#pragma unroll
+        for (int d = 1; d < CMP_GROUP; d <<= 1) {
+            const uint32_t y = __shfl_up(incl, d, CMP_GROUP);
+            if ((int)li >= d) incl += y;
+        }
+        uint32_t p = s_n[k] + incl - s4;
+        const uint32_t x0 = v.x, x1 = v.y, x2 = v.z;
+        v.x = p; p += x0;
+        v.y = p; p += x1;
+        v.z = p; p += x2;
+        v.w = p;
+        if (li < nq) cp[li] = v;
     }
 }
 
@@ -721,8 +834,10 @@ hipError_t launch_count(const float* d_xyz, const BatchDesc& D, const RayConst& 
 
 hipError_t launch_compact(const BatchDesc& D, const Table& T, const Work& Wk, Globals* G,
                           int parity, hipStream_t st) {
-    k_compact<<<grid_for(T.mask + 1, CMP_THREADS, 256), CMP_THREADS, 0, st>>>(D.n_scans, T, Wk,
-                                                                                G, parity);
+    const uint32_t nch = (uint32_t)compact_chunks(T.mask + 1);
+    k_compact_sum<<<nch, CMP_THREADS, 0, st>>>(D.n_scans, T, Wk);
+    k_compact_scan<<<1, CMP_SCAN_THREADS, 0, st>>>(nch, Wk, G, parity);
+    k_compact_write<<<nch, CMP_THREADS, 0, st>>>(D.n_scans, nch, T, Wk, G);
     return hipGetLastError();
 }
 
