@@ -186,6 +186,19 @@ def test_c4_dense_2048_2cm():
     assert_bitwise(g, o)
 
 
+def test_long_runs_unpacked_cells(scan0):
+    """(brick, scan) runs longer than the packed-cell limit (count carried in the int64 sum:
+    n tau 2^32 < 2^43) take the two-atomic path: 20000 returns on one point per scan, mixed with
+    ordinary scans in the same windows, and a 2 m truncation where the limit is ~1000."""
+    pts, org = scan0
+    hot = np.tile(np.array([[4.0, 1.0, 0.3]], np.float32), (20000, 1))
+    for tau in (TAU, 2.0):
+        scans = [(decimate(pts, 8), org), (np.concatenate([decimate(pts, 16), hot]), org),
+                 (hot[:3000] + np.float32(0.01), org)]
+        g, o = run_both(scans, sdf_trunc=tau)
+        assert assert_bitwise(g, o) > 0
+
+
 def test_c3_10cm(scan0):
     """C3 voxel size: 10 cm, 30 cm truncation."""
     g, o = run_both([(decimate(scan0[0], 4), scan0[1])], voxel_size=0.10, sdf_trunc=0.30)
