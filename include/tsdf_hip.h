@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define TSDF_ABI_VERSION 2
+#define TSDF_ABI_VERSION 3
 #define TSDF_MAX_BATCH 64 /* scans per GPU batch (see tsdf_params.max_batch) */
 #define TSDF_BRICK_SIDE 8 /* voxels per brick edge: a brick is 8^3 = 512 voxels */
 
@@ -50,6 +50,16 @@ extern "C" {
 
 /* weighting functions (VDBFusion's weighting_function argument; default constant 1) */
 #define TSDF_WEIGHT_CONSTANT 0
+
+/* Backend semantics (tsdf_params.semantics).  The node's MAP_BACKEND_IDX chooses between CPU
+ * backends with different fusion rules (reference README.md:44-50); this backend restates two:
+ *   TSDF_SEM_VDBFUSION  backend idx 3, VDBVolume::Integrate
+ *   TSDF_SEM_VOXBLOX    backend idx 2, voxblox SimpleTsdfIntegrator with use_const_weight
+ *                       (DESIGN.md §2b): projective sdf, behind-surface weight
+ *                       dropoff, clearing rays, fused distance clamped to +-tau, weight capped at
+ *                       max_weight, background (distance 0, weight 0). */
+#define TSDF_SEM_VDBFUSION 0
+#define TSDF_SEM_VOXBLOX 1
 
 typedef struct tsdf_params {
     double voxel_size;     /* metres (VDBVolume voxel_size) */
@@ -68,6 +78,13 @@ typedef struct tsdf_params {
                               place of batch b+1 run beside batch b's place / integrate; same field,
                               bit for bit); 0 (default): batches run one after another, so per-kernel
                               timings (tsdf_stats.kernel_ms) are not shared with another batch */
+    /* ABI v3: backend semantics */
+    int32_t semantics;          /* TSDF_SEM_VDBFUSION (default) or TSDF_SEM_VOXBLOX */
+    int32_t allow_clear;        /* Voxblox allow_clear: a ray longer than max_range becomes a
+                                   clearing ray of length min(max(d - tau, 0), max_range) (default 1) */
+    int32_t use_weight_dropoff; /* Voxblox use_weight_dropoff: w *= (tau + sdf) / (tau - voxel_size)
+                                   for sdf < -voxel_size, floored at 0 (default 1) */
+    float max_weight;           /* Voxblox max_weight: the fused weight is capped here (default 1e4) */
 } tsdf_params;
 
 /* Batching.  Scans are integrated in call order and the field after any sequence of calls is

@@ -338,6 +338,10 @@ void tsdf_default_params(tsdf_params* p) {
     p->device_id = 0;
     p->brick_side = TSDF_BRICK_SIDE;
     p->max_batch = 32;
+    p->semantics = TSDF_SEM_VDBFUSION;
+    p->allow_clear = 1;  // voxblox TsdfIntegratorBase::Config defaults
+    p->use_weight_dropoff = 1;
+    p->max_weight = 10000.0f;
 }
 
 int tsdf_abi_version(void) { return TSDF_ABI_VERSION; }
@@ -405,6 +409,12 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
     c->R.carving = p->space_carving ? 1 : 0;
     c->R.tau2_lo = (float)(((double)c->R.tau * (1.0 - 0x1p-20)) * ((double)c->R.tau * (1.0 - 0x1p-20)));
     c->R.tau2_hi = (float)(((double)c->R.tau * (1.0 + 0x1p-20)) * ((double)c->R.tau * (1.0 + 0x1p-20)));
+    c->R.sem = p->semantics;
+    c->R.allow_clear = p->allow_clear ? 1 : 0;
+    c->R.dropoff = p->use_weight_dropoff ? 1 : 0;
+    c->R.max_weight = p->max_weight;
+    c->R.bg = p->semantics == TSDF_SEM_VOXBLOX ? 0.0f : c->R.tau;
+    c->R.tau_m_vs = c->R.tau - c->R.vs;
 
     // Points one batch may hold: max_batch full scans, unless the per-ray worst cases (pair slots,
     // sample slots — large with space carving) exceed the u32 index space or the sample budget;
@@ -467,10 +477,10 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
                                 hipHostMallocDefault));
         HIPCHK(c, hipEventCreateWithFlags(&c->stage_done[i], hipEventDisableTiming));
     }
-    // VDBFusion background: tsdf = sdf_trunc, weight = 0
+    // background: (sdf_trunc, 0) VDBFusion, (0, 0) Voxblox TsdfVoxel
     HIPCHK(c, launch_fill_u64(c->T.keys, EMPTY_KEY, c->cap, c->stream));
     HIPCHK(c, launch_fill_u32(c->T.slots, UNASSIGNED, c->cap, c->stream));
-    HIPCHK(c, launch_fill(c->Pl.sdf, (float)p->sdf_trunc, p->max_bricks * BRICK_VOX, c->stream));
+    HIPCHK(c, launch_fill(c->Pl.sdf, c->R.bg, p->max_bricks * BRICK_VOX, c->stream));
     HIPCHK(c, hipMemsetAsync(c->Pl.weight, 0, p->max_bricks * BRICK_VOX * sizeof(float),
                              c->stream));
     HIPCHK(c, hipMemsetAsync(c->G, 0, sizeof(Globals), c->stream));
@@ -485,7 +495,9 @@ int tsdf_create(const tsdf_params* p, tsdf_ctx** out) {
     if (!(p->voxel_size > 0) || !(p->sdf_trunc > 0) || p->brick_side != TSDF_BRICK_SIDE ||
         p->weight_mode != TSDF_WEIGHT_CONSTANT || p->max_bricks == 0 ||
         p->max_bricks >= 0xFFFFFFF0ull || p->max_points == 0 || !(p->min_range >= 0) ||
-        !(p->max_range > p->min_range) || p->max_batch == 0 || p->max_batch > TSDF_MAX_BATCH)
+        !(p->max_range > p->min_range) || p->max_batch == 0 || p->max_batch > TSDF_MAX_BATCH ||
+        (p->semantics != TSDF_SEM_VDBFUSION && p->semantics != TSDF_SEM_VOXBLOX) ||
+        (p->semantics == TSDF_SEM_VOXBLOX && !(p->max_weight > 0.0f)))
         return TSDF_EINVAL;
     if (p->space_carving && !std::isfinite(p->max_range)) return TSDF_EINVAL;
     tsdf_ctx* c = new (std::nothrow) tsdf_ctx();
@@ -647,7 +659,7 @@ int tsdf_query_dense(tsdf_ctx* c, const int32_t lo[3], const int32_t hi[3], floa
     float *ds = nullptr, *dw = nullptr;
     HIPCHK(c, hipMalloc(&ds, total * sizeof(float)));
     hipError_t e = hipMalloc(&dw, total * sizeof(float));
-    if (e == hipSuccess) e = launch_query_dense(c->T, c->Pl, lo, dims, (float)c->p.sdf_trunc, ds,
+    if (e == hipSuccess) e = launch_query_dense(c->T, c->Pl, lo, dims, c->R.bg, ds,
                                                 dw, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e == hipSuccess && sdf) e = hipMemcpy(sdf, ds, total * 4, hipMemcpyDeviceToHost);

@@ -63,6 +63,11 @@ constexpr uint32_t OVF_TABLE = 1u, OVF_POOL = 2u, OVF_PAIRS = 4u, OVF_ACTIVE = 8
 struct RayConst {
     float vs, inv_vs, tau, min_range, max_range;
     int carving;
+    // backend semantics (TSDF_SEM_*) and the Voxblox mode's constants
+    int sem, allow_clear, dropoff;
+    float max_weight;
+    float bg;        // background distance of unobserved voxels: tau (VDBFusion) or 0 (Voxblox)
+    float tau_m_vs;  // tau - vs (Voxblox dropoff denominator)
     // squared-distance bounds bracketing tau by 2^-20 relative: d2 < tau2_lo implies
     // sqrt_rn(d2) < tau, d2 > tau2_hi implies sqrt_rn(d2) > tau (voxel_gate skips the sqrt)
     float tau2_lo, tau2_hi;

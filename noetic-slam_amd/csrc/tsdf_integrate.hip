@@ -19,6 +19,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "tsdf_device.h"
 #include "tsdf_ray.h"
 
@@ -66,10 +68,17 @@ constexpr uint32_t INT_MAX_WIN = TSDF_INT_WIN;       // scans per window (mask b
     } while (0)
 #endif
 
+// SEM = TSDF_SEM_*.  VDBFusion (0): a cell holds (sum of trunc(s 2^32), sample count) and the fuse
+// is the running average.  Voxblox (1): a cell holds (sum of trunc(s w 2^32), sum of
+// trunc(w 2^32)), w the sample's dropoff weight recomputed from its stored distance, and the fuse
+// clamps the distance to +-tau and the weight to max_weight.
+template <int SEM>
 __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchDesc D, Table T, Work Wk, Pool Pl,
-                                                          Globals* G, int parity, float tau) {
-    __shared__ unsigned long long cA[INT_CAP];  // live cell: sum of trunc(s * 2^32)
-    __shared__ uint32_t cB[INT_CAP];            // live cell: sample count
+                                                          Globals* G, int parity, RayConst R) {
+    typedef typename std::conditional<SEM == 1, unsigned long long, uint32_t>::type CellB;
+    __shared__ unsigned long long cA[INT_CAP];  // live cell: sum of trunc(s w * 2^32)
+    __shared__ CellB cB[INT_CAP];               // live cell: sample count / sum of trunc(w 2^32)
+    const float tau = R.tau;
     __shared__ MaskT sMask[BRICK_VOX];          // voxel: scans (bit t - t0) observed in the window
     __shared__ uint32_t sBase[BRICK_VOX];       // voxel: first live cell
     __shared__ float sS[BRICK_VOX], sW[BRICK_VOX];
@@ -114,8 +123,8 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchDesc D, Table T,
         B.cell = T.cell[(size_t)r.x * T.cell_stride + min((uint32_t)tid, T.cell_stride - 1u)];
         const float* Sg = Pl.sdf + (size_t)(has ? r.y : 0) * BRICK_VOX;
         const float* Wg = Pl.weight + (size_t)(has ? r.y : 0) * BRICK_VOX;
-        B.s0 = has ? Sg[tid] : tau;
-        B.s1 = has ? Sg[tid + 256] : tau;
+        B.s0 = has ? Sg[tid] : R.bg;
+        B.s1 = has ? Sg[tid + 256] : R.bg;
         B.w0 = has ? Wg[tid] : 0.0f;
         B.w1 = has ? Wg[tid + 256] : 0.0f;
     };
@@ -228,7 +237,7 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchDesc D, Table T,
                 // the window's cells start at zero (the previous window's P4 is past a barrier)
                 for (uint32_t j = tid; j < (tot & 0xFFFFu); j += INT_THREADS) {
                     cA[j] = 0ull;
-                    cB[j] = 0u;
+                    cB[j] = 0;
                 }
             }
             __syncthreads();
@@ -244,13 +253,22 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchDesc D, Table T,
                     if (w < nw) {
                         const uint32_t l = c[j].y & 511u;
                         const uint32_t cell = sBase[l] + MASK_POPC(sMask[l] & (((MaskT)1 << w) - 1));
-                        const long long fx = (long long)(__uint_as_float(c[j].x) * 4294967296.0f);
+                        const float sv = __uint_as_float(c[j].x);
+                        if constexpr (SEM == 1) {
+                            const float wv = vb_weight(R, sv);
+                            const long long fa = (long long)((sv * wv) * 4294967296.0f);
+                            const long long fb = (long long)(wv * 4294967296.0f);
+                            atomicAdd(&cA[cell], (unsigned long long)fa);
+                            atomicAdd(&cB[cell], (unsigned long long)fb);
+                        } else {
+                            const long long fx = (long long)(sv * 4294967296.0f);
 #ifdef TSDF_ABLATE_INT_NOP3
-                        if (fx == 12345)
+                            if (fx == 12345)
 #endif
-                        {
-                            atomicAdd(&cA[cell], (unsigned long long)fx);
-                            atomicAdd(&cB[cell], 1u);
+                            {
+                                atomicAdd(&cA[cell], (unsigned long long)fx);
+                                atomicAdd(&cB[cell], 1u);
+                            }
                         }
                     }
                 }
@@ -265,8 +283,11 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchDesc D, Table T,
                 const uint32_t ncell = s_ncell;
                 for (uint32_t j = tid; j < ncell; j += INT_THREADS) {
                     const long long av = (long long)cA[j];
-                    const uint32_t bv = cB[j];
-                    cF[j] = make_float2((float)((double)av * (1.0 / 4294967296.0)), (float)bv);
+                    const float af = (float)((double)av * (1.0 / 4294967296.0));
+                    if constexpr (SEM == 1)
+                        cF[j] = make_float2(af, (float)((double)(long long)cB[j] * (1.0 / 4294967296.0)));
+                    else
+                        cF[j] = make_float2(af, (float)cB[j]);
                 }
             }
             __syncthreads();
@@ -292,17 +313,39 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchDesc D, Table T,
                     // the second step of a pair is dropped past the chain's end
                     typedef const volatile __attribute__((address_space(3))) uint64_t lds_u64;
                     lds_u64* cV = (lds_u64*)(cA);
+                    // Voxblox updateTsdfVoxel on a cell (a, b) = (sum s w, sum w):
+                    // W' = W + b (no update below kFloatEpsilon), S' = (a + S W) / W' clamped to
+                    // +-tau, W = min(max_weight, W')
+                    auto vb_fuse = [&](float2 v, float& s_, float& w_) {
+                        const float nw = w_ + v.y;
+                        float ns = (v.x + s_ * w_) / nw;
+                        ns = ns > 0.0f ? (ns < tau ? ns : tau) : (-tau < ns ? ns : -tau);
+                        const bool ok = !(nw < 1e-6f);
+                        s_ = ok ? ns : s_;
+                        w_ = ok ? (nw < R.max_weight ? nw : R.max_weight) : w_;
+                    };
                     for (uint32_t k = 0; k < rem; k += 2) {
                         const uint64_t na = cV[min(cell + k + 2, INT_CAP - 1u)];
-                        float nwt = wt + va.y;
-                        s = (s * wt + va.x) / nwt;
-                        wt = nwt;
-                        const uint64_t nb = cV[min(cell + k + 3, INT_CAP - 1u)];
-                        nwt = wt + vb.y;
-                        const float s2 = (s * wt + vb.x) / nwt;
-                        const bool more = k + 1 < rem;
-                        s = more ? s2 : s;
-                        wt = more ? nwt : wt;
+                        uint64_t nb;
+                        if constexpr (SEM == 1) {
+                            vb_fuse(va, s, wt);
+                            nb = cV[min(cell + k + 3, INT_CAP - 1u)];
+                            float s2 = s, w2 = wt;
+                            vb_fuse(vb, s2, w2);
+                            const bool more = k + 1 < rem;
+                            s = more ? s2 : s;
+                            wt = more ? w2 : wt;
+                        } else {
+                            float nwt = wt + va.y;
+                            s = (s * wt + va.x) / nwt;
+                            wt = nwt;
+                            nb = cV[min(cell + k + 3, INT_CAP - 1u)];
+                            nwt = wt + vb.y;
+                            const float s2 = (s * wt + vb.x) / nwt;
+                            const bool more = k + 1 < rem;
+                            s = more ? s2 : s;
+                            wt = more ? nwt : wt;
+                        }
                         va = make_float2(__uint_as_float((uint32_t)na), __uint_as_float((uint32_t)(na >> 32)));
                         vb = make_float2(__uint_as_float((uint32_t)nb), __uint_as_float((uint32_t)(nb >> 32)));
                     }
@@ -356,13 +399,14 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchDesc D, Table T,
 // Grid = exactly the workgroups the device holds at once (CUs x resident workgroups per CU, from
 // the occupancy API: VGPRs or LDS, whichever binds): every workgroup of the grid-stride loop starts
 // at once, none waits for a second dispatch round.
+template <int SEM>
 static int integrate_grid() {
     static int grid = 0;
     if (grid == 0) {
         int dev = 0, cus = 0, per_cu = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_integrate, INT_THREADS, 0) !=
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_integrate<SEM>, INT_THREADS, 0) !=
                 hipSuccess ||
             cus <= 0 || per_cu <= 0) {
             cus = 256;
@@ -375,7 +419,10 @@ static int integrate_grid() {
 
 hipError_t launch_integrate(const BatchDesc& D, const RayConst& R, const Table& T, const Work& Wk,
                             const Pool& Pl, Globals* G, int parity, hipStream_t st) {
-    k_integrate<<<integrate_grid(), INT_THREADS, 0, st>>>(D, T, Wk, Pl, G, parity, R.tau);
+    if (R.sem == 1)
+        k_integrate<1><<<integrate_grid<1>(), INT_THREADS, 0, st>>>(D, T, Wk, Pl, G, parity, R);
+    else
+        k_integrate<0><<<integrate_grid<0>(), INT_THREADS, 0, st>>>(D, T, Wk, Pl, G, parity, R);
     return hipGetLastError();
 }
 

@@ -70,6 +70,7 @@ __device__ __forceinline__ int lds_insert(unsigned long long* s_key, uint64_t ke
 
 constexpr int CNT_THREADS = 256;
 
+template <int SEM>
 __global__ __launch_bounds__(CNT_THREADS) void k_count(const float* __restrict__ xyz, BatchDesc D,
                                                       RayConst R, Table T, Work Wk, Globals* G,
                                                       int parity) {
@@ -114,8 +115,8 @@ __global__ __launch_bounds__(CNT_THREADS) void k_count(const float* __restrict__
     for (uint32_t i = r0 + threadIdx.x; i < r1; i += CNT_THREADS) {
         uint32_t* pc = Wk.pair + (size_t)i * maxp;
         uint32_t k = 0;
-        RayState r;
-        const bool ok = ray_init(R, ox, oy, oz, xyz[3 * (size_t)i], xyz[3 * (size_t)i + 1],
+        typename Walk<SEM>::State r;
+        const bool ok = Walk<SEM>::init(R, ox, oy, oz, xyz[3 * (size_t)i], xyz[3 * (size_t)i + 1],
                                  xyz[3 * (size_t)i + 2], r);
         valid += ok ? 1u : 0u;
         // One pair per distinct brick; a line visits a brick in one contiguous run of DDA voxels,
@@ -129,7 +130,7 @@ __global__ __launch_bounds__(CNT_THREADS) void k_count(const float* __restrict__
                 uint64_t cur = EMPTY_KEY;
                 uint32_t ccount = 0;
                 for (int it = 0; it < MAX_DDA_STEPS; it++) {
-                    if (voxel_gate(R, ox, oy, oz, r)) {
+                    if (Walk<SEM>::gate(R, ox, oy, oz, r)) {
                         const uint64_t key = brick_key_of(r.vx, r.vy, r.vz);
                         if (key != cur) {
                             if (cur != EMPTY_KEY) {
@@ -144,7 +145,7 @@ __global__ __launch_bounds__(CNT_THREADS) void k_count(const float* __restrict__
                         }
                         ccount++;
                     }
-                    if (!ray_step(r)) break;
+                    if (!Walk<SEM>::step(r)) break;
                 }
                 if (cur != EMPTY_KEY) {
                     q0 = np == 0 ? cur : q0; n0 = np == 0 ? ccount : n0;
@@ -181,7 +182,7 @@ __global__ __launch_bounds__(CNT_THREADS) void k_count(const float* __restrict__
                     pc[k++] = pair_code(bkey, cnt_in);
                 };
                 for (int it = 0; it < MAX_DDA_STEPS; it++) {
-                    if (voxel_gate(R, ox, oy, oz, r)) {
+                    if (Walk<SEM>::gate(R, ox, oy, oz, r)) {
                         const uint64_t key = brick_key_of(r.vx, r.vy, r.vz);
                         if (key != cur) {
                             if (cur != EMPTY_KEY) emit(cur, ccount);
@@ -190,7 +191,7 @@ __global__ __launch_bounds__(CNT_THREADS) void k_count(const float* __restrict__
                         }
                         ccount++;
                     }
-                    if (!ray_step(r)) break;
+                    if (!Walk<SEM>::step(r)) break;
                 }
                 if (cur != EMPTY_KEY) emit(cur, ccount);
             }
@@ -515,6 +516,7 @@ __global__ __launch_bounds__(CMP_THREADS) void k_compact_write(uint32_t n_scans,
 constexpr int PLC_THREADS = RPB;      // one ray per lane
 constexpr int PLC_STAGE = 10112;      // staged samples per workgroup (6 B each; 2 workgroups per CU)
 
+template <int SEM>
 __global__ __launch_bounds__(PLC_THREADS) void k_place(const float* __restrict__ xyz, BatchDesc D,
                                                       RayConst R, Table T, Work Wk) {
     constexpr int PLC_WORDS = (PLC_STAGE + 31) / 32;
@@ -534,8 +536,8 @@ __global__ __launch_bounds__(PLC_THREADS) void k_place(const float* __restrict__
     const float ox = D.ox[t], oy = D.oy[t], oz = D.oz[t];
     const uint32_t maxp = Wk.maxp;
     const uint32_t i = r0 + threadIdx.x;
-    RayState r;
-    const bool ok = i < r1 && ray_init(R, ox, oy, oz, xyz[3 * (size_t)i], xyz[3 * (size_t)i + 1],
+    typename Walk<SEM>::State r;
+    const bool ok = i < r1 && Walk<SEM>::init(R, ox, oy, oz, xyz[3 * (size_t)i], xyz[3 * (size_t)i + 1],
                                        xyz[3 * (size_t)i + 2], r);
     const uint32_t* pc = Wk.pair + (size_t)i * maxp;
     uint4 code4 = make_uint4(NO_PAIR, NO_PAIR, NO_PAIR, NO_PAIR);
@@ -656,7 +658,7 @@ __global__ __launch_bounds__(PLC_THREADS) void k_place(const float* __restrict__
             uint32_t lq = 0xFFFFu;  // current pair's (staging position | count << 16)
             for (int it = 0; it < MAX_DDA_STEPS; it++) {
                 float s;
-                const bool g = voxel_sample_sel(R, ox, oy, oz, r, s);
+                const bool g = Walk<SEM>::sample_sel(R, ox, oy, oz, r, s);
                 const uint64_t key = brick_key_of(r.vx, r.vy, r.vz);
                 const bool nb = g && key != cur;  // the ray's next pair, in k_count's order
                 cur = nb ? key : cur;
@@ -684,12 +686,12 @@ __global__ __launch_bounds__(PLC_THREADS) void k_place(const float* __restrict__
                     Wk.smp[pos + w] = make_uint2(__float_as_uint(s), (t << 9) | l);
                 }
                 w += g ? 1u : 0u;
-                if (!ray_step(r)) break;
+                if (!Walk<SEM>::step(r)) break;
             }
         } else
         for (int it = 0; it < MAX_DDA_STEPS; it++) {
             float s;
-            if (voxel_sample(R, ox, oy, oz, r, s)) {
+            if (Walk<SEM>::sample(R, ox, oy, oz, r, s)) {
                 const uint64_t key = brick_key_of(r.vx, r.vy, r.vz);
                 if (key != cur) {  // the ray's next pair, in k_count's order
                     cur = key;
@@ -708,7 +710,7 @@ __global__ __launch_bounds__(PLC_THREADS) void k_place(const float* __restrict__
                 }
                 w++;
             }
-            if (!ray_step(r)) break;
+            if (!Walk<SEM>::step(r)) break;
         }
     }
     __syncthreads();
@@ -828,7 +830,8 @@ static int grid_for(uint64_t items, int per_block, int cap) {
 // (tsdf_capi.cpp) interleaves the cross-batch waits between them.
 hipError_t launch_count(const float* d_xyz, const BatchDesc& D, const RayConst& R, const Table& T,
                         const Work& Wk, Globals* G, int parity, hipStream_t st) {
-    k_count<<<D.n_blocks, CNT_THREADS, 0, st>>>(d_xyz, D, R, T, Wk, G, parity);
+    if (R.sem == 1) k_count<1><<<D.n_blocks, CNT_THREADS, 0, st>>>(d_xyz, D, R, T, Wk, G, parity);
+    else k_count<0><<<D.n_blocks, CNT_THREADS, 0, st>>>(d_xyz, D, R, T, Wk, G, parity);
     return hipGetLastError();
 }
 
@@ -843,7 +846,8 @@ hipError_t launch_compact(const BatchDesc& D, const Table& T, const Work& Wk, Gl
 
 hipError_t launch_place(const float* d_xyz, const BatchDesc& D, const RayConst& R, const Table& T,
                         const Work& Wk, hipStream_t st) {
-    k_place<<<D.n_blocks, PLC_THREADS, 0, st>>>(d_xyz, D, R, T, Wk);
+    if (R.sem == 1) k_place<1><<<D.n_blocks, PLC_THREADS, 0, st>>>(d_xyz, D, R, T, Wk);
+    else k_place<0><<<D.n_blocks, PLC_THREADS, 0, st>>>(d_xyz, D, R, T, Wk);
     return hipGetLastError();
 }
 

@@ -145,6 +145,174 @@ __device__ __forceinline__ bool ray_step(RayState& r) {
     return true;
 }
 
+// ------------------------------------------------------------------------------------------------
+// Voxblox ray model (TSDF_SEM_VOXBLOX; the bit-exact twin of oracle/tsdf_oracle.c walk_ray_vb,
+// which restates voxblox SimpleTsdfIntegrator / RayCaster / updateTsdfVoxel — DESIGN.md §2b)
+
+constexpr float VB_MIN_WEIGHT = 1.0f / 65536.0f;  // lighter samples are dropped whole
+
+struct VbState {
+    float px;              // hit x (diagnostic builds only)
+    float dx, dy, dz;      // p - o
+    float depth;           // |p - o| (Eigen association: x + (y + z))
+    float tnx, tny, tnz;   // t_to_next_boundary
+    float tdx, tdy, tdz;   // t_step_size
+    int vx, vy, vz;
+    int sx, sy, sz;
+    int rem;               // steps left (RayCaster: ray_length_in_steps - current_step)
+};
+
+__device__ __forceinline__ void vb_axis(float ss, float es, int& v, int& st, float& tn, float& td,
+                                        int& steps) {
+    v = (int)__builtin_floorf(ss + 1e-6f);  // getGridIndexFromPoint: floor(x + kCoordinateEpsilon)
+    const int e = (int)__builtin_floorf(es + 1e-6f);
+    steps += e > v ? e - v : v - e;
+    const float r = es - ss;
+    st = (0.0f < r) - (r < 0.0f);
+    const float corr = st > 0 ? 1.0f : 0.0f;
+    tn = st == 0 ? __builtin_inff() : (corr - (ss - (float)v)) / r;
+    td = st == 0 ? __builtin_inff() : (float)st / r;
+}
+
+// isPointValid + RayCaster setup; false when the ray is dropped.
+__device__ __forceinline__ bool vb_init(const RayConst& R, float ox, float oy, float oz, float px,
+                                        float py, float pz, VbState& r) {
+    const float dx = px - ox, dy = py - oy, dz = pz - oz;
+    const float depth = __builtin_sqrtf(dx * dx + (dy * dy + dz * dz));
+    if (!(depth > 0.0f)) return false;
+    if (depth < R.min_range) return false;
+    const bool clearing = depth > R.max_range;
+    if (clearing && !R.allow_clear) return false;
+    const float ux = dx / depth, uy = dy / depth, uz = dz / depth;
+    float ex, ey, ez, sx, sy, sz;
+    if (clearing) {
+        float len = depth - R.tau;
+        len = len > 0.0f ? len : 0.0f;
+        len = R.max_range < len ? R.max_range : len;
+        ex = ox + ux * len;
+        ey = oy + uy * len;
+        ez = oz + uz * len;
+        sx = ex;
+        sy = ey;
+        sz = ez;
+    } else {
+        ex = px + ux * R.tau;
+        ey = py + uy * R.tau;
+        ez = pz + uz * R.tau;
+        sx = px - ux * R.tau;
+        sy = py - uy * R.tau;
+        sz = pz - uz * R.tau;
+    }
+    if (R.carving) {
+        sx = ox;
+        sy = oy;
+        sz = oz;
+    }
+    int steps = 0;
+    vb_axis(sx * R.inv_vs, ex * R.inv_vs, r.vx, r.sx, r.tnx, r.tdx, steps);
+    vb_axis(sy * R.inv_vs, ey * R.inv_vs, r.vy, r.sy, r.tny, r.tdy, steps);
+    vb_axis(sz * R.inv_vs, ez * R.inv_vs, r.vz, r.sz, r.tnz, r.tdz, steps);
+    r.rem = min(steps, MAX_DDA_STEPS - 1);
+    r.px = px;
+    r.dx = dx;
+    r.dy = dy;
+    r.dz = dz;
+    r.depth = depth;
+    return true;
+}
+
+// updateTsdfVoxel's weight for a sample (use_const_weight, optional dropoff)
+__device__ __forceinline__ float vb_weight(const RayConst& R, float sdf) {
+    float w = 1.0f;
+    if (R.dropoff && sdf < -R.vs) {
+        w = (w * (R.tau + sdf)) / R.tau_m_vs;
+        w = w > 0.0f ? w : 0.0f;
+    }
+    return w;
+}
+
+// computeDistance at the current voxel (projective sdf, untruncated); true when its weight is kept
+__device__ __forceinline__ bool vb_sample(const RayConst& R, float ox, float oy, float oz,
+                                          const VbState& r, float& s) {
+    const bool inl = r.vx > -VOX_LIMIT && r.vx < VOX_LIMIT && r.vy > -VOX_LIMIT &&
+                     r.vy < VOX_LIMIT && r.vz > -VOX_LIMIT && r.vz < VOX_LIMIT;
+    const float cx = ((float)r.vx + 0.5f) * R.vs;
+    const float cy = ((float)r.vy + 0.5f) * R.vs;
+    const float cz = ((float)r.vz + 0.5f) * R.vs;
+    const float ax = cx - ox, ay = cy - oy, az = cz - oz;
+    const float proj = (ax * r.dx + (ay * r.dy + az * r.dz)) / r.depth;
+    const float sdf = r.depth - proj;
+    s = sdf;
+    return inl && vb_weight(R, sdf) >= VB_MIN_WEIGHT;
+}
+
+// nextRayIndex's advance: the first minimum of t_next (Eigen minCoeff) steps by its sign
+__device__ __forceinline__ bool vb_step(VbState& r) {
+    if (r.rem <= 0) return false;
+    r.rem--;
+    const bool y0 = r.tny < r.tnx;
+    const float m01 = y0 ? r.tny : r.tnx;
+    const bool mz = r.tnz < m01;
+    const bool my = y0 && !mz;
+    const bool mx = !y0 && !mz;
+    r.tnx = mx ? r.tnx + r.tdx : r.tnx;
+    r.tny = my ? r.tny + r.tdy : r.tny;
+    r.tnz = mz ? r.tnz + r.tdz : r.tnz;
+    r.vx += mx ? r.sx : 0;
+    r.vy += my ? r.sy : 0;
+    r.vz += mz ? r.sz : 0;
+    return true;
+}
+
+// The ray model of each semantics, as one interface for the walk kernels (k_count / k_place).
+template <int SEM>
+struct Walk;
+
+template <>
+struct Walk<0> {  // TSDF_SEM_VDBFUSION
+    typedef RayState State;
+    __device__ static __forceinline__ bool init(const RayConst& R, float ox, float oy, float oz,
+                                                float px, float py, float pz, State& r) {
+        return ray_init(R, ox, oy, oz, px, py, pz, r);
+    }
+    __device__ static __forceinline__ bool gate(const RayConst& R, float ox, float oy, float oz,
+                                                const State& r) {
+        return voxel_gate(R, ox, oy, oz, r);
+    }
+    __device__ static __forceinline__ bool sample(const RayConst& R, float ox, float oy, float oz,
+                                                  const State& r, float& s) {
+        return voxel_sample(R, ox, oy, oz, r, s);
+    }
+    __device__ static __forceinline__ bool sample_sel(const RayConst& R, float ox, float oy,
+                                                      float oz, const State& r, float& s) {
+        return voxel_sample_sel(R, ox, oy, oz, r, s);
+    }
+    __device__ static __forceinline__ bool step(State& r) { return ray_step(r); }
+};
+
+template <>
+struct Walk<1> {  // TSDF_SEM_VOXBLOX
+    typedef VbState State;
+    __device__ static __forceinline__ bool init(const RayConst& R, float ox, float oy, float oz,
+                                                float px, float py, float pz, State& r) {
+        return vb_init(R, ox, oy, oz, px, py, pz, r);
+    }
+    __device__ static __forceinline__ bool gate(const RayConst& R, float ox, float oy, float oz,
+                                                const State& r) {
+        float s;
+        return vb_sample(R, ox, oy, oz, r, s);
+    }
+    __device__ static __forceinline__ bool sample(const RayConst& R, float ox, float oy, float oz,
+                                                  const State& r, float& s) {
+        return vb_sample(R, ox, oy, oz, r, s);
+    }
+    __device__ static __forceinline__ bool sample_sel(const RayConst& R, float ox, float oy,
+                                                      float oz, const State& r, float& s) {
+        return vb_sample(R, ox, oy, oz, r, s);
+    }
+    __device__ static __forceinline__ bool step(State& r) { return vb_step(r); }
+};
+
 __device__ __forceinline__ uint64_t pack_brick(int bx, int by, int bz) {
     return (uint64_t)(bx + BRICK_COORD_BIAS) | ((uint64_t)(by + BRICK_COORD_BIAS) << 21) |
            ((uint64_t)(bz + BRICK_COORD_BIAS) << 42);

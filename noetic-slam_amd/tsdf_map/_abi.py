@@ -16,6 +16,11 @@ STATUS_NAMES = {
     TSDF_EHIP: "TSDF_EHIP", TSDF_ENODEV: "TSDF_ENODEV", TSDF_EOVERFLOW: "TSDF_EOVERFLOW",
 }
 
+ABI_VERSION = 3
+SEM_VDBFUSION = 0
+SEM_VOXBLOX = 1
+SEMANTICS = {"vdbfusion": SEM_VDBFUSION, "voxblox": SEM_VOXBLOX}
+
 KERNEL_KINDS = ("count", "compact", "place", "integrate")  # k_<kind>, KernelKind order
 
 
@@ -34,6 +39,11 @@ class TsdfParams(C.Structure):
         ("brick_side", C.c_int32),
         ("max_batch", C.c_uint32),
         ("pipeline", C.c_uint32),
+        # ABI v3
+        ("semantics", C.c_int32),
+        ("allow_clear", C.c_int32),
+        ("use_weight_dropoff", C.c_int32),
+        ("max_weight", C.c_float),
     ]
 
 
@@ -132,6 +142,7 @@ def default_params(lib=None, **kw):
         p.min_range, p.max_range = 0.0, math.inf
         p.max_bricks, p.max_points, p.max_pairs = 1 << 20, 1 << 18, 0
         p.device_id, p.brick_side, p.max_batch = 0, BRICK_SIDE, 32
+        p.semantics, p.allow_clear, p.use_weight_dropoff, p.max_weight = SEM_VDBFUSION, 1, 1, 1e4
     for k, v in kw.items():
         if not hasattr(p, k):
             raise TypeError("unknown tsdf_params field %r" % k)

@@ -8,6 +8,10 @@ space_carving), `integrate(points, extrinsic)` with extrinsic a (3,) origin or a
 translation is the origin, points already in the world frame) is what `TSDFVolume` mirrors, so a
 user of that backend finds the same names, argument meanings and errors.
 
+`semantics="voxblox"` selects backend idx 2's fusion rule instead (voxblox SimpleTsdfIntegrator
+with a constant weight: projective distance, weight dropoff, clamps), and
+`SimpleTsdfIntegrator` below mirrors voxblox's own names for it.
+
 `TSDFVolume` is bound to one library exporting include/tsdf_hip.h; `HipTSDFVolume` is the product
 class (MAP_BACKEND_IDX = 4) and loads libtsdf_hip.so only — it raises if the HIP library or the GPU
 is missing, there is no CPU fallback.
@@ -45,8 +49,11 @@ class TSDFVolume:
 
     def __init__(self, lib, voxel_size, sdf_trunc, space_carving=False, min_range=0.0,
                  max_range=math.inf, max_bricks=1 << 20, max_points=1 << 18, device_id=0,
-                 max_batch=32, pipeline=False):
+                 max_batch=32, pipeline=False, semantics="vdbfusion", allow_clear=True,
+                 use_weight_dropoff=True, max_weight=10000.0):
         self._lib = lib
+        if semantics not in _abi.SEMANTICS:
+            raise ValueError("semantics must be one of %s" % sorted(_abi.SEMANTICS))
         self._ctx = C.c_void_p()
         p = _abi.default_params(lib)
         p.voxel_size = float(voxel_size)
@@ -59,7 +66,12 @@ class TSDFVolume:
         p.max_points = int(max_points)
         p.max_batch = int(max_batch)
         p.device_id = int(device_id)
+        p.semantics = _abi.SEMANTICS[semantics]
+        p.allow_clear = 1 if allow_clear else 0
+        p.use_weight_dropoff = 1 if use_weight_dropoff else 0
+        p.max_weight = float(max_weight)
         self.params = p
+        self.semantics = semantics
         rc = lib.tsdf_create(C.byref(p), C.byref(self._ctx))
         if rc != _abi.TSDF_OK:
             self._ctx = C.c_void_p()
@@ -246,6 +258,50 @@ class HipTSDFVolume(TSDFVolume):
 
     def set_profiling(self, on=True):
         self._check(self._lib.tsdf_set_profiling(self._ctx, 1 if on else 0), "set_profiling")
+
+
+class TsdfIntegratorConfig:
+    """voxblox TsdfIntegratorBase::Config (the fields this backend implements; defaults as
+    upstream).  use_const_weight must stay True: the 1/z^2 weight needs the sensor-frame point per
+    sample, which the world-frame boundary does not carry."""
+
+    def __init__(self, default_truncation_distance=0.1, max_weight=10000.0,
+                 voxel_carving_enabled=True, min_ray_length_m=0.1, max_ray_length_m=5.0,
+                 use_const_weight=True, allow_clear=True, use_weight_dropoff=True):
+        self.default_truncation_distance = default_truncation_distance
+        self.max_weight = max_weight
+        self.voxel_carving_enabled = voxel_carving_enabled
+        self.min_ray_length_m = min_ray_length_m
+        self.max_ray_length_m = max_ray_length_m
+        self.use_const_weight = use_const_weight
+        self.allow_clear = allow_clear
+        self.use_weight_dropoff = use_weight_dropoff
+
+
+class SimpleTsdfIntegrator:
+    """voxblox-named facade over a `semantics="voxblox"` volume (MAP_BACKEND_IDX 2's fusion rule
+    on the GPU): `integratePointCloud(T_G_C, points_C)` transforms the sensor-frame points by the
+    4x4 pose (float64, then float32) and integrates them from the pose's translation."""
+
+    def __init__(self, config, voxel_size, volume_cls=None, **kw):
+        if not config.use_const_weight:
+            raise NotImplementedError("use_const_weight=False (1/z^2 weights) is not supported")
+        cls = volume_cls or HipTSDFVolume
+        self.config = config
+        self.volume = cls(voxel_size, config.default_truncation_distance,
+                          space_carving=config.voxel_carving_enabled,
+                          min_range=config.min_ray_length_m, max_range=config.max_ray_length_m,
+                          semantics="voxblox", allow_clear=config.allow_clear,
+                          use_weight_dropoff=config.use_weight_dropoff,
+                          max_weight=config.max_weight, **kw)
+
+    def integratePointCloud(self, T_G_C, points_C, colors=None, freespace_points=False):  # noqa: N802
+        if freespace_points:
+            raise NotImplementedError("freespace_points is not supported")
+        T = np.asarray(T_G_C, np.float64).reshape(4, 4)
+        pc = np.asarray(points_C, np.float64).reshape(-1, 3)
+        pts_g = (pc @ T[:3, :3].T + T[:3, 3]).astype(np.float32)
+        self.volume.integrate(pts_g, T)
 
 
 def select_sector(points, origin, sector, n_sectors, yaw0=0.0):

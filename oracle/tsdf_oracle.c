@@ -58,13 +58,15 @@ typedef struct {
     int32_t used;
     float S, W;     /* persistent field */
     int64_t A;      /* per-scan fixed-point sum of w*s (scale 2^32) */
-    uint32_t B;     /* per-scan count (sum of w, w = 1) */
+    int64_t B;      /* per-scan sum of w: a count (VDBFusion, w = 1) or fixed point 2^32 (Voxblox) */
     uint32_t stamp; /* last scan that touched it (for the touched list) */
 } vox_t;
 
 struct tsdf_ctx {
     tsdf_params p;
     float vs, inv_vs, tau;
+    float bg;   /* background distance: tau (VDBFusion) or 0 (Voxblox TsdfVoxel) */
+    int sem;    /* TSDF_SEM_* */
     vox_t* tab;
     uint64_t cap, n;
     uint32_t* touched; /* indices into tab of voxels touched this scan */
@@ -102,7 +104,7 @@ static int64_t vox_get(tsdf_ctx* c, int32_t x, int32_t y, int32_t z) {
         if (!v->used) {
             v->used = 1;
             v->x = x; v->y = y; v->z = z;
-            v->S = c->tau; /* VDBFusion background: tsdf = sdf_trunc, weight = 0 */
+            v->S = c->bg; /* background: (sdf_trunc, 0) VDBFusion, (0, 0) Voxblox */
             v->W = 0.0f;
             v->A = 0; v->B = 0; v->stamp = 0;
             c->n++;
@@ -166,6 +168,10 @@ void tsdf_default_params(tsdf_params* p) {
     p->device_id = 0;
     p->brick_side = TSDF_BRICK_SIDE;
     p->max_batch = 32; /* accepted for ABI parity; the oracle integrates scan by scan */
+    p->semantics = TSDF_SEM_VDBFUSION;
+    p->allow_clear = 1;        /* voxblox TsdfIntegratorBase::Config defaults */
+    p->use_weight_dropoff = 1;
+    p->max_weight = 10000.0f;
 }
 
 int tsdf_abi_version(void) { return TSDF_ABI_VERSION; }
@@ -173,7 +179,9 @@ int tsdf_abi_version(void) { return TSDF_ABI_VERSION; }
 int tsdf_create(const tsdf_params* params, tsdf_ctx** out) {
     if (!params || !out) return TSDF_EINVAL;
     if (!(params->voxel_size > 0) || !(params->sdf_trunc > 0) ||
-        params->brick_side != TSDF_BRICK_SIDE || params->weight_mode != TSDF_WEIGHT_CONSTANT)
+        params->brick_side != TSDF_BRICK_SIDE || params->weight_mode != TSDF_WEIGHT_CONSTANT ||
+        (params->semantics != TSDF_SEM_VDBFUSION && params->semantics != TSDF_SEM_VOXBLOX) ||
+        (params->semantics == TSDF_SEM_VOXBLOX && !(params->max_weight > 0.0f)))
         return TSDF_EINVAL;
     tsdf_ctx* c = (tsdf_ctx*)calloc(1, sizeof *c);
     if (!c) return TSDF_ENOMEM;
@@ -181,6 +189,8 @@ int tsdf_create(const tsdf_params* params, tsdf_ctx** out) {
     c->vs = (float)params->voxel_size;
     c->inv_vs = 1.0f / c->vs;
     c->tau = (float)params->sdf_trunc;
+    c->sem = params->semantics;
+    c->bg = c->sem == TSDF_SEM_VOXBLOX ? 0.0f : c->tau;
     c->mode = ORACLE_MODE_SCAN_FUSED;
     *out = c;
     return TSDF_OK;
@@ -204,7 +214,8 @@ int tsdf_oracle_set_mode(tsdf_ctx* c, int mode) {
 
 /* ---- the ray walk (VDBFusion Integrate body, one point) ---------------------------------- */
 
-typedef void (*visit_fn)(tsdf_ctx* c, int32_t vx, int32_t vy, int32_t vz, float s, void* user);
+typedef void (*visit_fn)(tsdf_ctx* c, int32_t vx, int32_t vy, int32_t vz, float s, float w,
+                         void* user);
 
 /* Returns the number of voxels visited by the DDA (gated or not); calls visit() for every voxel
  * with sdf > -tau, in DDA order.  All arithmetic fp32, no contraction (built -ffp-contract=off). */
@@ -261,7 +272,7 @@ static int64_t walk_ray(tsdf_ctx* c, float px, float py, float pz, float ox, flo
             const float proj = ax * bx + ay * by + az * bz;
             if (proj > 0.0f || proj < 0.0f) {
                 const float sdf = proj > 0.0f ? dist : -dist;
-                if (sdf > -tau) visit(c, v[0], v[1], v[2], sdf < tau ? sdf : tau, user);
+                if (sdf > -tau) visit(c, v[0], v[1], v[2], sdf < tau ? sdf : tau, 1.0f, user);
             }
         }
         /* math::MinIndex tie-break: equal entries resolve to the higher axis */
@@ -275,13 +286,132 @@ static int64_t walk_ray(tsdf_ctx* c, float px, float py, float pz, float ox, flo
     return visited;
 }
 
-static void visit_accum(tsdf_ctx* c, int32_t x, int32_t y, int32_t z, float s, void* user) {
+/* ---- the Voxblox ray walk (SimpleTsdfIntegrator::integrateFunction body, one point) ----------
+ *
+ * voxblox (ethz-asl/voxblox, unpinned version; not in /root/reference — SURVEY §8a9), restated:
+ *   isPointValid:   d = |p - o|; d < min_ray_length -> dropped; d > max_ray_length -> a clearing
+ *                   ray if allow_clear, else dropped
+ *   RayCaster ctor: u = (p - o).normalized();
+ *                   clearing: len = min(max(d - tau, 0), max_ray_length), end = o + u len,
+ *                             start = carving ? o : end
+ *                   else:     end = p + u tau, start = carving ? o : p - u tau
+ *                   start/end scaled by 1/voxel_size
+ *   setupRayCaster: cur = floor(start_s + kCoordinateEpsilon) (getGridIndexFromPoint, 1e-6),
+ *                   steps = |floor(end_s + eps) - cur|_1; r = end_s - start_s; sign = signum(r);
+ *                   t_next = (max(0, sign) - (start_s - cur)) / r; t_step = sign / r
+ *   nextRayIndex:   steps + 1 voxels; after each, the axis of the FIRST minimum of t_next
+ *                   (Eigen minCoeff: ties -> lower axis) advances by its sign
+ *   updateTsdfVoxel (use_const_weight): c = (v + 1/2) vs;
+ *                   sdf = |p - o| - ((c - o).(p - o)) / |p - o|     (computeDistance, projective)
+ *                   w = 1; dropoff: sdf < -vs -> w = (w (tau + sdf)) / (tau - vs), max(w, 0)
+ *                   W' = W + w (W' < kFloatEpsilon: no update); S' = (sdf w + S W) / W'
+ *                   S = S' > 0 ? min(tau, S') : max(-tau, S');  W = min(max_weight, W')
+ * Stated deviations:
+ *   - a zero component of r gets t_next = t_step = +inf (the axis never advances).  Upstream's
+ *     guard `std::abs(r) < 0.0` is never true, so it divides by zero and the NaN/-inf entry
+ *     stalls the walk on that axis; the +inf is the guard's evident intent;
+ *   - samples of weight < 2^-16 are dropped whole (no allocation, no fuse): upstream allocates the
+ *     block and applies the (negligible) update;
+ *   - zero-length rays (p == o) are dropped;
+ *   - validity uses |p - o| of the world-frame cloud (upstream: |point_C|, the same in exact
+ *     arithmetic).
+ * All fp32, -ffp-contract=off, the GPU's op order (tsdf_ray.h vb_*). */
+#define VB_MIN_WEIGHT (1.0f / 65536.0f)
+
+static int64_t walk_ray_vb(tsdf_ctx* c, float px, float py, float pz, float ox, float oy,
+                           float oz, visit_fn visit, void* user) {
+    const float vs = c->vs, inv_vs = c->inv_vs, tau = c->tau;
+    const float dx = px - ox, dy = py - oy, dz = pz - oz;
+    /* Eigen's fixed-size-3 reductions (squaredNorm, dot) associate as x + (y + z) */
+    const float depth = sqrtf(dx * dx + (dy * dy + dz * dz));
+    if (!(depth > 0.0f)) return -1;
+    if (depth < (float)c->p.min_range) return -1;
+    int clearing = 0;
+    if (depth > (float)c->p.max_range) {
+        if (!c->p.allow_clear) return -1;
+        clearing = 1;
+    }
+    const float ux = dx / depth, uy = dy / depth, uz = dz / depth;
+    float ex, ey, ez, sx, sy, sz;
+    if (clearing) {
+        float len = depth - tau;
+        len = len > 0.0f ? len : 0.0f;
+        len = (float)c->p.max_range < len ? (float)c->p.max_range : len;
+        ex = ox + ux * len; ey = oy + uy * len; ez = oz + uz * len;
+        if (c->p.space_carving) { sx = ox; sy = oy; sz = oz; }
+        else { sx = ex; sy = ey; sz = ez; }
+    } else {
+        ex = px + ux * tau; ey = py + uy * tau; ez = pz + uz * tau;
+        if (c->p.space_carving) { sx = ox; sy = oy; sz = oz; }
+        else { sx = px - ux * tau; sy = py - uy * tau; sz = pz - uz * tau; }
+    }
+    const float ss[3] = {sx * inv_vs, sy * inv_vs, sz * inv_vs};
+    const float es[3] = {ex * inv_vs, ey * inv_vs, ez * inv_vs};
+    int32_t v[3], st[3];
+    float tn[3], td[3];
+    int64_t steps = 0;
+    for (int a = 0; a < 3; a++) {
+        v[a] = (int32_t)floorf(ss[a] + 1e-6f);
+        const int32_t e = (int32_t)floorf(es[a] + 1e-6f);
+        steps += e > v[a] ? (int64_t)e - v[a] : (int64_t)v[a] - e;
+        const float r = es[a] - ss[a];
+        st[a] = (0.0f < r) - (r < 0.0f);
+        if (st[a] == 0) {
+            tn[a] = INFINITY;
+            td[a] = INFINITY;
+        } else {
+            const float corr = st[a] > 0 ? 1.0f : 0.0f;
+            tn[a] = (corr - (ss[a] - (float)v[a])) / r;
+            td[a] = (float)st[a] / r;
+        }
+    }
+    if (steps > MAX_DDA_STEPS) steps = MAX_DDA_STEPS;
+    for (int64_t k = 0;; k++) {
+        if (v[0] > -VOX_LIMIT && v[0] < VOX_LIMIT && v[1] > -VOX_LIMIT && v[1] < VOX_LIMIT &&
+            v[2] > -VOX_LIMIT && v[2] < VOX_LIMIT) {
+            const float cx = ((float)v[0] + 0.5f) * vs;
+            const float cy = ((float)v[1] + 0.5f) * vs;
+            const float cz = ((float)v[2] + 0.5f) * vs;
+            const float ax = cx - ox, ay = cy - oy, az = cz - oz; /* v_voxel_origin */
+            const float proj = (ax * dx + (ay * dy + az * dz)) / depth; /* dist_G_V */
+            const float sdf = depth - proj;
+            float w = 1.0f;
+            if (c->p.use_weight_dropoff && sdf < -vs) {
+                w = (w * (tau + sdf)) / (tau - vs);
+                w = w > 0.0f ? w : 0.0f;
+            }
+            if (w >= VB_MIN_WEIGHT) visit(c, v[0], v[1], v[2], sdf, w, user);
+        }
+        if (k >= steps) break;
+        /* Eigen minCoeff: the first minimum wins */
+        int a = 0;
+        if (tn[1] < tn[a]) a = 1;
+        if (tn[2] < tn[a]) a = 2;
+        v[a] += st[a];
+        tn[a] += td[a];
+    }
+    return steps + 1;
+}
+
+static void visit_accum(tsdf_ctx* c, int32_t x, int32_t y, int32_t z, float s, float w,
+                        void* user) {
     int* fail = (int*)user;
     int64_t i = vox_get(c, x, y, z);
     if (i < 0) { *fail = 1; return; }
     vox_t* v = &c->tab[i];
+    if (c->mode == ORACLE_MODE_SEQUENTIAL && c->sem == TSDF_SEM_VOXBLOX) {
+        /* updateTsdfVoxel, literally, in input order */
+        const float nw = v->W + w;
+        if (!(nw < 1e-6f)) { /* kFloatEpsilon */
+            const float ns = (s * w + v->S * v->W) / nw;
+            const float tau = c->tau;
+            v->S = ns > 0.0f ? (ns < tau ? ns : tau) : (-tau < ns ? ns : -tau);
+            v->W = nw < c->p.max_weight ? nw : c->p.max_weight;
+        }
+        if (v->stamp != c->scan_id) { v->stamp = c->scan_id; c->st.n_voxels_last++; }
+        return;
+    }
     if (c->mode == ORACLE_MODE_SEQUENTIAL) {
-        const float w = 1.0f;
         const float nw = v->W + w;
         v->S = (v->S * v->W + s * w) / nw;
         v->W = nw;
@@ -299,15 +429,34 @@ static void visit_accum(tsdf_ctx* c, int32_t x, int32_t y, int32_t z, float s, v
         }
         c->touched[c->n_touched++] = (uint32_t)i;
     }
+    if (c->sem == TSDF_SEM_VOXBLOX) {
+        v->A += (int64_t)((s * w) * 4294967296.0f); /* trunc(s w 2^32) */
+        v->B += (int64_t)(w * 4294967296.0f);       /* trunc(w 2^32) */
+        return;
+    }
     v->A += (int64_t)(s * 4294967296.0f); /* trunc(s * 2^32): exact scaling, C truncation */
-    v->B += 1u;
+    v->B += 1;
 }
 
 static void fuse_scan(tsdf_ctx* c) {
     for (uint64_t k = 0; k < c->n_touched; k++) {
         vox_t* v = &c->tab[c->touched[k]];
-        const float b = (float)v->B;
         const float a = (float)((double)v->A * (1.0 / 4294967296.0));
+        if (c->sem == TSDF_SEM_VOXBLOX) {
+            /* updateTsdfVoxel with the scan's samples applied together: (a, b) = (sum s w, sum w) */
+            const float b = (float)((double)v->B * (1.0 / 4294967296.0));
+            const float nw = v->W + b;
+            if (!(nw < 1e-6f)) {
+                const float ns = (a + v->S * v->W) / nw;
+                const float tau = c->tau;
+                v->S = ns > 0.0f ? (ns < tau ? ns : tau) : (-tau < ns ? ns : -tau);
+                v->W = nw < c->p.max_weight ? nw : c->p.max_weight;
+            }
+            v->A = 0;
+            v->B = 0;
+            continue;
+        }
+        const float b = (float)v->B;
         const float nw = v->W + b;
         v->S = (v->S * v->W + a) / nw;
         v->W = nw;
@@ -341,7 +490,10 @@ int tsdf_integrate(tsdf_ctx* c, const void* pts, uint64_t n, uint32_t point_step
             memcpy(f, q, sizeof f);
             px = f[0]; py = f[1]; pz = f[2];
         }
-        if (walk_ray(c, px, py, pz, ox, oy, oz, visit_accum, &fail) >= 0) c->st.n_rays_total++;
+        const int64_t r = c->sem == TSDF_SEM_VOXBLOX
+                              ? walk_ray_vb(c, px, py, pz, ox, oy, oz, visit_accum, &fail)
+                              : walk_ray(c, px, py, pz, ox, oy, oz, visit_accum, &fail);
+        if (r >= 0) c->st.n_rays_total++;
     }
     if (fail) return set_err(c, TSDF_ENOMEM, "oracle allocation failed");
     if (c->mode == ORACLE_MODE_SCAN_FUSED) fuse_scan(c);
@@ -363,7 +515,7 @@ int tsdf_query_dense(tsdf_ctx* c, const int32_t lo[3], const int32_t hi[3], floa
         for (int32_t y = lo[1]; y < hi[1]; y++)
             for (int32_t x = lo[0]; x < hi[0]; x++, i++) {
                 const vox_t* v = vox_find(c, x, y, z);
-                if (sdf) sdf[i] = v ? v->S : c->tau;
+                if (sdf) sdf[i] = v ? v->S : c->bg;
                 if (weight) weight[i] = v ? v->W : 0.0f;
             }
     return TSDF_OK;
@@ -426,7 +578,7 @@ int tsdf_export_bricks(tsdf_ctx* c, int32_t* coords, float* sdf, float* weight, 
         for (int l = 0; l < 512; l++) {
             const int lx = l & 7, ly = (l >> 3) & 7, lz = l >> 6;
             const vox_t* v = vox_find(c, e[i].b[0] * 8 + lx, e[i].b[1] * 8 + ly, e[i].b[2] * 8 + lz);
-            if (sdf) sdf[512 * i + l] = v ? v->S : c->tau;
+            if (sdf) sdf[512 * i + l] = v ? v->S : c->bg;
             if (weight) weight[512 * i + l] = v ? v->W : 0.0f;
         }
     }
@@ -522,8 +674,10 @@ int tsdf_oracle_export_voxels(const tsdf_ctx* c, int32_t* ijk, float* sdf, float
 
 typedef struct { int32_t* ijk; float* s; uint64_t n, cap; } ray_rec;
 
-static void visit_record(tsdf_ctx* c, int32_t x, int32_t y, int32_t z, float s, void* user) {
+static void visit_record(tsdf_ctx* c, int32_t x, int32_t y, int32_t z, float s, float w,
+                         void* user) {
     (void)c;
+    (void)w;
     ray_rec* r = (ray_rec*)user;
     if (r->n < r->cap) {
         r->ijk[3 * r->n] = x; r->ijk[3 * r->n + 1] = y; r->ijk[3 * r->n + 2] = z;
@@ -537,8 +691,10 @@ static void visit_record(tsdf_ctx* c, int32_t x, int32_t y, int32_t z, float s, 
 int64_t tsdf_oracle_ray_voxels(tsdf_ctx* c, const float p[3], const double origin[3],
                                int32_t* ijk, float* sdf, uint64_t cap) {
     ray_rec r = {ijk, sdf, 0, cap};
-    int64_t v = walk_ray(c, p[0], p[1], p[2], (float)origin[0], (float)origin[1],
-                         (float)origin[2], visit_record, &r);
+    const float ox = (float)origin[0], oy = (float)origin[1], oz = (float)origin[2];
+    int64_t v = c->sem == TSDF_SEM_VOXBLOX
+                    ? walk_ray_vb(c, p[0], p[1], p[2], ox, oy, oz, visit_record, &r)
+                    : walk_ray(c, p[0], p[1], p[2], ox, oy, oz, visit_record, &r);
     if (v < 0) return -1;
     return (int64_t)r.n;
 }
