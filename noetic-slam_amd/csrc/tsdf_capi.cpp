@@ -364,9 +364,9 @@ void tsdf_destroy(tsdf_ctx* c) {
                    c->T.touched,
                    c->T.brick_keys,  c->Pl.sdf,          c->Pl.weight,     c->G,
                    c->cell2[0],      c->cell2[1],        c->stage2[0],     c->stage2[1],
-                   c->W2[0].pair,    c->W2[0].blk,       c->W2[0].blk_occ, c->W2[0].fb,
+                   c->W2[0].pair,    c->W2[0].blk,       c->W2[0].blk_n, c->W2[0].fb,
                    c->W2[0].smp,     c->W2[0].active,    c->W2[1].pair,    c->W2[1].blk,
-                   c->W2[1].blk_occ, c->W2[1].fb,        c->W2[1].smp,     c->W2[1].active,
+                   c->W2[1].blk_n, c->W2[1].fb,        c->W2[1].smp,     c->W2[1].active,
                    c->W2[0].cagg,    c->W2[1].cagg};
     for (void* d : dev)
         if (d) (void)hipFree(d);
@@ -460,7 +460,7 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
         W = c->Wk;  // capacities
         HIPCHK(c, hipMalloc(&W.pair, slots * sizeof(uint32_t)));
         HIPCHK(c, hipMalloc(&W.blk, (size_t)c->max_blocks * HCAP * sizeof(uint4)));
-        HIPCHK(c, hipMalloc(&W.blk_occ, (size_t)c->max_blocks * (HCAP / 32) * sizeof(uint32_t)));
+        HIPCHK(c, hipMalloc(&W.blk_n, (size_t)c->max_blocks * sizeof(uint32_t)));
         HIPCHK(c, hipMalloc(&W.fb, (size_t)W.max_fb * sizeof(uint4)));
         HIPCHK(c, hipMalloc(&W.smp, (size_t)W.max_smp * sizeof(uint2)));
         HIPCHK(c, hipMalloc(&W.active, (size_t)W.max_active * sizeof(uint4)));

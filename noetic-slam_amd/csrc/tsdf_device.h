@@ -15,8 +15,8 @@
 //   Pool    sdf[max_bricks][512] f32, weight[max_bricks][512] f32 — voxel l = z*64 + y*8 + x;
 //           brick_keys[max_bricks] u64 (slot -> key, for export)
 //   Work    pair[max_batch_points * maxp] u32    per-ray pair codes (see PAIR_*)
-//           blk[n_blocks * HCAP] uint4          per-block local brick table (tidx, cell base,
-//                                               offset of the run in the block, run samples)
+//           blk[n_blocks * HCAP] uint4          per-block dense run list (tidx, cell rank -> sample
+//                                               position, offset of the run in the block, samples)
 //           fb[..] uint4                        fallback pairs (block's LDS hash full)
 //           smp[..] uint2                       the batch's samples: (sdf bits, scan << 9 | voxel),
 //                                               per brick contiguous and scan-ordered
@@ -101,8 +101,10 @@ struct Pool {
 
 struct Work {
     uint32_t* pair;
-    uint4* blk;      // n_blocks * HCAP: (table index, cell base, run offset, run samples)
-    uint32_t* blk_occ;  // n_blocks * HCAP/32 occupancy bits
+    uint4* blk;      // n_blocks * HCAP: per k_count workgroup its DENSE run list (table index,
+                     // rank in the (brick, scan) cell,
+                     // run offset in the workgroup's sample order, run samples | LDS slot << 16)
+    uint32_t* blk_n; // n_blocks: runs in the list
     uint4* fb;       // fallback pairs: (tidx, scan, rank, 0)
     uint2* smp;  // x = truncated sdf (f32 bits), y = scan << 9 | local voxel
     uint4* active;  // (h, slot, toff, cnt) per active brick (k_compact)

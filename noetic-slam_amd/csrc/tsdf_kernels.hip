@@ -76,15 +76,13 @@ __global__ __launch_bounds__(CNT_THREADS) void k_count(const float* __restrict__
                                                       int parity) {
     __shared__ unsigned long long s_key[HCAP];
     __shared__ uint32_t s_cnt[HCAP];
-    __shared__ uint32_t s_occ[HCAP / 32];
     __shared__ unsigned long long red[2][CNT_THREADS / 64];
-    __shared__ uint32_t s_wsum[CNT_THREADS / 64];
+    __shared__ unsigned long long s_wsum[CNT_THREADS / 64];
     Counters* C = &G->ctr[parity];  // zeroed by the previous batch of this parity (k_finish)
     for (int j = threadIdx.x; j < HCAP; j += CNT_THREADS) {
         s_key[j] = EMPTY_KEY;
         s_cnt[j] = 0u;
     }
-    if (threadIdx.x < HCAP / 32) s_occ[threadIdx.x] = 0u;
     __syncthreads();
     uint32_t t, r0, r1;
     block_range(D, blockIdx.x, t, r0, r1);
@@ -126,7 +124,11 @@ __global__ __launch_bounds__(CNT_THREADS) void k_count(const float* __restrict__
             // then emit pair j together, so the LDS hash work runs convergent, not once per lane.
             uint64_t q0 = EMPTY_KEY, q1 = EMPTY_KEY, q2 = EMPTY_KEY, q3 = EMPTY_KEY;
             uint32_t n0 = 0, n1 = 0, n2 = 0, n3 = 0, np = 0;
+#ifdef TSDF_ABLATE_CNT_NOWALK
+            if (ok && r.px == 1e30f) {
+#else
             if (ok) {
+#endif
                 uint64_t cur = EMPTY_KEY;
                 uint32_t ccount = 0;
                 for (int it = 0; it < MAX_DDA_STEPS; it++) {
@@ -203,29 +205,39 @@ __global__ __launch_bounds__(CNT_THREADS) void k_count(const float* __restrict__
     // one global find-or-insert + one atomic per distinct brick of the workgroup: the cell
     // (brick, scan) count reserves the workgroup's ranks; `touched` (a plain store) lists the brick
     // for k_compact, which also derives the brick's total from its cells.  Each thread takes
-    // HCAP / CNT_THREADS consecutive slots; a block scan over their sample counts gives every run
-    // its offset in the workgroup's sample order (k_place stages the samples in that order).
+    // HCAP / CNT_THREADS consecutive slots; a block scan over their sample and run counts gives
+    // every run its offset in the workgroup's sample order (k_place stages the samples in that
+    // order) and its index in the workgroup's DENSE run list (slot order = sample order).
     constexpr int SPT = HCAP / CNT_THREADS;
     uint4* bt = Wk.blk + (size_t)blockIdx.x * HCAP;
-    uint32_t run_sum = 0;
+    uint32_t run_sum = 0, run_cnt = 0;
 #pragma unroll
     for (int j = 0; j < SPT; j++) {
         const int slot = threadIdx.x * SPT + j;
-        run_sum += s_key[slot] != EMPTY_KEY ? s_cnt[slot] : 0u;
+        const bool occ = s_key[slot] != EMPTY_KEY;
+        run_sum += occ ? s_cnt[slot] : 0u;
+        run_cnt += occ ? 1u : 0u;
     }
-    uint32_t run_off;
+    uint32_t run_off, run_idx;
     {
         const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-        uint32_t incl = run_sum;
+        const unsigned long long x = (unsigned long long)run_sum | ((unsigned long long)run_cnt << 32);
+        unsigned long long incl = x;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t y = __shfl_up(incl, d, 64);
+            const unsigned long long y = __shfl_up(incl, d, 64);
             if (lane >= d) incl += y;
         }
         if (lane == 63) s_wsum[wid] = incl;
         __syncthreads();
-        run_off = incl - run_sum;
-        for (int w = 0; w < wid; w++) run_off += s_wsum[w];
+        unsigned long long ex = incl - x, tot = 0;
+        for (int w = 0; w < CNT_THREADS / 64; w++) {
+            ex += w < wid ? s_wsum[w] : 0ull;
+            tot += s_wsum[w];
+        }
+        run_off = (uint32_t)ex;
+        run_idx = (uint32_t)(ex >> 32);
+        if (threadIdx.x == CNT_THREADS - 1) Wk.blk_n[blockIdx.x] = (uint32_t)(tot >> 32);
     }
     // The thread's SPT slots go to the global table in three batched stages, so their round trips
     // overlap instead of running one slot after another: (1) first-probe loads of all keys,
@@ -253,12 +265,15 @@ __global__ __launch_bounds__(CNT_THREADS) void k_count(const float* __restrict__
         old[j] = hx[j] >= 0 ? atomicAdd(&T.cell[(size_t)hx[j] * T.cell_stride + t], s_cnt[slot])
                             : 0u;
     }
+    // dense run list: (table index | NO_PAIR, rank in the (brick, scan) cell, run offset in the
+    // workgroup's sample order, run samples | slot << 16)
+    static_assert(RPB * MAX_IN_BRICK < (1 << 16) && HCAP <= (1 << 16), "run record packing");
 #pragma unroll
     for (int j = 0; j < SPT; j++) {
         const int slot = threadIdx.x * SPT + j;
         if (key[j] == EMPTY_KEY) continue;
         const uint32_t n = s_cnt[slot];
-        uint4 e = make_uint4(NO_PAIR, 0u, run_off, n);
+        uint4 e = make_uint4(NO_PAIR, 0u, run_off, n | ((uint32_t)slot << 16));
         if (hx[j] >= 0) {
             e.x = (uint32_t)hx[j];
             e.y = old[j];
@@ -267,12 +282,8 @@ __global__ __launch_bounds__(CNT_THREADS) void k_count(const float* __restrict__
             if (old[j] == 0u) T.touched[e.x] = 1u;
         }
         run_off += n;
-        bt[slot] = e;
-        atomicOr(&s_occ[slot >> 5], 1u << (slot & 31));
+        bt[run_idx++] = e;
     }
-    __syncthreads();
-    if (threadIdx.x < HCAP / 32) Wk.blk_occ[(size_t)blockIdx.x * (HCAP / 32) + threadIdx.x] =
-        s_occ[threadIdx.x];
     // block-reduce the stats, one atomic per block on a shard picked by block index
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     unsigned long long v = wave_sum<unsigned long long>(valid);
@@ -531,8 +542,8 @@ __global__ __launch_bounds__(PLC_THREADS) void k_place(const float* __restrict__
     uint32_t t, r0, r1;
     block_range(D, blockIdx.x, t, r0, r1);
     const uint4* bt = Wk.blk + (size_t)blockIdx.x * HCAP;
-    const uint32_t* occ = Wk.blk_occ + (size_t)blockIdx.x * (HCAP / 32);
-    // the ray's own setup (point loads, divisions) overlaps the run-table gathers below
+    const uint32_t nruns = Wk.blk_n[blockIdx.x];
+    // the ray's own setup (point loads, divisions) overlaps the run-list loads below
     const float ox = D.ox[t], oy = D.oy[t], oz = D.oz[t];
     const uint32_t maxp = Wk.maxp;
     const uint32_t i = r0 + threadIdx.x;
@@ -545,25 +556,20 @@ __global__ __launch_bounds__(PLC_THREADS) void k_place(const float* __restrict__
     for (int j = threadIdx.x; j < PLC_WORDS; j += PLC_THREADS) s_bits[j] = 0u;
     if (threadIdx.x == 0) s_nst = 0u;
     __syncthreads();
-    // run table: global base and staging offset per run; staged runs mark their start
-    constexpr int SLOTS_PT = HCAP / PLC_THREADS;
-    uint32_t my_loff[SLOTS_PT];
-#pragma unroll
-    for (int q = 0; q < SLOTS_PT; q++) {
-        const int slot = threadIdx.x + q * PLC_THREADS;
-        my_loff[q] = 0xFFFFu;
-        if ((occ[slot >> 5] >> (slot & 31)) & 1u) {
-            const uint4 e = bt[slot];
-            uint32_t b = NO_PAIR;
-            if (e.x != NO_PAIR) b = T.cell[(size_t)e.x * T.cell_stride + t] + e.y;
-            s_base[slot] = b;
-            // runs starting past the staging capacity are stored directly (0xFFFF: not staged)
-            s_loff[slot] = e.z < (uint32_t)PLC_STAGE ? (uint16_t)e.z : (uint16_t)0xFFFFu;
-            if (e.z < (uint32_t)PLC_STAGE) {
-                my_loff[q] = e.z;
-                atomicOr(&s_bits[e.z >> 5], 1u << (e.z & 31));
-                atomicMax(&s_nst, min(e.z + e.w, (uint32_t)PLC_STAGE));
-            }
+    // run table from the dense run list (k_count order = sample order): the run's absolute sample
+    // position is its (brick, scan) cell (absolute after k_compact) + its rank; staged runs are a
+    // prefix of the list, so a staged run's list index is its staging rank
+    for (uint32_t j = threadIdx.x; j < nruns; j += PLC_THREADS) {
+        const uint4 e = bt[j];
+        const uint32_t slot = e.w >> 16, n = e.w & 0xFFFFu;
+        s_base[slot] = e.x != NO_PAIR ? T.cell[(size_t)e.x * T.cell_stride + t] + e.y : NO_PAIR;
+        // runs starting past the staging capacity are stored directly (0xFFFF: not staged)
+        const bool stg = e.z < (uint32_t)PLC_STAGE;
+        s_loff[slot] = stg ? (uint16_t)e.z : (uint16_t)0xFFFFu;
+        if (stg) {
+            s_ord[j] = (uint16_t)slot;
+            atomicOr(&s_bits[e.z >> 5], 1u << (e.z & 31));
+            atomicMax(&s_nst, min(e.z + n, (uint32_t)PLC_STAGE));
         }
     }
     __syncthreads();
@@ -591,13 +597,6 @@ __global__ __launch_bounds__(PLC_THREADS) void k_place(const float* __restrict__
         }
     }
     __syncthreads();
-#pragma unroll
-    for (int q = 0; q < SLOTS_PT; q++) {  // staged runs in staging order (read after the walk)
-        const uint32_t lo = my_loff[q];
-        if (lo != 0xFFFFu)
-            s_ord[s_wpre[lo >> 5] + __popc(s_bits[lo >> 5] & ((1u << (lo & 31)) - 1u))] =
-                (uint16_t)(threadIdx.x + q * PLC_THREADS);
-    }
 #ifdef TSDF_ABLATE_PL_NOWALK
     if (ok && r.px == 1e30f) {
 #else

@@ -4,7 +4,7 @@
 set -e
 OUT=${1:-gpurun_out/ablate}
 mkdir -p "$OUT"
-for v in ${VARIANTS:-real PLACE_NOWRITE INT_NOATOM INT_NOFUSE}; do
+for v in ${VARIANTS:-real PL_NOWALK PL_NOCOPY CNT_NOWALK INT_NOP1 INT_NOP3 INT_NOP4}; do
   lib=""
   [ "$v" != real ] && lib="noetic-slam_amd/lib/ablate/libtsdf_hip_$v.so"
   TSDF_HIP_LIB=$lib timeout -k 10 300 python3 bench.py --steps ${STEPS:-16} --warmup 2 --no-cpu > "$OUT/$v.json"
