@@ -415,6 +415,11 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
     c->R.max_weight = p->max_weight;
     c->R.bg = p->semantics == TSDF_SEM_VOXBLOX ? 0.0f : c->R.tau;
     c->R.tau_m_vs = c->R.tau - c->R.vs;
+    {
+        const double band = p->space_carving ? (p->max_range + p->sdf_trunc) / p->voxel_size
+                                             : 2.0 * p->sdf_trunc / p->voxel_size;
+        c->R.band_vox = (int)std::min(std::ceil(band) + 4.0, (double)(VOX_LIMIT / 2));
+    }
 
     // Points one batch may hold: max_batch full scans, unless the per-ray worst cases (pair slots,
     // sample slots — large with space carving) exceed the u32 index space or the sample budget;

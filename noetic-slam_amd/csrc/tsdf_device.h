@@ -68,6 +68,7 @@ struct RayConst {
     float max_weight;
     float bg;        // background distance of unobserved voxels: tau (VDBFusion) or 0 (Voxblox)
     float tau_m_vs;  // tau - vs (Voxblox dropoff denominator)
+    int band_vox;    // bound on any axis' index span of a ray's walk (+ margin), in voxels
     // squared-distance bounds bracketing tau by 2^-20 relative: d2 < tau2_lo implies
     // sqrt_rn(d2) < tau, d2 > tau2_hi implies sqrt_rn(d2) > tau (voxel_gate skips the sqrt)
     float tau2_lo, tau2_hi;

@@ -27,6 +27,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "tsdf_device.h"
 #include "tsdf_ray.h"
 
@@ -130,25 +132,32 @@ __global__ __launch_bounds__(CNT_THREADS) void k_count(const float* __restrict__
             if (ok) {
 #endif
                 uint64_t cur = EMPTY_KEY;
-                uint32_t ccount = 0;
-                for (int it = 0; it < MAX_DDA_STEPS; it++) {
-                    if (Walk<SEM>::gate(R, ox, oy, oz, r)) {
-                        const uint64_t key = brick_key_of(r.vx, r.vy, r.vz);
-                        if (key != cur) {
-                            if (cur != EMPTY_KEY) {
-                                q0 = np == 0 ? cur : q0; n0 = np == 0 ? ccount : n0;
-                                q1 = np == 1 ? cur : q1; n1 = np == 1 ? ccount : n1;
-                                q2 = np == 2 ? cur : q2; n2 = np == 2 ? ccount : n2;
-                                q3 = np == 3 ? cur : q3; n3 = np == 3 ? ccount : n3;
-                                np++;
+                uint32_t curc = ~0u, ccount = 0;
+                // a pair boundary is a brick-code change (32-bit); the full key is built per pair
+                auto walk = [&](auto chk) {
+                    for (int it = 0; it < MAX_DDA_STEPS; it++) {
+                        if (Walk<SEM>::gate(R, ox, oy, oz, r, decltype(chk)::value)) {
+                            const uint32_t bc = brick_code_of(r.vx, r.vy, r.vz);
+                            if (bc != curc) {
+                                if (cur != EMPTY_KEY) {
+                                    q0 = np == 0 ? cur : q0; n0 = np == 0 ? ccount : n0;
+                                    q1 = np == 1 ? cur : q1; n1 = np == 1 ? ccount : n1;
+                                    q2 = np == 2 ? cur : q2; n2 = np == 2 ? ccount : n2;
+                                    q3 = np == 3 ? cur : q3; n3 = np == 3 ? ccount : n3;
+                                    np++;
+                                }
+                                cur = brick_key_of(r.vx, r.vy, r.vz);
+                                curc = bc;
+                                ccount = 0;
                             }
-                            cur = key;
-                            ccount = 0;
+                            ccount++;
                         }
-                        ccount++;
+                        if (!Walk<SEM>::step(r)) break;
                     }
-                    if (!Walk<SEM>::step(r)) break;
-                }
+                };
+                // rays far from the index-domain edge (all, in practice) skip the per-voxel check
+                if (__all(Walk<SEM>::inside(R, r))) walk(std::false_type{});
+                else walk(std::true_type{});
                 if (cur != EMPTY_KEY) {
                     q0 = np == 0 ? cur : q0; n0 = np == 0 ? ccount : n0;
                     q1 = np == 1 ? cur : q1; n1 = np == 1 ? ccount : n1;
@@ -175,7 +184,7 @@ __global__ __launch_bounds__(CNT_THREADS) void k_count(const float* __restrict__
         } else {
             if (ok) {
                 uint64_t cur = EMPTY_KEY;
-                uint32_t ccount = 0;
+                uint32_t curc = ~0u, ccount = 0;
                 auto emit = [&](uint64_t bkey, uint32_t cnt_in) {
                     if (k >= maxp) {
                         atomicOr(&G->overflow, OVF_PAIRS);
@@ -185,10 +194,11 @@ __global__ __launch_bounds__(CNT_THREADS) void k_count(const float* __restrict__
                 };
                 for (int it = 0; it < MAX_DDA_STEPS; it++) {
                     if (Walk<SEM>::gate(R, ox, oy, oz, r)) {
-                        const uint64_t key = brick_key_of(r.vx, r.vy, r.vz);
-                        if (key != cur) {
+                        const uint32_t bc = brick_code_of(r.vx, r.vy, r.vz);
+                        if (bc != curc) {
                             if (cur != EMPTY_KEY) emit(cur, ccount);
-                            cur = key;
+                            cur = brick_key_of(r.vx, r.vy, r.vz);
+                            curc = bc;
                             ccount = 0;
                         }
                         ccount++;
@@ -648,17 +658,18 @@ __global__ __launch_bounds__(PLC_THREADS) void k_place(const float* __restrict__
             resolve_q(code.z, P2, Q2);
             resolve_q(code.w, P3, Q3);
         }
-        uint64_t cur = EMPTY_KEY;
+        uint32_t cur = ~0u;  // brick code of the current pair
         // current pair: global position, or staging position (lpos < PLC_STAGE)
         uint32_t k = 0, pos = NO_PAIR, lpos = NO_PAIR, cnt = 0, w = 0;
         if (fast) {
             // Branch-free walk: lanes are at different steps of different pairs, so every
             // data-dependent branch here would run for the whole wave; selects cost less.
             uint32_t lq = 0xFFFFu;  // current pair's (staging position | count << 16)
+            auto walk = [&](auto chk) {
             for (int it = 0; it < MAX_DDA_STEPS; it++) {
                 float s;
-                const bool g = Walk<SEM>::sample_sel(R, ox, oy, oz, r, s);
-                const uint64_t key = brick_key_of(r.vx, r.vy, r.vz);
+                const bool g = Walk<SEM>::sample_sel(R, ox, oy, oz, r, s, decltype(chk)::value);
+                const uint32_t key = brick_code_of(r.vx, r.vy, r.vz);
                 const bool nb = g && key != cur;  // the ray's next pair, in k_count's order
                 cur = nb ? key : cur;
                 // take the head of the ray's pair queue (P0, L0, N0) and shift the queue: plain
@@ -687,11 +698,14 @@ __global__ __launch_bounds__(PLC_THREADS) void k_place(const float* __restrict__
                 w += g ? 1u : 0u;
                 if (!Walk<SEM>::step(r)) break;
             }
+            };
+            if (__all(Walk<SEM>::inside(R, r))) walk(std::false_type{});
+            else walk(std::true_type{});
         } else
         for (int it = 0; it < MAX_DDA_STEPS; it++) {
             float s;
             if (Walk<SEM>::sample(R, ox, oy, oz, r, s)) {
-                const uint64_t key = brick_key_of(r.vx, r.vy, r.vz);
+                const uint32_t key = brick_code_of(r.vx, r.vy, r.vz);
                 if (key != cur) {  // the ray's next pair, in k_count's order
                     cur = key;
                     resolve(k < maxp ? pc[k] : NO_PAIR, pos, lpos, cnt);

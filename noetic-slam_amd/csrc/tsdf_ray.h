@@ -69,8 +69,8 @@ __device__ __forceinline__ bool ray_init(const RayConst& R, float ox, float oy, 
 
 // ComputeSDF at the current voxel; true (and the truncated sample) when it passes sdf > -tau.
 __device__ __forceinline__ bool voxel_sample(const RayConst& R, float ox, float oy, float oz,
-                                             const RayState& r, float& s) {
-    if (!(r.vx > -VOX_LIMIT && r.vx < VOX_LIMIT && r.vy > -VOX_LIMIT && r.vy < VOX_LIMIT &&
+                                             const RayState& r, float& s, bool check = true) {
+    if (check && !(r.vx > -VOX_LIMIT && r.vx < VOX_LIMIT && r.vy > -VOX_LIMIT && r.vy < VOX_LIMIT &&
           r.vz > -VOX_LIMIT && r.vz < VOX_LIMIT))
         return false;
     const float cx = ((float)r.vx + 0.5f) * R.vs;
@@ -90,9 +90,9 @@ __device__ __forceinline__ bool voxel_sample(const RayConst& R, float ox, float 
 // voxel_sample without early exits (same fp32 ops, same verdict and sample): for walks whose lanes
 // diverge, where straight-line selects beat branches.
 __device__ __forceinline__ bool voxel_sample_sel(const RayConst& R, float ox, float oy, float oz,
-                                                 const RayState& r, float& s) {
-    const bool inl = r.vx > -VOX_LIMIT && r.vx < VOX_LIMIT && r.vy > -VOX_LIMIT &&
-                     r.vy < VOX_LIMIT && r.vz > -VOX_LIMIT && r.vz < VOX_LIMIT;
+                                                 const RayState& r, float& s, bool check = true) {
+    const bool inl = !check || (r.vx > -VOX_LIMIT && r.vx < VOX_LIMIT && r.vy > -VOX_LIMIT &&
+                                r.vy < VOX_LIMIT && r.vz > -VOX_LIMIT && r.vz < VOX_LIMIT);
     const float cx = ((float)r.vx + 0.5f) * R.vs;
     const float cy = ((float)r.vy + 0.5f) * R.vs;
     const float cz = ((float)r.vz + 0.5f) * R.vs;
@@ -109,8 +109,8 @@ __device__ __forceinline__ bool voxel_sample_sel(const RayConst& R, float ox, fl
 // projection; a voxel in front of the hit (proj > 0) always passes, and behind it the sqrt is only
 // evaluated when d2 lies within 2^-20 of tau^2, so the result equals voxel_sample's bit for bit.
 __device__ __forceinline__ bool voxel_gate(const RayConst& R, float ox, float oy, float oz,
-                                           const RayState& r) {
-    if (!(r.vx > -VOX_LIMIT && r.vx < VOX_LIMIT && r.vy > -VOX_LIMIT && r.vy < VOX_LIMIT &&
+                                           const RayState& r, bool check = true) {
+    if (check && !(r.vx > -VOX_LIMIT && r.vx < VOX_LIMIT && r.vy > -VOX_LIMIT && r.vy < VOX_LIMIT &&
           r.vz > -VOX_LIMIT && r.vz < VOX_LIMIT))
         return false;
     const float cx = ((float)r.vx + 0.5f) * R.vs;
@@ -233,9 +233,9 @@ __device__ __forceinline__ float vb_weight(const RayConst& R, float sdf) {
 
 // computeDistance at the current voxel (projective sdf, untruncated); true when its weight is kept
 __device__ __forceinline__ bool vb_sample(const RayConst& R, float ox, float oy, float oz,
-                                          const VbState& r, float& s) {
-    const bool inl = r.vx > -VOX_LIMIT && r.vx < VOX_LIMIT && r.vy > -VOX_LIMIT &&
-                     r.vy < VOX_LIMIT && r.vz > -VOX_LIMIT && r.vz < VOX_LIMIT;
+                                          const VbState& r, float& s, bool check = true) {
+    const bool inl = !check || (r.vx > -VOX_LIMIT && r.vx < VOX_LIMIT && r.vy > -VOX_LIMIT &&
+                                r.vy < VOX_LIMIT && r.vz > -VOX_LIMIT && r.vz < VOX_LIMIT);
     const float cx = ((float)r.vx + 0.5f) * R.vs;
     const float cy = ((float)r.vy + 0.5f) * R.vs;
     const float cz = ((float)r.vz + 0.5f) * R.vs;
@@ -276,16 +276,22 @@ struct Walk<0> {  // TSDF_SEM_VDBFUSION
         return ray_init(R, ox, oy, oz, px, py, pz, r);
     }
     __device__ static __forceinline__ bool gate(const RayConst& R, float ox, float oy, float oz,
-                                                const State& r) {
-        return voxel_gate(R, ox, oy, oz, r);
+                                                const State& r, bool check = true) {
+        return voxel_gate(R, ox, oy, oz, r, check);
     }
     __device__ static __forceinline__ bool sample(const RayConst& R, float ox, float oy, float oz,
-                                                  const State& r, float& s) {
-        return voxel_sample(R, ox, oy, oz, r, s);
+                                                  const State& r, float& s, bool check = true) {
+        return voxel_sample(R, ox, oy, oz, r, s, check);
     }
     __device__ static __forceinline__ bool sample_sel(const RayConst& R, float ox, float oy,
-                                                      float oz, const State& r, float& s) {
-        return voxel_sample_sel(R, ox, oy, oz, r, s);
+                                                      float oz, const State& r, float& s,
+                                                      bool check = true) {
+        return voxel_sample_sel(R, ox, oy, oz, r, s, check);
+    }
+    // the ray's voxels all lie inside |index| < VOX_LIMIT (so the per-voxel check can go)
+    __device__ static __forceinline__ bool inside(const RayConst& R, const State& r) {
+        const int m = max(max(abs(r.vx), abs(r.vy)), abs(r.vz));
+        return m < VOX_LIMIT - R.band_vox;
     }
     __device__ static __forceinline__ bool step(State& r) { return ray_step(r); }
 };
@@ -298,17 +304,22 @@ struct Walk<1> {  // TSDF_SEM_VOXBLOX
         return vb_init(R, ox, oy, oz, px, py, pz, r);
     }
     __device__ static __forceinline__ bool gate(const RayConst& R, float ox, float oy, float oz,
-                                                const State& r) {
+                                                const State& r, bool check = true) {
         float s;
-        return vb_sample(R, ox, oy, oz, r, s);
+        return vb_sample(R, ox, oy, oz, r, s, check);
     }
     __device__ static __forceinline__ bool sample(const RayConst& R, float ox, float oy, float oz,
-                                                  const State& r, float& s) {
-        return vb_sample(R, ox, oy, oz, r, s);
+                                                  const State& r, float& s, bool check = true) {
+        return vb_sample(R, ox, oy, oz, r, s, check);
     }
     __device__ static __forceinline__ bool sample_sel(const RayConst& R, float ox, float oy,
-                                                      float oz, const State& r, float& s) {
-        return vb_sample(R, ox, oy, oz, r, s);
+                                                      float oz, const State& r, float& s,
+                                                      bool check = true) {
+        return vb_sample(R, ox, oy, oz, r, s, check);
+    }
+    __device__ static __forceinline__ bool inside(const RayConst& R, const State& r) {
+        const int m = max(max(abs(r.vx), abs(r.vy)), abs(r.vz));
+        return m < VOX_LIMIT - R.band_vox;
     }
     __device__ static __forceinline__ bool step(State& r) { return vb_step(r); }
 };
@@ -320,6 +331,14 @@ __device__ __forceinline__ uint64_t pack_brick(int bx, int by, int bz) {
 
 __device__ __forceinline__ uint64_t brick_key_of(int vx, int vy, int vz) {
     return pack_brick(vx >> 3, vy >> 3, vz >> 3);
+}
+
+// A ray's brick, truncated to 10 bits per axis: consecutive gated voxels of a ray lie in the same
+// or adjacent bricks (a monotone line, gated voxels contiguous up to isolated skips), so equal
+// codes mean the same brick; a pair boundary is a code change (one 32-bit compare per voxel).
+__device__ __forceinline__ uint32_t brick_code_of(int vx, int vy, int vz) {
+    return ((uint32_t)(vx >> 3) & 1023u) | (((uint32_t)(vy >> 3) & 1023u) << 10) |
+           (((uint32_t)(vz >> 3) & 1023u) << 20);
 }
 
 __device__ __forceinline__ uint64_t mix64(uint64_t k) {
