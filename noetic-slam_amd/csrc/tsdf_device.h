@@ -37,8 +37,14 @@ constexpr int BRICK_COORD_BIAS = 1 << 20;
 constexpr int VOX_LIMIT = 1 << 23;  // |voxel index| < 2^23 on every axis (same as the oracle)
 constexpr int MAX_DDA_STEPS = 1 << 20;
 constexpr int MAX_BATCH = 64;          // scans per batch
-constexpr int RPB = 1024;              // rays per k_count / k_place block (one scan per block)
-constexpr int HCAP = 2048;             // LDS brick-hash slots per k_count block (~300-800 used)
+#ifndef TSDF_RPB
+#define TSDF_RPB 1024
+#endif
+#ifndef TSDF_HCAP
+#define TSDF_HCAP 2048
+#endif
+constexpr int RPB = TSDF_RPB;          // rays per k_count / k_place block (one scan per block)
+constexpr int HCAP = TSDF_HCAP;        // LDS brick-hash slots per k_count block (~300-800 used)
 constexpr int LDS_PROBES = 64;         // probe limit before a pair takes the global fallback
 constexpr int MAX_IN_BRICK = 22;       // a line visits at most 8+8+8-2 voxels of an 8^3 brick
 

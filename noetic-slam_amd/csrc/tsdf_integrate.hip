@@ -208,12 +208,16 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchDesc D, Table T,
                 const uint32_t v0 = m0 ? 1u : 0u, v1 = m1 ? 1u : 0u;
                 dirty |= v0 | (v1 << 1);
                 const uint32_t x = (c0 + c1) | ((v0 + v1) << 16);
+#ifdef TSDF_SHFL_SCAN
                 uint32_t incl = x;
 #pragma unroll
                 for (int d = 1; d < 64; d <<= 1) {
                     const uint32_t y = __shfl_up(incl, d, 64);
                     if (lane >= d) incl += y;
                 }
+#else
+                const uint32_t incl = wave_incl_scan(x);
+#endif
                 if (lane == 63) s_red[wid] = incl;
                 __syncthreads();
                 uint32_t off = 0, tot = 0;

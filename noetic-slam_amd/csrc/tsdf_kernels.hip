@@ -535,7 +535,10 @@ __global__ __launch_bounds__(CMP_THREADS) void k_compact_write(uint32_t n_scans,
 // past the staging capacity, and fallback pairs, are stored directly.
 
 constexpr int PLC_THREADS = RPB;      // one ray per lane
-constexpr int PLC_STAGE = 10112;      // staged samples per workgroup (6 B each; 2 workgroups per CU)
+#ifndef TSDF_PLC_STAGE
+#define TSDF_PLC_STAGE 10112
+#endif
+constexpr int PLC_STAGE = TSDF_PLC_STAGE;  // staged samples per workgroup (6 B each; 2 workgroups per CU)
 
 template <int SEM>
 __global__ __launch_bounds__(PLC_THREADS) void k_place(const float* __restrict__ xyz, BatchDesc D,

@@ -380,6 +380,18 @@ __device__ __forceinline__ int64_t table_find(const Table& T, uint64_t key) {
     return -1;
 }
 
+// Inclusive prefix sum over a wave's 64 lanes in DPP (row shifts 1/2/4/8 scan each 16-lane row,
+// row broadcasts 15/31 carry the row totals): six VALU ops instead of six ds_bpermute round trips.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return x;
+}
+
 template <typename Tv>
 __device__ __forceinline__ Tv wave_sum(Tv v) {
 #pragma unroll
