@@ -232,12 +232,8 @@ __global__ __launch_bounds__(CNT_THREADS) void k_count(const float* __restrict__
     {
         const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
         const unsigned long long x = (unsigned long long)run_sum | ((unsigned long long)run_cnt << 32);
-        unsigned long long incl = x;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const unsigned long long y = __shfl_up(incl, d, 64);
-            if (lane >= d) incl += y;
-        }
+        const unsigned long long incl = (unsigned long long)wave_incl_scan(run_sum) |
+                                        ((unsigned long long)wave_incl_scan(run_cnt) << 32);
         if (lane == 63) s_wsum[wid] = incl;
         __syncthreads();
         unsigned long long ex = incl - x, tot = 0;
@@ -328,12 +324,7 @@ template <int NT>
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t* s_w, uint32_t* total) {
     constexpr int NW = NT / 64;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    uint32_t v = x;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(v, d, 64);
-        if (lane >= d) v += y;
-    }
+    const uint32_t v = wave_incl_scan(x);
     if (lane == 63) s_w[wid] = v;
     __syncthreads();
     uint32_t off = 0, tot = 0;
@@ -509,12 +500,8 @@ __global__ __launch_bounds__(CMP_THREADS) void k_compact_write(uint32_t n_scans,
         uint4* cp = reinterpret_cast<uint4*>(T.cell + (size_t)s_h[k] * T.cell_stride);
         uint4 v = li < nq ? cp[li] : make_uint4(0u, 0u, 0u, 0u);
         const uint32_t s4 = v.x + v.y + v.z + v.w;
-        uint32_t incl = s4;
-#pragma unroll
-        for (int d = 1; d < CMP_GROUP; d <<= 1) {
-            const uint32_t y = __shfl_up(incl, d, CMP_GROUP);
-            if ((int)li >= d) incl += y;
-        }
+        static_assert(CMP_GROUP == 16, "a cell row is one 16-lane DPP row");
+        const uint32_t incl = row16_incl_scan(s4);
         uint32_t p = s_n[k] + incl - s4;
         const uint32_t x0 = v.x, x1 = v.y, x2 = v.z;
         v.x = p; p += x0;
@@ -595,12 +582,7 @@ __global__ __launch_bounds__(PLC_THREADS) void k_place(const float* __restrict__
             cnt[q] = wd < PLC_WORDS ? (uint32_t)__popc(s_bits[wd]) : 0u;
             sum += cnt[q];
         }
-        uint32_t incl = sum;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t y = __shfl_up(incl, d, 64);
-            if ((int)threadIdx.x >= d) incl += y;
-        }
+        const uint32_t incl = wave_incl_scan(sum);
         uint32_t pre = incl - sum;
 #pragma unroll
         for (int q = 0; q < WPL; q++) {

@@ -112,12 +112,7 @@ __global__ __launch_bounds__(MESH_THREADS) void k_mesh_emit(Table T, Pool Pl,
         const int k = mesh_case(s_S, s_ok, l, S);
         const uint32_t nt = k >= 0 ? c_mc[k][0] : 0u;
         // exclusive scan of the lanes' triangle counts (cube order)
-        uint32_t incl = nt;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t y = __shfl_up(incl, d, 64);
-            if (lane >= d) incl += y;
-        }
+        const uint32_t incl = wave_incl_scan(nt);
         if (lane == 63) s_w[wid] = incl;
         __syncthreads();
         uint32_t off = 0;
