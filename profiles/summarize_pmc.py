@@ -20,7 +20,7 @@ def main(root):
                 k = row.get("Kernel_Name", "")
                 if "tsdf::" not in k:
                     continue
-                name = k.split("tsdf::")[1].split("(")[0]
+                name = k.split("tsdf::")[1].split("(")[0].split("<")[0]
                 vals[name][row["Counter_Name"]].append(float(row["Counter_Value"]))
     out = {}
     for kname in sorted(vals):
