@@ -70,7 +70,10 @@ __device__ __forceinline__ int lds_insert(unsigned long long* s_key, uint64_t ke
 // ------------------------------------------------------------------------------------------------
 // k_count
 
-constexpr int CNT_THREADS = 256;
+#ifndef TSDF_CNT_THREADS
+#define TSDF_CNT_THREADS 256
+#endif
+constexpr int CNT_THREADS = TSDF_CNT_THREADS;
 
 template <int SEM>
 __global__ __launch_bounds__(CNT_THREADS) void k_count(const float* __restrict__ xyz, BatchDesc D,
