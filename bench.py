@@ -42,6 +42,8 @@ def parse():
     ap.add_argument("--pipeline", action="store_true",
                     help="overlap consecutive batches on two HIP streams (tsdf_params.pipeline); "
                          "per-kernel times then include the overlap")
+    ap.add_argument("--semantics", default="vdbfusion", choices=("vdbfusion", "voxblox"),
+                    help="fusion rule (tsdf_params.semantics); the headline metric is vdbfusion")
     ap.add_argument("--no-profile", action="store_true",
                     help="do not record per-kernel HIP events in the timed region")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_r01.json"),
@@ -92,7 +94,7 @@ def main():
 
     vol = HipTSDFVolume(args.voxel, args.trunc, max_points=max(max_pts, 1 << 17),
                         max_bricks=1 << 20, device_id=local, max_batch=min(args.batch, 64),
-                        pipeline=args.pipeline)
+                        pipeline=args.pipeline, semantics=args.semantics)
 
     def run_step(i):
         x, offs, org = steps[i]
@@ -177,7 +179,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import oracle
-        ov = oracle.OracleTSDFVolume(args.voxel, args.trunc)
+        ov = oracle.OracleTSDFVolume(args.voxel, args.trunc, semantics=args.semantics)
         n_done, tc, busy = 0, time.perf_counter(), 0.0
         for i in range(args.warmup, n_steps):  # the timed steps' scans, in order, until the budget
             x, offs, org = steps[i]
@@ -215,6 +217,7 @@ def main():
                        "scans_per_step": scans_per_step, "global_batch": scans_per_step,
                        "points_per_scan": int(round(rays_per_scan * world)),
                     "scans_per_gpu_batch": args.batch, "pipelined_batches": args.pipeline,
+                       "semantics": args.semantics,
                        "parallelism": "azimuth-sector x%d" % world if world > 1 else "single"},
             "roofline": roofline,
             "cpu_baseline": cpu,
