@@ -281,9 +281,16 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchDesc D, Table T,
             if (q1 < n) load_chunk(q1);
             __syncthreads();
             PHASE(5);
+#ifndef TSDF_FUSE_P4A
+            // VDBFusion: the chains convert their raw cells themselves, two steps ahead of use
+            // (off the chain's critical path), so there is no conversion pass and no barrier
+            constexpr bool inline_cvt = SEM == 0;
+#else
+            constexpr bool inline_cvt = false;
+#endif
             // P4a: convert every live cell to (A 2^-32, B) in f32, in parallel, so the serial
             // per-voxel chains below are one LDS read, a multiply-add and a division per step
-            {
+            if constexpr (!inline_cvt) {
                 const uint32_t ncell = s_ncell;
                 for (uint32_t j = tid; j < ncell; j += INT_THREADS) {
                     const long long av = (long long)cA[j];
@@ -294,7 +301,7 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchDesc D, Table T,
                         cF[j] = make_float2(af, (float)cB[j]);
                 }
             }
-            __syncthreads();
+            if constexpr (!inline_cvt) __syncthreads();
             PHASE(8);
             // P4b: fuse.  Lane tid takes live voxels tid, tid + 256 and runs each one's chain in scan
             // order; the next cell is read from LDS while the current step divides, so a step costs
@@ -311,6 +318,37 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchDesc D, Table T,
                     const uint32_t rem = MASK_POPC(sMask[l]);
                     sMask[l] = 0;
                     float s = sS[l], wt = sW[l];
+                    if constexpr (inline_cvt) {
+                        typedef const volatile __attribute__((address_space(3))) uint64_t lds_u64r;
+                        typedef const volatile __attribute__((address_space(3))) uint32_t lds_u32r;
+                        lds_u64r* rA = (lds_u64r*)(cA);
+                        lds_u32r* rB = (lds_u32r*)(cB);
+                        uint64_t a0 = rA[cell], a1 = rA[min(cell + 1u, INT_CAP - 1u)];
+                        uint32_t b0 = rB[cell], b1 = rB[min(cell + 1u, INT_CAP - 1u)];
+                        for (uint32_t k = 0; k < rem; k += 2) {
+                            const uint64_t na0 = rA[min(cell + k + 2, INT_CAP - 1u)];
+                            const uint32_t nb0 = rB[min(cell + k + 2, INT_CAP - 1u)];
+                            const uint64_t na1 = rA[min(cell + k + 3, INT_CAP - 1u)];
+                            const uint32_t nb1 = rB[min(cell + k + 3, INT_CAP - 1u)];
+                            const float fa0 = (float)((double)(long long)a0 * (1.0 / 4294967296.0));
+                            const float fa1 = (float)((double)(long long)a1 * (1.0 / 4294967296.0));
+                            float nwt = wt + (float)b0;
+                            s = (s * wt + fa0) / nwt;
+                            wt = nwt;
+                            nwt = wt + (float)b1;
+                            const float s2 = (s * wt + fa1) / nwt;
+                            const bool more = k + 1 < rem;
+                            s = more ? s2 : s;
+                            wt = more ? nwt : wt;
+                            a0 = na0;
+                            a1 = na1;
+                            b0 = nb0;
+                            b1 = nb1;
+                        }
+                        sS[l] = s;
+                        sW[l] = wt;
+                        continue;
+                    }
                     // two cells in flight: a step's operand was read one step earlier
                     float2 va = cF[cell], vb = cF[min(cell + 1u, INT_CAP - 1u)];
                     // branch-free body (one basic block, so the reads stay ahead of their use);
