@@ -189,6 +189,9 @@ static int launch(tsdf_ctx* c, const float* d_xyz, BatchDesc& D) {
         if (tm) tm->end(KIND_COUNT, st);
         if (tm) tm->begin(KIND_COMPACT, st);
         HIPCHK(c, launch_compact(D, T, W, c->G, par, st));
+#ifndef TSDF_NO_ORDER
+        HIPCHK(c, launch_order(W, c->G, par, st));
+#endif
         if (tm) tm->end(KIND_COMPACT, st);
     }
     HIPCHK(c, hipEventRecord(c->ev_compact[par], st));
@@ -200,7 +203,13 @@ static int launch(tsdf_ctx* c, const float* d_xyz, BatchDesc& D) {
     if (c->batch_id > 0) HIPCHK(c, hipStreamWaitEvent(st, c->ev_integ[par ^ 1], 0));
     if (D.n_blocks) {
         if (tm) tm->begin(KIND_INTEGRATE, st);
+#ifndef TSDF_NO_ORDER
+        Work Wi = W;
+        Wi.active = W.active_ord;  // largest bricks first (k_order)
+        HIPCHK(c, launch_integrate(D, c->R, T, Wi, c->Pl, c->G, par, st));
+#else
         HIPCHK(c, launch_integrate(D, c->R, T, W, c->Pl, c->G, par, st));
+#endif
         if (tm) tm->end(KIND_INTEGRATE, st);
     }
     HIPCHK(c, launch_finish(c->G, par, st));
@@ -365,7 +374,8 @@ void tsdf_destroy(tsdf_ctx* c) {
                    c->T.brick_keys,  c->Pl.sdf,          c->Pl.weight,     c->G,
                    c->cell2[0],      c->cell2[1],        c->stage2[0],     c->stage2[1],
                    c->W2[0].pair,    c->W2[0].blk,       c->W2[0].blk_n, c->W2[0].fb,
-                   c->W2[0].smp,     c->W2[0].active,    c->W2[1].pair,    c->W2[1].blk,
+                   c->W2[0].smp,     c->W2[0].active,  c->W2[0].active_ord, c->W2[1].active_ord,
+                   c->W2[0].ord_hist, c->W2[1].ord_hist,    c->W2[1].pair,    c->W2[1].blk,
                    c->W2[1].blk_n, c->W2[1].fb,        c->W2[1].smp,     c->W2[1].active,
                    c->W2[0].cagg,    c->W2[1].cagg};
     for (void* d : dev)
@@ -469,6 +479,8 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
         HIPCHK(c, hipMalloc(&W.fb, (size_t)W.max_fb * sizeof(uint4)));
         HIPCHK(c, hipMalloc(&W.smp, (size_t)W.max_smp * sizeof(uint2)));
         HIPCHK(c, hipMalloc(&W.active, (size_t)W.max_active * sizeof(uint4)));
+        HIPCHK(c, hipMalloc(&W.active_ord, (size_t)W.max_active * sizeof(uint4)));
+        HIPCHK(c, hipMalloc(&W.ord_hist, 64 * 32 * sizeof(uint32_t)));
         HIPCHK(c, hipMalloc(&W.cagg, compact_chunks(c->cap) * 2 * sizeof(uint4)));
         HIPCHK(c, hipMalloc(&c->cell2[q], c->cap * c->T.cell_stride * sizeof(uint32_t)));
         HIPCHK(c, hipMemsetAsync(c->cell2[q], 0, c->cap * c->T.cell_stride * sizeof(uint32_t),

@@ -115,6 +115,8 @@ struct Work {
     uint4* fb;       // fallback pairs: (tidx, scan, rank, 0)
     uint2* smp;  // x = truncated sdf (f32 bits), y = scan << 9 | local voxel
     uint4* active;  // (h, slot, toff, cnt) per active brick (k_compact)
+    uint4* active_ord;  // the same records, largest size class first (k_order; k_integrate's list)
+    uint32_t* ord_hist; // k_order: per (slice, size class) counts, then first positions
     uint4* cagg;    // k_compact: per table chunk (touched bricks, samples, new bricks), then bases
     uint32_t maxp;        // pair slots per ray
     uint32_t max_active;  // capacity of `active`
@@ -166,6 +168,8 @@ hipError_t launch_compact(const BatchDesc& D, const Table& T, const Work& Wk, Gl
 hipError_t launch_place(const float* d_xyz, const BatchDesc& D, const RayConst& R, const Table& T,
                         const Work& Wk, hipStream_t st);
 hipError_t launch_finish(Globals* G, int parity, hipStream_t st);
+// Orders the batch's active bricks by size class, largest first (k_integrate's load balance).
+hipError_t launch_order(const Work& Wk, Globals* G, int parity, hipStream_t st);
 hipError_t launch_integrate(const BatchDesc& D, const RayConst& R, const Table& T, const Work& Wk,
                             const Pool& Pl, Globals* G, int parity, hipStream_t st);
 hipError_t launch_query_dense(const Table& T, const Pool& Pl, const int lo[3], const int dims[3],

@@ -98,6 +98,7 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchDesc D, Table T,
     uint32_t nvox = 0, ndirty = 0, par = 0;
 #ifdef TSDF_PHASE_TIMING
     unsigned long long ph[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, t_last = clock64();
+    const unsigned long long t_first = __builtin_amdgcn_s_memrealtime();
     uint32_t nb = 0, nwin = 0;
 #endif
     // Software pipeline over the workgroup's bricks: while brick a is processed, brick a + G's
@@ -419,7 +420,14 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchDesc D, Table T,
         __syncthreads();  // write-back reads of sS / sW done before the next brick stages its own
     }
 #ifdef TSDF_PHASE_TIMING
+#ifdef TSDF_PHASE_ALL
+    if (tid == 0)
+        printf("wg %u bricks %u total %llu start %llu\n", blockIdx.x, nb,
+               ph[0] + ph[1] + ph[2] + ph[3] + ph[4] + ph[5] + ph[6] + ph[7] + ph[8], t_first);
+    if (false)
+#else
     if (tid == 0 && (blockIdx.x % 97) == 0)
+#endif
         printf("phase blk %u bricks %u windows %u meta %llu bar0 %llu load %llu mask %llu scan %llu "
                "acc %llu conv %llu fuse %llu tail %llu\n", blockIdx.x, nb, nwin, ph[0], ph[1], ph[2],
                ph[3], ph[4], ph[5], ph[8], ph[6], ph[7]);

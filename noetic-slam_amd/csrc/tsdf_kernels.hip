@@ -852,6 +852,92 @@ hipError_t launch_place(const float* d_xyz, const BatchDesc& D, const RayConst& 
     return hipGetLastError();
 }
 
+// ------------------------------------------------------------------------------------------------
+// k_order: k_integrate hands its workgroups bricks in list order (grid stride), and bricks hold
+// from a few to ~40 k samples, so a random order leaves the kernel waiting on the workgroups that
+// drew several large bricks.  A counting sort by size class (floor(log2(samples)), largest class
+// first) deals the large bricks out first and evenly (greedy largest-first).  Order inside a class
+// is whatever the atomics give: each brick is fused independently, so the field does not depend
+// on it.
+
+constexpr int ORD_THREADS = 256;
+constexpr int ORD_BLOCKS = 64;  // each takes a contiguous slice of the active list
+constexpr int ORD_CLASSES = 32;
+
+__device__ __forceinline__ uint32_t size_class(uint32_t n) {
+    return (uint32_t)__clz(max(n, 1u));  // 31 - floor(log2 n): large bricks -> small index
+}
+
+__device__ __forceinline__ void ord_slice(uint32_t n_active, uint32_t b, uint32_t& i0,
+                                          uint32_t& i1) {
+    const uint32_t per = (n_active + ORD_BLOCKS - 1) / ORD_BLOCKS;
+    i0 = min(n_active, b * per);
+    i1 = min(n_active, i0 + per);
+}
+
+// pass 1: per-slice class histogram (LDS), written out without global atomics
+__global__ __launch_bounds__(ORD_THREADS) void k_order_hist(Work Wk, Globals* G, int parity) {
+    __shared__ uint32_t h[ORD_CLASSES];
+    if (threadIdx.x < ORD_CLASSES) h[threadIdx.x] = 0u;
+    __syncthreads();
+    uint32_t i0, i1;
+    ord_slice(min(G->ctr[parity].n_active, Wk.max_active), blockIdx.x, i0, i1);
+    for (uint32_t i = i0 + threadIdx.x; i < i1; i += ORD_THREADS)
+        atomicAdd(&h[size_class(Wk.active[i].w)], 1u);
+    __syncthreads();
+    if (threadIdx.x < ORD_CLASSES) Wk.ord_hist[blockIdx.x * ORD_CLASSES + threadIdx.x] = h[threadIdx.x];
+}
+
+// pass 2 (one workgroup): slice s's first position in class k = all records of larger classes +
+// class k's records in the slices before s
+__global__ __launch_bounds__(ORD_BLOCKS * ORD_CLASSES / 2) void k_order_scan(Work Wk) {
+    constexpr int NT = ORD_BLOCKS * ORD_CLASSES / 2;  // two (slice, class) entries per thread
+    __shared__ uint32_t tot[ORD_CLASSES];
+    __shared__ uint32_t cls_base[ORD_CLASSES];
+    const int t = threadIdx.x;
+    if (t < ORD_CLASSES) {
+        uint32_t sum = 0;  // class t over all slices
+        for (int b = 0; b < ORD_BLOCKS; b++) sum += Wk.ord_hist[b * ORD_CLASSES + t];
+        tot[t] = sum;
+    }
+    __syncthreads();
+    if (t < 64) {
+        const uint32_t v = t < ORD_CLASSES ? tot[t] : 0u;
+        const uint32_t incl = wave_incl_scan(v);
+        if (t < ORD_CLASSES) cls_base[t] = incl - v;
+    }
+    __syncthreads();
+    if (t < ORD_CLASSES) {  // running prefix over the slices of class t
+        uint32_t run = cls_base[t];
+        for (int b = 0; b < ORD_BLOCKS; b++) {
+            const uint32_t v = Wk.ord_hist[b * ORD_CLASSES + t];
+            Wk.ord_hist[b * ORD_CLASSES + t] = run;
+            run += v;
+        }
+    }
+    (void)NT;
+}
+
+// pass 3: every record to its class position (rank inside a slice's class from LDS atomics)
+__global__ __launch_bounds__(ORD_THREADS) void k_order_scatter(Work Wk, Globals* G, int parity) {
+    __shared__ uint32_t base[ORD_CLASSES];
+    if (threadIdx.x < ORD_CLASSES) base[threadIdx.x] = Wk.ord_hist[blockIdx.x * ORD_CLASSES + threadIdx.x];
+    __syncthreads();
+    uint32_t i0, i1;
+    ord_slice(min(G->ctr[parity].n_active, Wk.max_active), blockIdx.x, i0, i1);
+    for (uint32_t i = i0 + threadIdx.x; i < i1; i += ORD_THREADS) {
+        const uint4 r = Wk.active[i];
+        Wk.active_ord[atomicAdd(&base[size_class(r.w)], 1u)] = r;
+    }
+}
+
+hipError_t launch_order(const Work& Wk, Globals* G, int parity, hipStream_t st) {
+    k_order_hist<<<ORD_BLOCKS, ORD_THREADS, 0, st>>>(Wk, G, parity);
+    k_order_scan<<<1, ORD_BLOCKS * ORD_CLASSES / 2, 0, st>>>(Wk);
+    k_order_scatter<<<ORD_BLOCKS, ORD_THREADS, 0, st>>>(Wk, G, parity);
+    return hipGetLastError();
+}
+
 // End of a batch: keep its counters as the "last batch" snapshot and zero them for the next batch
 // of the same parity (the same stream, so ordered after every reader of this batch).
 __global__ void k_finish(Globals* G, int parity) {
