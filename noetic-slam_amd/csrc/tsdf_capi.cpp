@@ -474,8 +474,8 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
         Work& W = c->W2[q];
         W = c->Wk;  // capacities
         HIPCHK(c, hipMalloc(&W.pair, slots * sizeof(uint32_t)));
-        HIPCHK(c, hipMalloc(&W.blk, (size_t)c->max_blocks * HCAP * sizeof(uint4)));
-        HIPCHK(c, hipMalloc(&W.blk_n, (size_t)c->max_blocks * sizeof(uint32_t)));
+        HIPCHK(c, hipMalloc(&W.blk, (size_t)c->max_blocks * 2 * HCAP * sizeof(uint4)));
+        HIPCHK(c, hipMalloc(&W.blk_n, (size_t)c->max_blocks * 2 * sizeof(uint32_t)));
         HIPCHK(c, hipMalloc(&W.fb, (size_t)W.max_fb * sizeof(uint4)));
         HIPCHK(c, hipMalloc(&W.smp, (size_t)W.max_smp * sizeof(uint2)));
         HIPCHK(c, hipMalloc(&W.active, (size_t)W.max_active * sizeof(uint4)));

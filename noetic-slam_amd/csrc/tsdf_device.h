@@ -108,10 +108,10 @@ struct Pool {
 
 struct Work {
     uint32_t* pair;
-    uint4* blk;      // n_blocks * HCAP: per k_count workgroup its DENSE run list (table index,
+    uint4* blk;      // n_blocks * 2 * HCAP: per k_count workgroup and half its DENSE run list (table index,
                      // rank in the (brick, scan) cell,
                      // run offset in the workgroup's sample order, run samples | LDS slot << 16)
-    uint32_t* blk_n; // n_blocks: runs in the list
+    uint32_t* blk_n; // n_blocks * 2: runs in each list
     uint4* fb;       // fallback pairs: (tidx, scan, rank, 0)
     uint2* smp;  // x = truncated sdf (f32 bits), y = scan << 9 | local voxel
     uint4* active;  // (h, slot, toff, cnt) per active brick (k_compact)

@@ -83,6 +83,7 @@ __global__ __launch_bounds__(CNT_THREADS) void k_count(const float* __restrict__
     __shared__ uint32_t s_cnt[HCAP];
     __shared__ unsigned long long red[2][CNT_THREADS / 64];
     __shared__ unsigned long long s_wsum[CNT_THREADS / 64];
+    __shared__ uint32_t s_wcnt[CNT_THREADS / 64];
     Counters* C = &G->ctr[parity];  // zeroed by the previous batch of this parity (k_finish)
     for (int j = threadIdx.x; j < HCAP; j += CNT_THREADS) {
         s_key[j] = EMPTY_KEY;
@@ -96,10 +97,14 @@ __global__ __launch_bounds__(CNT_THREADS) void k_count(const float* __restrict__
     uint32_t valid = 0, npairs = 0;
     // The pair code of (ray, brick run): LDS-hash rank in the workgroup's run for the brick, or a
     // fallback record when the LDS hash is full.  cnt_in = the pair's gated voxels (<= MAX_IN_BRICK).
-    auto pair_code = [&](uint64_t bkey, uint32_t cnt_in) -> uint32_t {
+    // A run's samples are counted per half workgroup (rays [0, RPB/2) and [RPB/2, RPB): k_place
+    // runs one 512-lane workgroup per half), packed in s_cnt as n0 | n1 << 16 (a run holds at
+    // most RPB/2 * MAX_IN_BRICK samples per half); the pair's rank is within its half's sub-run.
+    auto pair_code = [&](uint64_t bkey, uint32_t cnt_in, uint32_t half) -> uint32_t {
         const int lid = lds_insert(s_key, bkey);
-        if (lid >= 0) {  // s_cnt: the run's samples; the pair's offset in it
-            const uint32_t lr = atomicAdd(&s_cnt[lid], cnt_in);
+        if (lid >= 0) {
+            const uint32_t old = atomicAdd(&s_cnt[lid], half ? cnt_in << 16 : cnt_in);
+            const uint32_t lr = half ? old >> 16 : old & 0xFFFFu;
             return (cnt_in << PAIR_CNT_SHIFT) | ((uint32_t)lid << PAIR_LID_SHIFT) | lr;
         }
         const uint32_t f = atomicAdd(&C->n_fb, 1u);  // LDS hash full: the global path
@@ -172,10 +177,11 @@ __global__ __launch_bounds__(CNT_THREADS) void k_count(const float* __restrict__
             if (np > maxp) atomicOr(&G->overflow, OVF_PAIRS);  // beyond the geometric bound
             k = min(np, maxp);
             uint4 code = make_uint4(NO_PAIR, NO_PAIR, NO_PAIR, NO_PAIR);
-            if (k > 0) code.x = pair_code(q0, n0);
-            if (k > 1) code.y = pair_code(q1, n1);
-            if (k > 2) code.z = pair_code(q2, n2);
-            if (k > 3) code.w = pair_code(q3, n3);
+            const uint32_t hf = i - r0 >= (uint32_t)(RPB / 2) ? 1u : 0u;
+            if (k > 0) code.x = pair_code(q0, n0, hf);
+            if (k > 1) code.y = pair_code(q1, n1, hf);
+            if (k > 2) code.z = pair_code(q2, n2, hf);
+            if (k > 3) code.w = pair_code(q3, n3, hf);
             if (maxp == 4) {
                 *reinterpret_cast<uint4*>(pc) = code;  // one 16-B store per ray
             } else {
@@ -193,7 +199,7 @@ __global__ __launch_bounds__(CNT_THREADS) void k_count(const float* __restrict__
                         atomicOr(&G->overflow, OVF_PAIRS);
                         return;
                     }
-                    pc[k++] = pair_code(bkey, cnt_in);
+                    pc[k++] = pair_code(bkey, cnt_in, i - r0 >= (uint32_t)(RPB / 2) ? 1u : 0u);
                 };
                 for (int it = 0; it < MAX_DDA_STEPS; it++) {
                     if (Walk<SEM>::gate(R, ox, oy, oz, r)) {
@@ -222,31 +228,42 @@ __global__ __launch_bounds__(CNT_THREADS) void k_count(const float* __restrict__
     // every run its offset in the workgroup's sample order (k_place stages the samples in that
     // order) and its index in the workgroup's DENSE run list (slot order = sample order).
     constexpr int SPT = HCAP / CNT_THREADS;
-    uint4* bt = Wk.blk + (size_t)blockIdx.x * HCAP;
-    uint32_t run_sum = 0, run_cnt = 0;
+    // two dense run lists per workgroup, one per half (k_place workgroup 2 b + half)
+    uint4* bt0 = Wk.blk + (size_t)blockIdx.x * 2 * HCAP;
+    uint4* bt1 = bt0 + HCAP;
+    uint32_t n0s = 0, n1s = 0, c01 = 0;
 #pragma unroll
     for (int j = 0; j < SPT; j++) {
         const int slot = threadIdx.x * SPT + j;
-        const bool occ = s_key[slot] != EMPTY_KEY;
-        run_sum += occ ? s_cnt[slot] : 0u;
-        run_cnt += occ ? 1u : 0u;
+        const uint32_t c = s_key[slot] != EMPTY_KEY ? s_cnt[slot] : 0u;
+        n0s += c & 0xFFFFu;
+        n1s += c >> 16;
+        c01 += ((c & 0xFFFFu) ? 1u : 0u) | ((c >> 16) ? 1u << 16 : 0u);
     }
-    uint32_t run_off, run_idx;
+    uint32_t off0, off1, idx0, idx1;
     {
         const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-        const unsigned long long x = (unsigned long long)run_sum | ((unsigned long long)run_cnt << 32);
-        const unsigned long long incl = (unsigned long long)wave_incl_scan(run_sum) |
-                                        ((unsigned long long)wave_incl_scan(run_cnt) << 32);
-        if (lane == 63) s_wsum[wid] = incl;
+        const uint32_t i0 = wave_incl_scan(n0s), i1 = wave_incl_scan(n1s), ic = wave_incl_scan(c01);
+        if (lane == 63) {
+            s_wsum[wid] = (unsigned long long)i0 | ((unsigned long long)i1 << 32);
+            s_wcnt[wid] = ic;
+        }
         __syncthreads();
-        unsigned long long ex = incl - x, tot = 0;
+        unsigned long long ex = 0;
+        uint32_t exc = 0, totc = 0;
         for (int w = 0; w < CNT_THREADS / 64; w++) {
             ex += w < wid ? s_wsum[w] : 0ull;
-            tot += s_wsum[w];
+            exc += w < wid ? s_wcnt[w] : 0u;
+            totc += s_wcnt[w];
         }
-        run_off = (uint32_t)ex;
-        run_idx = (uint32_t)(ex >> 32);
-        if (threadIdx.x == CNT_THREADS - 1) Wk.blk_n[blockIdx.x] = (uint32_t)(tot >> 32);
+        off0 = (uint32_t)ex + (i0 - n0s);
+        off1 = (uint32_t)(ex >> 32) + (i1 - n1s);
+        idx0 = (exc & 0xFFFFu) + ((ic - c01) & 0xFFFFu);
+        idx1 = (exc >> 16) + ((ic - c01) >> 16);
+        if (threadIdx.x == CNT_THREADS - 1) {
+            Wk.blk_n[2 * blockIdx.x] = totc & 0xFFFFu;
+            Wk.blk_n[2 * blockIdx.x + 1] = totc >> 16;
+        }
     }
     // The thread's SPT slots go to the global table in three batched stages, so their round trips
     // overlap instead of running one slot after another: (1) first-probe loads of all keys,
@@ -271,27 +288,35 @@ __global__ __launch_bounds__(CNT_THREADS) void k_count(const float* __restrict__
 #pragma unroll
     for (int j = 0; j < SPT; j++) {
         const int slot = threadIdx.x * SPT + j;
-        old[j] = hx[j] >= 0 ? atomicAdd(&T.cell[(size_t)hx[j] * T.cell_stride + t], s_cnt[slot])
-                            : 0u;
+        const uint32_t c = s_cnt[slot];
+        old[j] = hx[j] >= 0
+                     ? atomicAdd(&T.cell[(size_t)hx[j] * T.cell_stride + t], (c & 0xFFFFu) + (c >> 16))
+                     : 0u;
     }
-    // dense run list: (table index | NO_PAIR, rank in the (brick, scan) cell, run offset in the
-    // workgroup's sample order, run samples | slot << 16)
-    static_assert(RPB * MAX_IN_BRICK < (1 << 16) && HCAP <= (1 << 16), "run record packing");
+    // dense run lists: (table index | NO_PAIR, rank in the (brick, scan) cell, run offset in the
+    // half's sample order, run samples | slot << 16); the half-1 sub-run follows half 0's
+    static_assert((RPB / 2) * MAX_IN_BRICK < (1 << 16) && HCAP <= (1 << 16), "run record packing");
 #pragma unroll
     for (int j = 0; j < SPT; j++) {
         const int slot = threadIdx.x * SPT + j;
         if (key[j] == EMPTY_KEY) continue;
-        const uint32_t n = s_cnt[slot];
-        uint4 e = make_uint4(NO_PAIR, 0u, run_off, n | ((uint32_t)slot << 16));
+        const uint32_t c = s_cnt[slot], n0 = c & 0xFFFFu, n1 = c >> 16;
+        uint32_t tx = NO_PAIR, rk = 0u;
         if (hx[j] >= 0) {
-            e.x = (uint32_t)hx[j];
-            e.y = old[j];
+            tx = (uint32_t)hx[j];
+            rk = old[j];
             // the brick's first run of this scan marks it (one store per (brick, scan), not one
             // per (workgroup, brick): partial-line stores from every XCD cost HBM writes)
-            if (old[j] == 0u) T.touched[e.x] = 1u;
+            if (old[j] == 0u) T.touched[tx] = 1u;
         }
-        run_off += n;
-        bt[run_idx++] = e;
+        if (n0) {
+            bt0[idx0++] = make_uint4(tx, rk, off0, n0 | ((uint32_t)slot << 16));
+            off0 += n0;
+        }
+        if (n1) {
+            bt1[idx1++] = make_uint4(tx, rk + n0, off1, n1 | ((uint32_t)slot << 16));
+            off1 += n1;
+        }
     }
     // block-reduce the stats, one atomic per block on a shard picked by block index
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -524,11 +549,11 @@ __global__ __launch_bounds__(CMP_THREADS) void k_compact_write(uint32_t n_scans,
 // from k_count's block scan) and then copies each (brick) run out as one contiguous write; samples
 // past the staging capacity, and fallback pairs, are stored directly.
 
-constexpr int PLC_THREADS = RPB;      // one ray per lane
+constexpr int PLC_THREADS = RPB / 2;  // one ray per lane, half a k_count workgroup's rays
 #ifndef TSDF_PLC_STAGE
-#define TSDF_PLC_STAGE 10112
+#define TSDF_PLC_STAGE 3800
 #endif
-constexpr int PLC_STAGE = TSDF_PLC_STAGE;  // staged samples per workgroup (6 B each; 2 workgroups per CU)
+constexpr int PLC_STAGE = TSDF_PLC_STAGE;  // staged samples per workgroup (6 B each; 4 workgroups per CU)
 
 template <int SEM>
 __global__ __launch_bounds__(PLC_THREADS) void k_place(const float* __restrict__ xyz, BatchDesc D,
@@ -542,8 +567,10 @@ __global__ __launch_bounds__(PLC_THREADS) void k_place(const float* __restrict__
     __shared__ float st_s[PLC_STAGE];      // staged samples
     __shared__ uint16_t st_l[PLC_STAGE];
     __shared__ uint32_t s_nst;             // staged samples (end of the last staged run)
+    // workgroup 2 b + hf takes half hf of k_count workgroup b's rays, and that half's run list
     uint32_t t, r0, r1;
-    block_range(D, blockIdx.x, t, r0, r1);
+    block_range(D, blockIdx.x >> 1, t, r0, r1);
+    r0 += (blockIdx.x & 1u) * PLC_THREADS;
     const uint4* bt = Wk.blk + (size_t)blockIdx.x * HCAP;
     const uint32_t nruns = Wk.blk_n[blockIdx.x];
     // the ray's own setup (point loads, divisions) overlaps the run-list loads below
@@ -847,8 +874,8 @@ hipError_t launch_compact(const BatchDesc& D, const Table& T, const Work& Wk, Gl
 
 hipError_t launch_place(const float* d_xyz, const BatchDesc& D, const RayConst& R, const Table& T,
                         const Work& Wk, hipStream_t st) {
-    if (R.sem == 1) k_place<1><<<D.n_blocks, PLC_THREADS, 0, st>>>(d_xyz, D, R, T, Wk);
-    else k_place<0><<<D.n_blocks, PLC_THREADS, 0, st>>>(d_xyz, D, R, T, Wk);
+    if (R.sem == 1) k_place<1><<<2 * D.n_blocks, PLC_THREADS, 0, st>>>(d_xyz, D, R, T, Wk);
+    else k_place<0><<<2 * D.n_blocks, PLC_THREADS, 0, st>>>(d_xyz, D, R, T, Wk);
     return hipGetLastError();
 }
 
