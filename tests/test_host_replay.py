@@ -1,0 +1,92 @@
+"""The C-ABI driven from C++ the way tsdf_map_node drives it (noetic-slam_amd/host/tsdf_replay.cpp:
+one PointCloud2 per scan through tsdf_integrate, then the map write-out through
+tsdf_export_bricks).  On the CPU the same driver is linked against the oracle library, which
+exports the same ABI; on the GPU the shipped binary (linked against libtsdf_hip.so) must write the
+oracle's map bit for bit.
+"""
+import os
+import struct
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle
+from conftest import REPO, decimate
+from tsdf_map import bricks_to_voxels
+
+HOST = os.path.join(REPO, "noetic-slam_amd", "host")
+
+
+def dlio_records(xyz):
+    """dlio::Point records (32 B: x y z 1 | intensity pad t pad; dlio.h:85-106)."""
+    rec = np.zeros((xyz.shape[0], 8), np.float32)
+    rec[:, :3] = xyz
+    rec[:, 3] = 1.0
+    rec[:, 4] = 7.0
+    return rec
+
+
+def write_stream(path, scans):
+    with open(path, "wb") as f:
+        for xyz, org in scans:
+            rec = dlio_records(xyz)
+            f.write(struct.pack("<QIIi3d", rec.shape[0], 32, 0, 0, *[float(v) for v in org]))
+            f.write(rec.tobytes())
+
+
+def read_bricks(path):
+    with open(path, "rb") as f:
+        n = struct.unpack("<Q", f.read(8))[0]
+        coords = np.frombuffer(f.read(12 * n), np.int32).reshape(n, 3)
+        sdf = np.frombuffer(f.read(2048 * n), np.float32).reshape(n, 512)
+        w = np.frombuffer(f.read(2048 * n), np.float32).reshape(n, 512)
+    return coords, sdf, w
+
+
+def scans_for_test(sim):
+    return [(decimate(p, 16), org) for p, org in (sim.scan(k) for k in (0, 1, 5))]
+
+
+def oracle_voxels(scans, **kw):
+    o = oracle.OracleTSDFVolume(0.05, 0.15, **kw)
+    for xyz, org in scans:
+        o.integrate_cloud(dlio_records(xyz).tobytes(), xyz.shape[0], 32, 0, org)
+    return bricks_to_voxels(*o.export_bricks())
+
+
+@pytest.mark.parametrize("semantics", ["vdbfusion", "voxblox"])
+def test_replay_driver_against_oracle_library(tmp_path, sim, semantics):
+    lib = oracle.load()  # builds oracle/build/libtsdf_oracle.so if needed
+    del lib
+    exe = tmp_path / "tsdf_replay_oracle"
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-o", str(exe),
+                           os.path.join(HOST, "tsdf_replay.cpp"),
+                           "-L" + os.path.dirname(oracle.LIB_PATH), "-ltsdf_oracle",
+                           "-Wl,-rpath," + os.path.dirname(oracle.LIB_PATH)])
+    scans = scans_for_test(sim)
+    write_stream(tmp_path / "in.scans", scans)
+    subprocess.check_call([str(exe), str(tmp_path / "in.scans"), str(tmp_path / "out.bricks"),
+                           "0.05", "0.15", semantics])
+    got = bricks_to_voxels(*read_bricks(tmp_path / "out.bricks"))
+    ref = oracle_voxels(scans, semantics=semantics)
+    assert got[0].shape[0] > 1000
+    for a, b in zip(got, ref):
+        assert np.array_equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("semantics", ["vdbfusion", "voxblox"])
+def test_replay_driver_on_gpu_bitwise(tmp_path, sim, semantics):
+    exe = os.path.join(REPO, "noetic-slam_amd", "lib", "tsdf_replay")
+    assert os.path.exists(exe), "run __graft_entry__.build() first"
+    scans = scans_for_test(sim)
+    write_stream(tmp_path / "in.scans", scans)
+    out = subprocess.run([exe, str(tmp_path / "in.scans"), str(tmp_path / "out.bricks"), "0.05",
+                          "0.15", semantics], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    got = bricks_to_voxels(*read_bricks(tmp_path / "out.bricks"))
+    ref = oracle_voxels(scans, semantics=semantics)
+    assert got[0].shape[0] > 1000
+    assert np.array_equal(got[0], ref[0]) and np.array_equal(got[2], ref[2])
+    assert np.array_equal(got[1].view(np.uint32), ref[1].view(np.uint32))
