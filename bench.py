@@ -61,11 +61,21 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and world > 1:
         raise SystemExit("--gpus %d but WORLD_SIZE %d" % (args.gpus, world))
+    # TSDF_BENCH_SHARED_GPU=1 (rehearsal only, never the driver's runs): every rank on device
+    # local % device_count, collectives over gloo on host tensors -- exercises the N-rank path
+    # (sector sharding, max-over-ranks timing, read-out merge) on a one-GPU box
+    shared = os.environ.get("TSDF_BENCH_SHARED_GPU") == "1"
+    if shared:
+        local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    cdev = torch.device("cpu") if shared else dev  # where collective tensors live
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        if shared:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     from tsdf_map import HipTSDFVolume
     from tsdf_map.scan_gen import TorchOusterSim, sector_mask_torch
@@ -121,7 +131,7 @@ def main():
     elapsed = time.perf_counter() - t0
     st = vol.stats()
 
-    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    el = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
@@ -150,11 +160,12 @@ def main():
         t_launch = kernel_ms_per_launch[dom] * 1e-3
         achieved = bytes_per_launch / t_launch / 1e9
         traffic = None
-        try:
-            with open(args.traffic_json) as f:
-                traffic = json.load(f)["bytes_per_launch"].get("k_" + dom)
-        except (OSError, ValueError, KeyError):
-            traffic = None
+        if world == 1:  # the PMC profile is of the one-GPU workload (a rank's launch is smaller)
+            try:
+                with open(args.traffic_json) as f:
+                    traffic = json.load(f)["bytes_per_launch"].get("k_" + dom)
+            except (OSError, ValueError, KeyError):
+                traffic = None
         roofline = {"bound": "hbm", "kernel": "k_" + dom, "achieved": round(achieved, 2),
                     "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 5),
                     "traffic": traffic,
@@ -170,7 +181,7 @@ def main():
         from tsdf_map.distributed import merged_bricks
         dist.barrier()
         tm = time.perf_counter()
-        merged_bricks(vol, device=dev)
+        merged_bricks(vol, device=cdev)
         dist.barrier()
         merge_ms = (time.perf_counter() - tm) * 1e3
 
