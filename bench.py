@@ -42,6 +42,12 @@ def parse():
     ap.add_argument("--pipeline", action="store_true",
                     help="overlap consecutive batches on two HIP streams (tsdf_params.pipeline); "
                          "per-kernel times then include the overlap")
+    ap.add_argument("--sensor", default="os1_128_1024", choices=("os1_128_1024", "os1_128_2048"),
+                    help="beam table of the synthetic scans (os1_128_2048 + --voxel 0.02 --trunc "
+                         "0.06 --hz 20: the C4 workload); the headline metric is os1_128_1024")
+    ap.add_argument("--hz", type=float, default=10.0)
+    ap.add_argument("--max-bricks", type=int, default=1 << 20,
+                    help="brick pool capacity (4 KiB per brick)")
     ap.add_argument("--semantics", default="vdbfusion", choices=("vdbfusion", "voxblox"),
                     help="fusion rule (tsdf_params.semantics); the headline metric is vdbfusion")
     ap.add_argument("--no-profile", action="store_true",
@@ -81,7 +87,7 @@ def main():
     from tsdf_map.scan_gen import TorchOusterSim, sector_mask_torch
 
     # ---- synthesize every scan of every step, this rank's sector, resident in HBM -------------
-    sim = TorchOusterSim(dev)
+    sim = TorchOusterSim(dev, beams=args.sensor, hz=args.hz)
     n_steps = args.warmup + args.steps
     scans_per_step = world * args.batch
     steps = []
@@ -103,7 +109,7 @@ def main():
     max_pts = max(int(np.diff(o).max()) for _, o, _ in steps)
 
     vol = HipTSDFVolume(args.voxel, args.trunc, max_points=max(max_pts, 1 << 17),
-                        max_bricks=1 << 20, device_id=local, max_batch=min(args.batch, 64),
+                        max_bricks=args.max_bricks, device_id=local, max_batch=min(args.batch, 64),
                         pipeline=args.pipeline, semantics=args.semantics)
 
     def run_step(i):
@@ -223,7 +229,11 @@ def main():
             "dtype": "f32",
             "data": "synthetic (OS-1-128 1024x10 beam angles from the reference's metadata "
                     "fixture; analytic scene; resident in HBM)",
-            "config": {"workload": "C1/M1 ouster_os1_128_1024x10_synthetic_5cm",
+            "config": {"workload": ("C1/M1 ouster_os1_128_1024x10_synthetic_5cm"
+                                    if args.sensor == "os1_128_1024" else
+                                    "C4/M4 ouster_%s_synthetic_%gcm_%ghz" % (args.sensor,
+                                                                            args.voxel * 100,
+                                                                            args.hz)),
                        "voxel_size_m": args.voxel, "sdf_trunc_m": args.trunc,
                        "scans_per_step": scans_per_step, "global_batch": scans_per_step,
                        "points_per_scan": int(round(rays_per_scan * world)),
