@@ -549,6 +549,9 @@ __global__ __launch_bounds__(CMP_THREADS) void k_compact_write(uint32_t n_scans,
 // from k_count's block scan) and then copies each (brick) run out as one contiguous write; samples
 // past the staging capacity, and fallback pairs, are stored directly.
 
+#ifdef TSDF_ABLATE_PHASE  // `make ablate ABLATE=PHASE`
+#define TSDF_PLC_PHASE
+#endif
 constexpr int PLC_THREADS = RPB / 2;  // one ray per lane, half a k_count workgroup's rays
 #ifndef TSDF_PLC_STAGE
 #define TSDF_PLC_STAGE 3800
@@ -567,32 +570,51 @@ __global__ __launch_bounds__(PLC_THREADS) void k_place(const float* __restrict__
     __shared__ float st_s[PLC_STAGE];      // staged samples
     __shared__ uint16_t st_l[PLC_STAGE];
     __shared__ uint32_t s_nst;             // staged samples (end of the last staged run)
+#ifdef TSDF_PLC_PHASE  // diagnostic build: thread 0's clock at the phase boundaries
+    unsigned long long pt[6];
+    if (threadIdx.x == 0) pt[0] = clock64();
+#endif
     // workgroup 2 b + hf takes half hf of k_count workgroup b's rays, and that half's run list
     uint32_t t, r0, r1;
     block_range(D, blockIdx.x >> 1, t, r0, r1);
     r0 += (blockIdx.x & 1u) * PLC_THREADS;
     const uint4* bt = Wk.blk + (size_t)blockIdx.x * HCAP;
-    const uint32_t nruns = Wk.blk_n[blockIdx.x];
-    // the ray's own setup (point loads, divisions) overlaps the run-list loads below
-    const float ox = D.ox[t], oy = D.oy[t], oz = D.oz[t];
     const uint32_t maxp = Wk.maxp;
     const uint32_t i = r0 + threadIdx.x;
-    typename Walk<SEM>::State r;
-    const bool ok = i < r1 && Walk<SEM>::init(R, ox, oy, oz, xyz[3 * (size_t)i], xyz[3 * (size_t)i + 1],
-                                       xyz[3 * (size_t)i + 2], r);
-    const uint32_t* pc = Wk.pair + (size_t)i * maxp;
+    // Every independent global load is issued first, so the prologue waits two memory round trips
+    // (list entry -> its cell) instead of four (point -> pair codes, list -> cell): the ray's point
+    // and pair codes, the list length, and each lane's first list entry.
+    float px = 0.0f, py = 0.0f, pz = 0.0f;
     uint4 code4 = make_uint4(NO_PAIR, NO_PAIR, NO_PAIR, NO_PAIR);
-    if (ok && maxp == 4) code4 = *reinterpret_cast<const uint4*>(pc);
+    const uint32_t* pc = Wk.pair + (size_t)i * maxp;
+    if (i < r1) {
+        px = xyz[3 * (size_t)i];
+        py = xyz[3 * (size_t)i + 1];
+        pz = xyz[3 * (size_t)i + 2];
+        if (maxp == 4) code4 = *reinterpret_cast<const uint4*>(pc);
+    }
+    const uint32_t nruns = Wk.blk_n[blockIdx.x];
+    static_assert(PLC_THREADS <= HCAP, "a lane's first list entry lies inside the list");
+    const uint4 e0 = bt[threadIdx.x];
+    // a run's absolute sample position is its (brick, scan) cell (absolute after k_compact) + its
+    // rank
+    const uint32_t base0 = (threadIdx.x < nruns && e0.x != NO_PAIR)
+                               ? T.cell[(size_t)e0.x * T.cell_stride + t] + e0.y
+                               : NO_PAIR;
+    const float ox = D.ox[t], oy = D.oy[t], oz = D.oz[t];
+    typename Walk<SEM>::State r;
+    const bool ok = i < r1 && Walk<SEM>::init(R, ox, oy, oz, px, py, pz, r);
     for (int j = threadIdx.x; j < PLC_WORDS; j += PLC_THREADS) s_bits[j] = 0u;
     if (threadIdx.x == 0) s_nst = 0u;
     __syncthreads();
-    // run table from the dense run list (k_count order = sample order): the run's absolute sample
-    // position is its (brick, scan) cell (absolute after k_compact) + its rank; staged runs are a
-    // prefix of the list, so a staged run's list index is its staging rank
-    for (uint32_t j = threadIdx.x; j < nruns; j += PLC_THREADS) {
-        const uint4 e = bt[j];
+#ifdef TSDF_PLC_PHASE
+    if (threadIdx.x == 0) pt[1] = clock64();
+#endif
+    // run table from the dense run list (k_count order = sample order); staged runs are a prefix
+    // of the list, so a staged run's list index is its staging rank
+    auto fill = [&](uint32_t j, const uint4& e, uint32_t base) {
         const uint32_t slot = e.w >> 16, n = e.w & 0xFFFFu;
-        s_base[slot] = e.x != NO_PAIR ? T.cell[(size_t)e.x * T.cell_stride + t] + e.y : NO_PAIR;
+        s_base[slot] = base;
         // runs starting past the staging capacity are stored directly (0xFFFF: not staged)
         const bool stg = e.z < (uint32_t)PLC_STAGE;
         s_loff[slot] = stg ? (uint16_t)e.z : (uint16_t)0xFFFFu;
@@ -601,8 +623,16 @@ __global__ __launch_bounds__(PLC_THREADS) void k_place(const float* __restrict__
             atomicOr(&s_bits[e.z >> 5], 1u << (e.z & 31));
             atomicMax(&s_nst, min(e.z + n, (uint32_t)PLC_STAGE));
         }
+    };
+    if (threadIdx.x < nruns) fill(threadIdx.x, e0, base0);
+    for (uint32_t j = threadIdx.x + PLC_THREADS; j < nruns; j += PLC_THREADS) {
+        const uint4 e = bt[j];
+        fill(j, e, e.x != NO_PAIR ? T.cell[(size_t)e.x * T.cell_stride + t] + e.y : NO_PAIR);
     }
     __syncthreads();
+#ifdef TSDF_PLC_PHASE
+    if (threadIdx.x == 0) pt[2] = clock64();
+#endif
     if (threadIdx.x < 64) {  // exclusive prefix of run starts per bitmap word (one wave)
         constexpr int WPL = (PLC_WORDS + 63) / 64;
         uint32_t cnt[WPL], sum = 0;
@@ -622,6 +652,9 @@ __global__ __launch_bounds__(PLC_THREADS) void k_place(const float* __restrict__
         }
     }
     __syncthreads();
+#ifdef TSDF_PLC_PHASE
+    if (threadIdx.x == 0) pt[3] = clock64();
+#endif
 #ifdef TSDF_ABLATE_PL_NOWALK
     if (ok && r.px == 1e30f) {
 #else
@@ -742,6 +775,9 @@ __global__ __launch_bounds__(PLC_THREADS) void k_place(const float* __restrict__
         }
     }
     __syncthreads();
+#ifdef TSDF_PLC_PHASE
+    if (threadIdx.x == 0) pt[4] = clock64();
+#endif
     // copy-out: one lane per staged sample; its run = the last run start at or before it
 #ifdef TSDF_ABLATE_PL_NOCOPY
     const uint32_t nst = 0;
@@ -759,6 +795,13 @@ __global__ __launch_bounds__(PLC_THREADS) void k_place(const float* __restrict__
                 Wk.smp[dst] = make_uint2(__float_as_uint(st_s[j]), (t << 9) | st_l[j]);
         }
     }
+#ifdef TSDF_PLC_PHASE
+    if (threadIdx.x == 0 && (blockIdx.x % 61) == 0) {
+        pt[5] = clock64();
+        printf("place %u prol0 %llu prol1 %llu prol2 %llu walk %llu copy %llu\n", blockIdx.x,
+               pt[1] - pt[0], pt[2] - pt[1], pt[3] - pt[2], pt[4] - pt[3], pt[5] - pt[4]);
+    }
+#endif
 }
 
 // ------------------------------------------------------------------------------------------------
