@@ -173,14 +173,24 @@ static int launch(tsdf_ctx* c, const float* d_xyz, BatchDesc& D) {
     if (D.n_blocks > c->max_blocks)
         return fail(c, TSDF_EINVAL, "batch needs %u workgroups > %u", D.n_blocks, c->max_blocks);
     const int par = (int)(c->batch_id & 1);
-    hipStream_t st = c->bst[par];
+#ifndef TSDF_TWO_STREAM_SERIAL
+    // serial batches share one stream (stream order replaces the cross-stream waits); pipelined
+    // batches alternate between two
+    const bool cross = c->p.pipeline != 0;
+#else
+    const bool cross = true;
+#endif
+    hipStream_t st = c->bst[cross ? par : 0];
     Table T = c->T;
     T.cell = c->cell2[par];
     const Work& W = c->W2[par];
     EventTimer* tm = c->timer;
-    HIPCHK(c, hipEventRecord(c->ev_main, c->stream));  // staging uploads, imports, ...
-    HIPCHK(c, hipStreamWaitEvent(st, c->ev_main, 0));
-    if (c->batch_id > 0)  // pipelined: after the previous batch's compact; else after all of it
+    // staging uploads, imports, ... (an idle context stream has nothing to order against)
+    if (hipStreamQuery(c->stream) != hipSuccess) {
+        HIPCHK(c, hipEventRecord(c->ev_main, c->stream));
+        HIPCHK(c, hipStreamWaitEvent(st, c->ev_main, 0));
+    }
+    if (c->batch_id > 0 && cross)  // pipelined: after the previous batch's compact; else after all of it
         HIPCHK(c, hipStreamWaitEvent(st, c->p.pipeline ? c->ev_compact[par ^ 1]
                                                        : c->ev_integ[par ^ 1], 0));
     if (D.n_blocks) {
@@ -200,7 +210,7 @@ static int launch(tsdf_ctx* c, const float* d_xyz, BatchDesc& D) {
         HIPCHK(c, launch_place(d_xyz, D, c->R, T, W, st));
         if (tm) tm->end(KIND_PLACE, st);
     }
-    if (c->batch_id > 0) HIPCHK(c, hipStreamWaitEvent(st, c->ev_integ[par ^ 1], 0));
+    if (c->batch_id > 0 && cross) HIPCHK(c, hipStreamWaitEvent(st, c->ev_integ[par ^ 1], 0));
     if (D.n_blocks) {
         if (tm) tm->begin(KIND_INTEGRATE, st);
 #ifndef TSDF_NO_ORDER
