@@ -49,9 +49,6 @@ constexpr uint32_t INT_MAX_WIN = TSDF_INT_WIN;       // scans per window (mask b
 #ifdef TSDF_ABLATE_PHASE  // `make ablate ABLATE=PHASE`
 #define TSDF_PHASE_TIMING
 #endif
-#ifdef TSDF_ABLATE_PHASE  // `make ablate ABLATE=PHASE`
-#define TSDF_PHASE_TIMING
-#endif
 // Diagnostic build only (-DTSDF_PHASE_TIMING, never shipped): thread 0 of a few workgroups reads
 // the clock at each phase boundary (no counter drain: outstanding loads stay in flight) and
 // prints the cycles spent per phase.
