@@ -40,6 +40,8 @@ def load():
         lib = _abi.declare(C.CDLL(LIB_PATH), optional=HOST_ONLY)
         lib.tsdf_oracle_set_mode.restype = C.c_int
         lib.tsdf_oracle_set_mode.argtypes = [C.c_void_p, C.c_int]
+        lib.tsdf_oracle_set_threads.restype = C.c_int
+        lib.tsdf_oracle_set_threads.argtypes = [C.c_void_p, C.c_int]
         lib.tsdf_oracle_num_voxels.restype = C.c_uint64
         lib.tsdf_oracle_num_voxels.argtypes = [C.c_void_p]
         lib.tsdf_oracle_export_voxels.restype = C.c_int
@@ -55,9 +57,12 @@ def load():
 class OracleTSDFVolume(TSDFVolume):
     """The CPU restatement behind the same host interface as HipTSDFVolume."""
 
-    def __init__(self, voxel_size, sdf_trunc, space_carving=False, mode=MODE_SCAN_FUSED, **kw):
+    def __init__(self, voxel_size, sdf_trunc, space_carving=False, mode=MODE_SCAN_FUSED, threads=1,
+                 **kw):
         super().__init__(load(), voxel_size, sdf_trunc, space_carving, **kw)
         self._check(self._lib.tsdf_oracle_set_mode(self._ctx, mode), "set_mode")
+        # threads > 1: the partitioned multi-threaded scan-fused mode (same field, bit for bit)
+        self._check(self._lib.tsdf_oracle_set_threads(self._ctx, int(threads)), "set_threads")
 
     def export_voxels(self):
         n = int(self._lib.tsdf_oracle_num_voxels(self._ctx))

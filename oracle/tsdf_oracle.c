@@ -75,7 +75,16 @@ struct tsdf_ctx {
     int mode;
     tsdf_stats st;
     char err[256];
+    /* multi-threaded scan-fused mode (tsdf_oracle_set_threads, n_thr > 1): the field is split into
+     * n_thr partitions by brick hash, each a full context of its own (sub[p]); tab is then only a
+     * read-out snapshot, rebuilt from the partitions when mt_dirty */
+    int n_thr, mt_dirty;
+    struct tsdf_ctx** sub;
+    struct mt_bucket* bk; /* n_thr x n_thr: samples of ray-thread t for partition p at [t n_thr + p] */
 };
+
+typedef struct { int32_t x, y, z; float s, w; } mt_sample;
+struct mt_bucket { mt_sample* v; uint64_t n, cap; };
 
 static uint64_t mix3(int32_t x, int32_t y, int32_t z) {
     uint64_t h = (uint64_t)(uint32_t)x * 0x9E3779B97F4A7C15ull;
@@ -198,6 +207,12 @@ int tsdf_create(const tsdf_params* params, tsdf_ctx** out) {
 
 void tsdf_destroy(tsdf_ctx* c) {
     if (!c) return;
+    if (c->sub)
+        for (int p = 0; p < c->n_thr; p++) tsdf_destroy(c->sub[p]);
+    if (c->bk)
+        for (int k = 0; k < c->n_thr * c->n_thr; k++) free(c->bk[k].v);
+    free(c->sub);
+    free(c->bk);
     free(c->tab);
     free(c->touched);
     free(c);
@@ -208,6 +223,7 @@ const char* tsdf_last_error(const tsdf_ctx* c) { return c ? c->err : "null conte
 int tsdf_oracle_set_mode(tsdf_ctx* c, int mode) {
     if (!c || (mode != ORACLE_MODE_SCAN_FUSED && mode != ORACLE_MODE_SEQUENTIAL))
         return TSDF_EINVAL;
+    if (c->n_thr > 1 && mode != ORACLE_MODE_SCAN_FUSED) return TSDF_EINVAL;
     c->mode = mode;
     return TSDF_OK;
 }
@@ -467,6 +483,147 @@ static void fuse_scan(tsdf_ctx* c) {
     c->n_touched = 0;
 }
 
+/* ---- multi-threaded scan-fused mode (the CPU baseline's multi-core leg) ------
+ * Bit-identical to the serial scan-fused mode: a voxel's scan update is an exact integer sum
+ * (order-free) followed by one fuse per scan, and every voxel lives in exactly one partition.
+ *   phase 1  threads walk contiguous ray ranges and bucket each gated sample by its brick's
+ *            partition (hash of the 8^3 brick coordinates);
+ *   phase 2  thread p accumulates partition p's samples into its own context and fuses them. */
+#include <pthread.h>
+
+typedef struct {
+    tsdf_ctx* c;
+    int t;
+    const char* base;
+    uint64_t i0, i1;
+    uint32_t point_step, xyz_offset;
+    int32_t xyz_is_f64;
+    float ox, oy, oz;
+    uint64_t rays;
+    int fail;
+} mt_job;
+
+static void mt_point(const char* q, int32_t f64, float* px, float* py, float* pz) {
+    if (f64) {
+        double d[3];
+        memcpy(d, q, sizeof d);
+        *px = (float)d[0]; *py = (float)d[1]; *pz = (float)d[2];
+    } else {
+        float f[3];
+        memcpy(f, q, sizeof f);
+        *px = f[0]; *py = f[1]; *pz = f[2];
+    }
+}
+
+static void visit_bucket(tsdf_ctx* c, int32_t x, int32_t y, int32_t z, float s, float w,
+                         void* user) {
+    mt_job* j = (mt_job*)user;
+    const int T = c->n_thr;
+    /* floor division by the brick side (arithmetic shift) */
+    const int p = (int)(mix3(x >> 3, y >> 3, z >> 3) % (uint64_t)T);
+    struct mt_bucket* b = &c->bk[j->t * T + p];
+    if (b->n == b->cap) {
+        const uint64_t nc = b->cap ? 2 * b->cap : 4096;
+        mt_sample* v = (mt_sample*)realloc(b->v, nc * sizeof(mt_sample));
+        if (!v) { j->fail = 1; return; }
+        b->v = v;
+        b->cap = nc;
+    }
+    b->v[b->n++] = (mt_sample){x, y, z, s, w};
+}
+
+static void* mt_walk(void* arg) {
+    mt_job* j = (mt_job*)arg;
+    tsdf_ctx* c = j->c;
+    for (uint64_t i = j->i0; i < j->i1 && !j->fail; i++) {
+        float px, py, pz;
+        mt_point(j->base + i * j->point_step + j->xyz_offset, j->xyz_is_f64, &px, &py, &pz);
+        const int64_t r = c->sem == TSDF_SEM_VOXBLOX
+                              ? walk_ray_vb(c, px, py, pz, j->ox, j->oy, j->oz, visit_bucket, j)
+                              : walk_ray(c, px, py, pz, j->ox, j->oy, j->oz, visit_bucket, j);
+        if (r >= 0) j->rays++;
+    }
+    return NULL;
+}
+
+static void* mt_fuse(void* arg) {
+    mt_job* j = (mt_job*)arg;
+    tsdf_ctx* c = j->c;
+    const int T = c->n_thr, p = j->t;
+    tsdf_ctx* sc = c->sub[p];
+    sc->scan_id = c->scan_id;
+    sc->st.n_voxels_last = 0;
+    for (int t = 0; t < T && !j->fail; t++) {
+        struct mt_bucket* b = &c->bk[t * T + p];
+        for (uint64_t k = 0; k < b->n && !j->fail; k++)
+            visit_accum(sc, b->v[k].x, b->v[k].y, b->v[k].z, b->v[k].s, b->v[k].w, &j->fail);
+        b->n = 0;
+    }
+    fuse_scan(sc);
+    return NULL;
+}
+
+static int mt_integrate(tsdf_ctx* c, const char* base, uint64_t n, uint32_t point_step,
+                        uint32_t xyz_offset, int32_t xyz_is_f64, float ox, float oy, float oz) {
+    const int T = c->n_thr;
+    mt_job job[64];
+    pthread_t th[64];
+    for (int phase = 0; phase < 2; phase++) {
+        for (int t = 0; t < T; t++) {
+            job[t] = (mt_job){c, t, base, n * (uint64_t)t / T, n * (uint64_t)(t + 1) / T,
+                              point_step, xyz_offset, xyz_is_f64, ox, oy, oz, 0, 0};
+            if (pthread_create(&th[t], NULL, phase ? mt_fuse : mt_walk, &job[t])) {
+                for (int k = 0; k < t; k++) pthread_join(th[k], NULL);
+                return set_err(c, TSDF_ENOMEM, "oracle thread creation failed");
+            }
+        }
+        int fail = 0;
+        for (int t = 0; t < T; t++) {
+            pthread_join(th[t], NULL);
+            fail |= job[t].fail;
+            if (phase == 0) c->st.n_rays_total += job[t].rays;
+            else c->st.n_voxels_last += c->sub[t]->st.n_voxels_last;
+        }
+        if (fail) return set_err(c, TSDF_ENOMEM, "oracle allocation failed");
+    }
+    c->mt_dirty = 1;
+    return TSDF_OK;
+}
+
+/* tab <- the union of the partitions (read-outs of the multi-threaded mode) */
+static void mt_collect(const tsdf_ctx* cc) {
+    tsdf_ctx* c = (tsdf_ctx*)cc;
+    if (c->n_thr <= 1 || !c->mt_dirty) return;
+    if (c->cap) memset(c->tab, 0, c->cap * sizeof(vox_t));
+    c->n = 0;
+    for (int p = 0; p < c->n_thr; p++) {
+        const tsdf_ctx* sc = c->sub[p];
+        for (uint64_t i = 0; i < sc->cap; i++) {
+            if (!sc->tab[i].used) continue;
+            const int64_t h = vox_get(c, sc->tab[i].x, sc->tab[i].y, sc->tab[i].z);
+            if (h < 0) return;
+            c->tab[h].S = sc->tab[i].S;
+            c->tab[h].W = sc->tab[i].W;
+        }
+    }
+    c->mt_dirty = 0;
+}
+
+/* n >= 1 threads; n > 1 selects the partitioned scan-fused mode (before the first scan only) */
+int tsdf_oracle_set_threads(tsdf_ctx* c, int n) {
+    if (!c || n < 1 || n > 64 || c->n || c->mode != ORACLE_MODE_SCAN_FUSED || c->sub)
+        return TSDF_EINVAL;
+    if (n == 1) return TSDF_OK;
+    c->sub = (tsdf_ctx**)calloc((size_t)n, sizeof(tsdf_ctx*));
+    c->bk = (struct mt_bucket*)calloc((size_t)n * n, sizeof(struct mt_bucket));
+    if (!c->sub || !c->bk) return set_err(c, TSDF_ENOMEM, "oracle allocation failed");
+    c->n_thr = n;
+    for (int p = 0; p < n; p++)
+        if (tsdf_create(&c->p, &c->sub[p]) != TSDF_OK)
+            return set_err(c, TSDF_ENOMEM, "oracle allocation failed");
+    return TSDF_OK;
+}
+
 int tsdf_integrate(tsdf_ctx* c, const void* pts, uint64_t n, uint32_t point_step,
                    uint32_t xyz_offset, int32_t xyz_is_f64, const double origin[3]) {
     if (!c || (!pts && n) || !origin) return set_err(c, TSDF_EINVAL, "null argument");
@@ -478,6 +635,14 @@ int tsdf_integrate(tsdf_ctx* c, const void* pts, uint64_t n, uint32_t point_step
     c->st.n_voxels_last = 0;
     int fail = 0;
     const char* base = (const char*)pts;
+    if (c->n_thr > 1) {
+        const int rc = mt_integrate(c, base, n, point_step, xyz_offset, xyz_is_f64, ox, oy, oz);
+        if (rc != TSDF_OK) return rc;
+        c->st.n_scans++;
+        c->st.n_points_in += n;
+        c->st.n_voxels_total += c->st.n_voxels_last;
+        return TSDF_OK;
+    }
     for (uint64_t i = 0; i < n && !fail; i++) {
         const char* q = base + i * point_step + xyz_offset;
         float px, py, pz;
@@ -508,6 +673,7 @@ int tsdf_sync(tsdf_ctx* c) { return c ? TSDF_OK : TSDF_EINVAL; }
 int tsdf_query_dense(tsdf_ctx* c, const int32_t lo[3], const int32_t hi[3], float* sdf,
                      float* weight) {
     if (!c || !lo || !hi) return TSDF_EINVAL;
+    mt_collect(c);
     for (int a = 0; a < 3; a++)
         if (hi[a] < lo[a]) return set_err(c, TSDF_EINVAL, "hi < lo");
     uint64_t i = 0;
@@ -538,6 +704,7 @@ static int cmp_brick(const void* a, const void* b) {
 
 /* unique bricks holding at least one voxel with W > 0, sorted by (z, y, x) */
 static brick_ent* list_bricks(const tsdf_ctx* c, uint64_t* nb) {
+    mt_collect(c);
     brick_ent* e = (brick_ent*)malloc((c->n ? c->n : 1) * sizeof(brick_ent));
     if (!e) return NULL;
     uint64_t k = 0;
@@ -589,6 +756,7 @@ int tsdf_export_bricks(tsdf_ctx* c, int32_t* coords, float* sdf, float* weight, 
 int tsdf_import_bricks(tsdf_ctx* c, const int32_t* coords, const float* sdf, const float* weight,
                        uint64_t n) {
     if (!c || (n && (!coords || !sdf || !weight))) return TSDF_EINVAL;
+    if (c->n_thr > 1) return set_err(c, TSDF_EINVAL, "import is not supported in the threaded mode");
     for (uint64_t i = 0; i < n; i++)
         for (int l = 0; l < 512; l++) {
             const float wi = weight[512 * i + l];
@@ -630,6 +798,7 @@ int tsdf_reset_stats(tsdf_ctx* c) {
 
 /* number of voxels with W > 0 */
 uint64_t tsdf_oracle_num_voxels(const tsdf_ctx* c) {
+    mt_collect(c);
     uint64_t k = 0;
     for (uint64_t i = 0; i < c->cap; i++)
         if (c->tab[i].used && c->tab[i].W > 0.0f) k++;
