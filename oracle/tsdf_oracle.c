@@ -611,9 +611,9 @@ static void mt_collect(const tsdf_ctx* cc) {
 
 /* n >= 1 threads; n > 1 selects the partitioned scan-fused mode (before the first scan only) */
 int tsdf_oracle_set_threads(tsdf_ctx* c, int n) {
-    if (!c || n < 1 || n > 64 || c->n || c->mode != ORACLE_MODE_SCAN_FUSED || c->sub)
-        return TSDF_EINVAL;
-    if (n == 1) return TSDF_OK;
+    if (!c || n < 1 || n > 64) return TSDF_EINVAL;
+    if (n == 1 && !c->sub) return TSDF_OK;
+    if (c->n || c->mode != ORACLE_MODE_SCAN_FUSED || c->sub) return TSDF_EINVAL;
     c->sub = (tsdf_ctx**)calloc((size_t)n, sizeof(tsdf_ctx*));
     c->bk = (struct mt_bucket*)calloc((size_t)n * n, sizeof(struct mt_bucket));
     if (!c->sub || !c->bk) return set_err(c, TSDF_ENOMEM, "oracle allocation failed");
