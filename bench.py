@@ -5,9 +5,11 @@ A step integrates one batch of synthetic scans that are already resident in HBM 
 workload of SURVEY.md §8d: OS-1-128 1024x10 beams, analytic scene, circular trajectory at 10 Hz,
 5 cm voxels, 15 cm truncation, no carving), scan after scan, through libtsdf_hip.so's
 tsdf_integrate_batch_device.  Multi-GPU (one process per GPU, torch.distributed over RCCL): every
-rank integrates its azimuth sector of every scan of the step into its own partial field (weak
-scaling: a step of N GPUs holds N * batch scans, each rank's share is `batch` scans' worth of rays);
-no collective runs on the data path — the border-brick merge is a read-out operation, timed
+rank holds every FULL scan of the step and integrates its azimuth sector of each (the sector
+filter runs inside the walk kernels, in the timed region: tsdf_params.n_sectors / sector) into its
+own partial field (weak scaling: a step of N GPUs holds N * batch scans, each rank's share is
+`batch` scans' worth of rays); no collective runs on the data path — the device-resident
+border-brick reduce over RCCL (tsdf_map.distributed.border_reduce) is a read-out operation, timed
 separately (readout_merge_ms).
 
 Prints ONE JSON line on rank 0.
@@ -87,9 +89,9 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
 
     from tsdf_map import HipTSDFVolume
-    from tsdf_map.scan_gen import TorchOusterSim, sector_mask_torch
+    from tsdf_map.scan_gen import TorchOusterSim
 
-    # ---- synthesize every scan of every step, this rank's sector, resident in HBM -------------
+    # ---- synthesize every (full) scan of every step, resident in HBM ----------------------------
     sim = TorchOusterSim(dev, beams=args.sensor, hz=args.hz)
     n_steps = args.warmup + args.steps
     scans_per_step = world * args.batch
@@ -100,8 +102,6 @@ def main():
         for j in range(scans_per_step):
             k = s * scans_per_step + j
             pts, org = sim.scan(k)
-            if world > 1:
-                pts = pts[sector_mask_torch(pts, org, rank, world)]
             parts.append(pts)
             offs.append(offs[-1] + pts.shape[0])
             origins.append(org)
@@ -113,7 +113,8 @@ def main():
 
     vol = HipTSDFVolume(args.voxel, args.trunc, max_points=max(max_pts, 1 << 17),
                         max_bricks=args.max_bricks, device_id=local, max_batch=min(args.batch, 64),
-                        pipeline=args.pipeline, semantics=args.semantics)
+                        pipeline=args.pipeline, semantics=args.semantics,
+                        n_sectors=world, sector=rank)  # this rank's azimuth sector of every scan
 
     def run_step(i):
         x, offs, org = steps[i]
@@ -185,12 +186,12 @@ def main():
     path_ms_per_scan = sum(kernel_ms_per_launch.values()) * n_batches / n_scans_rank
 
     # ---- read-out merge of border bricks (not in the timed region) ----------------------------
-    merge_ms = None
+    merge_ms = merge_info = None
     if world > 1:
-        from tsdf_map.distributed import merged_bricks
+        from tsdf_map.distributed import border_reduce
         dist.barrier()
         tm = time.perf_counter()
-        merged_bricks(vol, device=cdev)
+        merge_info = border_reduce(vol, comm_device=cdev)
         dist.barrier()
         merge_ms = (time.perf_counter() - tm) * 1e3
 
@@ -225,6 +226,7 @@ def main():
         n_mt, t_mt = oracle_leg(threads)
         n_1, t_1 = oracle_leg(1)
         cpu = {"value": round(n_mt / t_mt, 4), "unit": "scans/s", "cores": threads, "kind": "port",
+               "host_nproc": os.cpu_count(), "affinity_cpus": share,
                "sample": "the first %d scans of the timed steps (%.1f s), C oracle in its partitioned "
                          "multi-threaded scan-fused mode (%d threads), same inputs"
                          % (n_mt, t_mt, threads),
@@ -257,7 +259,8 @@ def main():
                        "points_per_scan": int(round(rays_per_scan * world)),
                     "scans_per_gpu_batch": args.batch, "pipelined_batches": args.pipeline,
                        "semantics": args.semantics,
-                       "parallelism": "azimuth-sector x%d" % world if world > 1 else "single"},
+                       "parallelism": "azimuth-sector x%d" % world if world > 1 else "single",
+                       "sector_split": "in-kernel (timed)" if world > 1 else None},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "path_ms_per_scan": round(path_ms_per_scan, 5),
@@ -269,6 +272,7 @@ def main():
             if path_ms_per_scan else None,
             "bricks": st["n_bricks"],
             "readout_merge_ms": merge_ms,
+            "readout_merge": merge_info,
             "gen_seconds": round(t_gen, 2),
         }
         print(json.dumps(out))

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define TSDF_ABI_VERSION 3
+#define TSDF_ABI_VERSION 4
 #define TSDF_MAX_BATCH 64 /* scans per GPU batch (see tsdf_params.max_batch) */
 #define TSDF_BRICK_SIDE 8 /* voxels per brick edge: a brick is 8^3 = 512 voxels */
 
@@ -85,6 +85,14 @@ typedef struct tsdf_params {
     int32_t use_weight_dropoff; /* Voxblox use_weight_dropoff: w *= (tau + sdf) / (tau - voxel_size)
                                    for sdf < -voxel_size, floored at 0 (default 1) */
     float max_weight;           /* Voxblox max_weight: the fused weight is capped here (default 1e4) */
+    /* ABI v4: azimuth-sector sharding (multi-GPU, one context per GPU).  With
+     * n_sectors > 1 a context integrates only the rays whose azimuth around their scan's origin
+     * lies in sector `sector` of n_sectors equal sectors starting at sector_yaw0 (world frame);
+     * the other rays are dropped like out-of-range ones, inside the walk kernels.  The rule is
+     * tsdf_sector_of's: every ray belongs to exactly one sector. */
+    uint32_t n_sectors;  /* 0 or 1: no sharding (default) */
+    uint32_t sector;     /* 0 .. n_sectors - 1 */
+    double sector_yaw0;  /* radians */
 } tsdf_params;
 
 /* Batching.  Scans are integrated in call order and the field after any sequence of calls is
@@ -219,11 +227,53 @@ int tsdf_os_decode_device(tsdf_ctx* ctx, const tsdf_os_format* fmt, const uint8_
 int tsdf_os_cartesian_device(tsdf_ctx* ctx, const uint32_t* d_range, uint64_t n, const float* d_dir,
                              const float* d_off, const double pose[12], float* d_xyz);
 
-/* Azimuth-sector selection for multi-GPU sharding: keep the points whose azimuth around origin
- * (atan2(y-oy, x-ox) in [-pi, pi), offset by yaw0) falls in sector `sector` of `n_sectors`
- * equal sectors.  Writes the selected points packed to out_xyz (host, 3 f32 each). */
+/* Azimuth sectors (multi-GPU sharding).  A ray's azimuth is taken as the fp32 pseudo-angle
+ * a(dx, dy) in [0, 4) of (dx, dy) = (px - (float)ox, py - (float)oy) — monotone in the true
+ * angle, exactly reproducible on host and GPU (one IEEE division, no trig):
+ *     dy >= 0: dx >= 0 ? dy / (dx + dy) (0 when dx + dy == 0) : 1 - dx / (dy - dx)
+ *     dy <  0: dx <  0 ? 2 - dy / (-dx - dy)                  : 3 + dx / (dx - dy)
+ * Sector k starts at the pseudo-angle of yaw0 + 2 pi k / n (cos/sin in double, rounded to
+ * float); sector k is [start_k, start_{k+1}) taken cyclically, so the sectors partition the
+ * plane.  tsdf_sector_of gives the sector of one point (-1: zero-length / NaN). */
+int32_t tsdf_sector_of(float px, float py, const double origin[3], double yaw0, uint32_t n_sectors);
+
+/* Keep the points of sector `sector` (tsdf_sector_of's rule); packed to out_xyz (host, 3 f32 each). */
 int tsdf_select_sector(const float* xyz, uint64_t n, const double origin[3], double yaw0,
                        uint32_t sector, uint32_t n_sectors, float* out_xyz, uint64_t* n_out);
+
+/* ---- Border-brick reduce (multi-GPU read-out) ----------------------
+ * Sector shards hold partial fields; VDBFusion's field is the weighted mean over all samples, so
+ * the partial fields of a brick held by several ranks combine exactly (up to fp32 rounding).  The
+ * reduce moves every shared brick's mass to its OWNER — the lowest rank holding it — over the
+ * caller's collective (RCCL all-to-all over xGMI; the library does no communication):
+ *   1. tsdf_brick_keys_device: this rank's brick keys -> all-gathered by the caller;
+ *   2. tsdf_border_pack_device: this rank's bricks owned by a lower rank are packed as tiles
+ *      (grouped by owner) and reset to the background (their mass now travels to the owner);
+ *   3. all_to_all of the tiles (caller), then tsdf_border_merge_device on every rank merges the
+ *      received tiles into its bricks, sources in ascending rank order, by the rule of
+ *      tsdf_import_bricks (weighted mean; copy where W == 0).
+ * Afterwards every brick's full mass sits on its owner (the others hold it at W = 0), so
+ * integration may continue and the reduce may be repeated.  All buffers are DEVICE memory of the
+ * context's GPU and must be ready when the call is made; the calls return after their own GPU work
+ * finished.  Brick keys: 21 bits per axis, biased by 2^20 (x | y << 21 | z << 42). */
+#define TSDF_TILE_WORDS 1028 /* u32 words per tile: 512 sdf f32, 512 weight f32, key lo, key hi, 0, 0 */
+#define TSDF_MAX_WORLD 64
+
+/* Keys of the context's bricks (device, cap entries); *n_out = bricks (TSDF_EOVERFLOW if > cap). */
+int tsdf_brick_keys_device(tsdf_ctx* ctx, uint64_t* d_keys, uint64_t cap, uint64_t* n_out);
+
+/* d_all_keys: world blocks of `stride` keys (device), block r = rank r's keys, counts[r] valid
+ * (host array).  Packs the bricks of this context owned by a lower rank into d_send (device, rows
+ * of TSDF_TILE_WORDS, grouped by owner rank ascending; cap_rows rows) and resets them.
+ * send_counts[world] (host) receives the rows per destination; d_send == NULL only counts. */
+int tsdf_border_pack_device(tsdf_ctx* ctx, const uint64_t* d_all_keys, const uint64_t* counts,
+                            uint64_t stride, uint32_t world, uint32_t rank, uint32_t* d_send,
+                            uint64_t cap_rows, uint64_t* send_counts);
+
+/* Merge received tiles: d_recv (device) holds recv_counts[r] rows from each rank r, grouped by r
+ * ascending.  Every tile's brick must exist here (it does on its owner). */
+int tsdf_border_merge_device(tsdf_ctx* ctx, const uint32_t* d_recv, const uint64_t* recv_counts,
+                             uint32_t world);
 
 #ifdef __cplusplus
 }

@@ -23,6 +23,7 @@
 using namespace tsdf;
 
 static_assert(TSDF_MAX_BATCH == MAX_BATCH, "header and device batch limits differ");
+static_assert(TSDF_TILE_WORDS == TILE_WORDS && TSDF_MAX_WORLD == MAX_WORLD, "border tile layout differs");
 
 namespace {
 
@@ -82,6 +83,21 @@ uint64_t next_pow2(uint64_t v) {
     uint64_t p = 1;
     while (p < v) p <<= 1;
     return p;
+}
+
+// Sector k of n starts at the pseudo-angle of yaw0 + 2 pi k / n (include/tsdf_hip.h
+// tsdf_sector_of); the oracle computes the same bounds with the same operations.
+float sector_start(double yaw0, uint32_t k, uint32_t n) {
+    const double th = yaw0 + 6.283185307179586476925286766559 * (double)k / (double)n;
+    return pseudo_angle((float)std::cos(th), (float)std::sin(th));
+}
+
+void sector_bounds(double yaw0, uint32_t sector, uint32_t n, RayConst& R) {
+    R.sec_on = n > 1 ? 1 : 0;
+    if (!R.sec_on) return;
+    R.sec_lo = sector_start(yaw0, sector, n);
+    R.sec_hi = sector_start(yaw0, (sector + 1) % n, n);
+    R.sec_wrap = R.sec_hi <= R.sec_lo ? 1 : 0;
 }
 
 }  // namespace
@@ -435,6 +451,7 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
     c->R.max_weight = p->max_weight;
     c->R.bg = p->semantics == TSDF_SEM_VOXBLOX ? 0.0f : c->R.tau;
     c->R.tau_m_vs = c->R.tau - c->R.vs;
+    sector_bounds(p->sector_yaw0, p->sector, p->n_sectors, c->R);
     {
         const double band = p->space_carving ? (p->max_range + p->sdf_trunc) / p->voxel_size
                                              : 2.0 * p->sdf_trunc / p->voxel_size;
@@ -524,7 +541,8 @@ int tsdf_create(const tsdf_params* p, tsdf_ctx** out) {
         p->max_bricks >= 0xFFFFFFF0ull || p->max_points == 0 || !(p->min_range >= 0) ||
         !(p->max_range > p->min_range) || p->max_batch == 0 || p->max_batch > TSDF_MAX_BATCH ||
         (p->semantics != TSDF_SEM_VDBFUSION && p->semantics != TSDF_SEM_VOXBLOX) ||
-        (p->semantics == TSDF_SEM_VOXBLOX && !(p->max_weight > 0.0f)))
+        (p->semantics == TSDF_SEM_VOXBLOX && !(p->max_weight > 0.0f)) ||
+        (p->n_sectors > 1 && p->sector >= p->n_sectors) || !std::isfinite(p->sector_yaw0))
         return TSDF_EINVAL;
     if (p->space_carving && !std::isfinite(p->max_range)) return TSDF_EINVAL;
     tsdf_ctx* c = new (std::nothrow) tsdf_ctx();
@@ -651,6 +669,8 @@ int tsdf_sync(tsdf_ctx* c) {
     HIPCHK(c, hipMemcpy(&ovf, &c->G->overflow, sizeof ovf, hipMemcpyDeviceToHost));
     if (ovf) {
         HIPCHK(c, hipMemset(&c->G->overflow, 0, sizeof ovf));
+        if (ovf & ERR_MERGE_KEY)
+            return fail(c, TSDF_EINVAL, "border merge: a tile's brick is not held by this context");
         return fail(c, TSDF_ENOMEM, "capacity overflow (%s%s%s%s): updates were dropped",
                     (ovf & OVF_TABLE) ? "hash table full; " : "",
                     (ovf & OVF_POOL) ? "brick pool exhausted; " : "",
@@ -998,25 +1018,132 @@ int tsdf_set_profiling(tsdf_ctx* c, int32_t on) {
     return (on && !c->timer) ? TSDF_ENOMEM : TSDF_OK;
 }
 
+int32_t tsdf_sector_of(float px, float py, const double origin[3], double yaw0,
+                       uint32_t n_sectors) {
+    if (!origin || n_sectors == 0) return -1;
+    const float dx = px - (float)origin[0], dy = py - (float)origin[1];
+    if (!(dx == dx) || !(dy == dy)) return -1;
+    if (n_sectors == 1) return 0;
+    // the sector whose [start, next start) holds a, cyclically
+    for (uint32_t k = 0; k < n_sectors; k++) {
+        RayConst R{};
+        sector_bounds(yaw0, k, n_sectors, R);
+        if (in_sector(R, dx, dy)) return (int32_t)k;
+    }
+    return -1;
+}
+
 int tsdf_select_sector(const float* xyz, uint64_t n, const double origin[3], double yaw0,
                        uint32_t sector, uint32_t n_sectors, float* out_xyz, uint64_t* n_out) {
     if (!xyz || !origin || !out_xyz || !n_out || n_sectors == 0 || sector >= n_sectors)
         return TSDF_EINVAL;
-    const double two_pi = 6.283185307179586476925286766559;
+    RayConst R{};
+    sector_bounds(yaw0, sector, n_sectors, R);
+    const float ox = (float)origin[0], oy = (float)origin[1];
     uint64_t k = 0;
     for (uint64_t i = 0; i < n; i++) {
-        double az = std::atan2((double)xyz[3 * i + 1] - origin[1], (double)xyz[3 * i] - origin[0]) - yaw0;
-        az = std::fmod(az, two_pi);
-        if (az < 0) az += two_pi;
-        uint32_t s = (uint32_t)(az / two_pi * n_sectors);
-        if (s >= n_sectors) s = n_sectors - 1;
-        if (s == sector) {
-            std::memcpy(out_xyz + 3 * k, xyz + 3 * i, 12);
-            k++;
-        }
+        if (!in_sector(R, xyz[3 * i] - ox, xyz[3 * i + 1] - oy)) continue;
+        std::memcpy(out_xyz + 3 * k, xyz + 3 * i, 12);
+        k++;
     }
     *n_out = k;
     return TSDF_OK;
+}
+
+// ---- border-brick reduce (include/tsdf_hip.h; kernels in tsdf_border.hip) ----------------------
+
+int tsdf_brick_keys_device(tsdf_ctx* c, uint64_t* d_keys, uint64_t cap, uint64_t* n_out) {
+    if (!c || !n_out) return TSDF_EINVAL;
+    uint64_t nb = 0;
+    int rc = pool_bricks(c, &nb);
+    if (rc) return rc;
+    *n_out = nb;
+    if (nb > cap) return fail(c, TSDF_EOVERFLOW, "brick keys need %llu entries", (unsigned long long)nb);
+    if (!nb) return TSDF_OK;
+    if (!d_keys) return fail(c, TSDF_EINVAL, "null key buffer");
+    HIPCHK(c, hipMemcpyAsync(d_keys, c->T.brick_keys, nb * 8, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return TSDF_OK;
+}
+
+int tsdf_border_pack_device(tsdf_ctx* c, const uint64_t* d_all_keys, const uint64_t* counts,
+                            uint64_t stride, uint32_t world, uint32_t rank, uint32_t* d_send,
+                            uint64_t cap_rows, uint64_t* send_counts) {
+    if (!c) return TSDF_EINVAL;
+    if (!counts || !send_counts || world == 0 || world > TSDF_MAX_WORLD || rank >= world)
+        return fail(c, TSDF_EINVAL, "bad world/rank or null counts");
+    WorldCounts wc{};
+    for (uint32_t r = 0; r < world; r++) {
+        if (counts[r] > stride) return fail(c, TSDF_EINVAL, "counts[%u] > stride", r);
+        wc.n[r] = counts[r];
+        send_counts[r] = 0;
+    }
+    uint64_t nb = 0;
+    int rc = pool_bricks(c, &nb);
+    if (rc) return rc;
+    if (!nb || rank == 0) return TSDF_OK;  // rank 0 owns everything it holds
+    bool lower = false;
+    for (uint32_t r = 0; r < rank; r++) lower |= wc.n[r] > 0;
+    if (!lower) return TSDF_OK;
+    if (!d_all_keys) return fail(c, TSDF_EINVAL, "null key buffer");
+    uint32_t *d_owner = nullptr, *d_aux = nullptr, *d_rows = nullptr;
+    uint32_t dest[MAX_WORLD] = {}, cursor[MAX_WORLD] = {};
+    uint64_t rows = 0;
+    hipError_t e = hipMalloc(&d_owner, nb * 4);
+    if (e == hipSuccess) e = hipMalloc(&d_aux, 2 * MAX_WORLD * 4);
+    if (e == hipSuccess)
+        e = launch_border_owner(c->T, (uint32_t)nb, d_all_keys, wc, stride, rank, d_owner, d_aux,
+                                c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(dest, d_aux, sizeof dest, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess) {
+        for (uint32_t r = 0; r < world; r++) {
+            cursor[r] = (uint32_t)rows;
+            send_counts[r] = dest[r];
+            rows += dest[r];
+        }
+    }
+    if (e == hipSuccess && d_send && rows) {
+        if (rows > cap_rows) {
+            (void)hipFree(d_owner);
+            (void)hipFree(d_aux);
+            return fail(c, TSDF_EOVERFLOW, "border pack needs %llu rows", (unsigned long long)rows);
+        }
+        e = hipMalloc(&d_rows, rows * 4);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(d_aux + MAX_WORLD, cursor, sizeof cursor, hipMemcpyHostToDevice,
+                               c->stream);
+        if (e == hipSuccess)
+            e = launch_border_pack(c->T, c->Pl, c->R.bg, (uint32_t)nb, rank, d_owner,
+                                   d_aux + MAX_WORLD, d_rows, (uint32_t)rows, d_send, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    }
+    for (void* q : {(void*)d_owner, (void*)d_aux, (void*)d_rows})
+        if (q) (void)hipFree(q);
+    if (e != hipSuccess) return fail(c, TSDF_EHIP, "border pack: %s", hipGetErrorString(e));
+    return TSDF_OK;
+}
+
+int tsdf_border_merge_device(tsdf_ctx* c, const uint32_t* d_recv, const uint64_t* recv_counts,
+                             uint32_t world) {
+    if (!c) return TSDF_EINVAL;
+    if (!recv_counts || world == 0 || world > TSDF_MAX_WORLD)
+        return fail(c, TSDF_EINVAL, "bad world or null counts");
+    uint64_t total = 0;
+    for (uint32_t r = 0; r < world; r++) total += recv_counts[r];
+    if (!total) return TSDF_OK;
+    if (!d_recv) return fail(c, TSDF_EINVAL, "null tile buffer");
+    int rc = drain(c);
+    if (rc) return rc;
+    uint64_t row = 0;
+    for (uint32_t r = 0; r < world; r++) {  // sources in ascending rank order
+        if (recv_counts[r])
+            HIPCHK(c, launch_border_merge(c->T, c->Pl, d_recv + row * TSDF_TILE_WORDS,
+                                          recv_counts[r], c->G, c->stream));
+        row += recv_counts[r];
+    }
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return tsdf_sync(c);
 }
 
 }  // extern "C"

@@ -64,6 +64,8 @@ static_assert(HCAP <= (1 << (PAIR_CNT_SHIFT - PAIR_LID_SHIFT)), "lid overflows")
 
 // overflow bits (sticky until tsdf_sync reads them)
 constexpr uint32_t OVF_TABLE = 1u, OVF_POOL = 2u, OVF_PAIRS = 4u, OVF_ACTIVE = 8u, OVF_FB = 16u;
+// a border tile whose brick this context lacks (tsdf_border_merge_device; sticky like OVF_*)
+constexpr uint32_t ERR_MERGE_KEY = 1u << 8;
 
 // per-context constants of the ray model
 struct RayConst {
@@ -78,7 +80,31 @@ struct RayConst {
     // squared-distance bounds bracketing tau by 2^-20 relative: d2 < tau2_lo implies
     // sqrt_rn(d2) < tau, d2 > tau2_hi implies sqrt_rn(d2) > tau (voxel_gate skips the sqrt)
     float tau2_lo, tau2_hi;
+    // azimuth-sector sharding (tsdf_params.n_sectors > 1): keep rays whose pseudo-angle lies in
+    // [sec_lo, sec_hi), or outside [sec_hi, sec_lo) when the sector wraps past 4 (sec_wrap)
+    int sec_on, sec_wrap;
+    float sec_lo, sec_hi;
 };
+
+// fp32 pseudo-angle of (x, y) in [0, 4), monotone in atan2 (include/tsdf_hip.h tsdf_sector_of):
+// one IEEE division, so host and GPU agree bit for bit (built with -ffp-contract=off)
+__host__ __device__ inline float pseudo_angle(float x, float y) {
+    if (y >= 0.0f) {
+        if (x >= 0.0f) {
+            const float d = x + y;
+            return d > 0.0f ? y / d : 0.0f;
+        }
+        return 1.0f - x / (y - x);
+    }
+    if (x < 0.0f) return 2.0f - y / (-x - y);
+    return 3.0f + x / (x - y);
+}
+
+__host__ __device__ inline bool in_sector(const RayConst& R, float dx, float dy) {
+    if (!R.sec_on) return true;
+    const float a = pseudo_angle(dx, dy);
+    return R.sec_wrap ? (a >= R.sec_lo || a < R.sec_hi) : (a >= R.sec_lo && a < R.sec_hi);
+}
 
 // one batch: scan s = points [off[s], off[s+1]) seen from (ox[s], oy[s], oz[s]) (fp32);
 // k_count / k_place blocks [blk[s], blk[s+1]) cover scan s, RPB rays each
@@ -178,6 +204,21 @@ hipError_t launch_import(const Table& T, const Pool& Pl, const int32_t* d_coords
                          const float* d_sdf, const float* d_w, uint32_t* d_tidx, Globals* G,
                          hipStream_t st);
 hipError_t launch_fill(float* p, float v, uint64_t n, hipStream_t st);
+// border-brick reduce (tsdf_border.hip)
+constexpr int TILE_WORDS = 1028;  // include/tsdf_hip.h TSDF_TILE_WORDS
+constexpr int MAX_WORLD = 64;
+struct WorldCounts { uint64_t n[MAX_WORLD]; };
+// owner[slot] = the lowest rank (< rank) holding the brick, else rank
+hipError_t launch_border_owner(const Table& T, uint32_t n_bricks, const uint64_t* d_all_keys,
+                               const WorldCounts& counts, uint64_t stride, uint32_t rank,
+                               uint32_t* d_owner, uint32_t* d_dest_n, hipStream_t st);
+// rows of the bricks owned elsewhere (cursor[r] = first row of destination r), tiles packed and the
+// bricks reset to the background
+hipError_t launch_border_pack(const Table& T, const Pool& Pl, float bg, uint32_t n_bricks,
+                              uint32_t rank, const uint32_t* d_owner, uint32_t* d_cursor,
+                              uint32_t* d_rows, uint32_t n_rows, uint32_t* d_send, hipStream_t st);
+hipError_t launch_border_merge(const Table& T, const Pool& Pl, const uint32_t* d_recv,
+                               uint64_t n_rows, Globals* G, hipStream_t st);
 // Ouster packets (tsdf_ouster.hip)
 struct OsField {
     uint32_t nbytes;  // little-endian source bytes (0: the profile has no such field)

@@ -44,6 +44,7 @@ __device__ __forceinline__ void axis_init(float u, float s, float t0i, int v, fl
 __device__ __forceinline__ bool ray_init(const RayConst& R, float ox, float oy, float oz, float px,
                                          float py, float pz, RayState& r) {
     const float dx = px - ox, dy = py - oy, dz = pz - oz;
+    if (!in_sector(R, dx, dy)) return false;  // another GPU's azimuth sector
     const float depth = __builtin_sqrtf(dx * dx + dy * dy + dz * dz);
     if (!(depth > 0.0f)) return false;
     if (!(depth >= R.min_range) || !(depth <= R.max_range)) return false;
@@ -178,6 +179,7 @@ __device__ __forceinline__ void vb_axis(float ss, float es, int& v, int& st, flo
 __device__ __forceinline__ bool vb_init(const RayConst& R, float ox, float oy, float oz, float px,
                                         float py, float pz, VbState& r) {
     const float dx = px - ox, dy = py - oy, dz = pz - oz;
+    if (!in_sector(R, dx, dy)) return false;  // another GPU's azimuth sector
     const float depth = __builtin_sqrtf(dx * dx + (dy * dy + dz * dz));
     if (!(depth > 0.0f)) return false;
     if (depth < R.min_range) return false;

@@ -16,7 +16,9 @@ STATUS_NAMES = {
     TSDF_EHIP: "TSDF_EHIP", TSDF_ENODEV: "TSDF_ENODEV", TSDF_EOVERFLOW: "TSDF_EOVERFLOW",
 }
 
-ABI_VERSION = 3
+ABI_VERSION = 4
+TILE_WORDS = 1028  # TSDF_TILE_WORDS: u32 words of one border-brick tile
+MAX_WORLD = 64
 SEM_VDBFUSION = 0
 SEM_VOXBLOX = 1
 SEMANTICS = {"vdbfusion": SEM_VDBFUSION, "voxblox": SEM_VOXBLOX}
@@ -44,6 +46,10 @@ class TsdfParams(C.Structure):
         ("allow_clear", C.c_int32),
         ("use_weight_dropoff", C.c_int32),
         ("max_weight", C.c_float),
+        # ABI v4
+        ("n_sectors", C.c_uint32),
+        ("sector", C.c_uint32),
+        ("sector_yaw0", C.c_double),
     ]
 
 
@@ -106,6 +112,11 @@ SIGNATURES = {
     "tsdf_set_profiling": (C.c_int, [P, C.c_int32]),
     "tsdf_select_sector": (C.c_int, [FP, C.c_uint64, D3, C.c_double, C.c_uint32, C.c_uint32, FP,
                                      U64P]),
+    "tsdf_sector_of": (C.c_int32, [C.c_float, C.c_float, D3, C.c_double, C.c_uint32]),
+    "tsdf_brick_keys_device": (C.c_int, [P, P, C.c_uint64, U64P]),
+    "tsdf_border_pack_device": (C.c_int, [P, P, U64P, C.c_uint64, C.c_uint32, C.c_uint32, P,
+                                          C.c_uint64, U64P]),
+    "tsdf_border_merge_device": (C.c_int, [P, P, U64P, C.c_uint32]),
     "tsdf_extract_mesh": (C.c_int, [P, C.c_float, FP, C.c_uint64, U64P]),
     "tsdf_mc_table": (C.c_int, [C.POINTER(C.c_uint8)]),
     "tsdf_os_packet_bytes": (C.c_int, [C.POINTER(OsFormat), C.POINTER(C.c_uint32)]),
@@ -143,6 +154,7 @@ def default_params(lib=None, **kw):
         p.max_bricks, p.max_points, p.max_pairs = 1 << 20, 1 << 18, 0
         p.device_id, p.brick_side, p.max_batch = 0, BRICK_SIDE, 32
         p.semantics, p.allow_clear, p.use_weight_dropoff, p.max_weight = SEM_VDBFUSION, 1, 1, 1e4
+        p.n_sectors, p.sector, p.sector_yaw0 = 0, 0, 0.0
     for k, v in kw.items():
         if not hasattr(p, k):
             raise TypeError("unknown tsdf_params field %r" % k)

@@ -204,15 +204,6 @@ class TorchOusterSim:
         return pts.to(torch.float32), pos.astype(np.float64)
 
 
-def sector_mask_torch(pts, origin, sector, n_sectors, yaw0=0.0):
-    """Azimuth sector of each point around origin (same rule as tsdf_select_sector)."""
-    import torch
-    az = torch.atan2(pts[:, 1].double() - origin[1], pts[:, 0].double() - origin[0]) - yaw0
-    az = torch.remainder(az, 2 * math.pi)
-    s = torch.clamp((az / (2 * math.pi) * n_sectors).long(), max=n_sectors - 1)
-    return s == sector
-
-
 def single_ray_scan(points, origin=(0.0, 0.0, 0.0)):
     """Helper for KATs: float32 points + float64 origin."""
     return np.asarray(points, np.float32).reshape(-1, 3), np.asarray(origin, np.float64)

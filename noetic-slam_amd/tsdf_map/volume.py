@@ -47,10 +47,15 @@ def _d3(a):
 class TSDFVolume:
     """A sparse TSDF volume of 8^3-voxel bricks behind the C-ABI of `lib`."""
 
+    # where the library's "device" buffers live (the border-reduce entry points take pointers
+    # into this memory): host memory for a CPU library, the context's GPU for libtsdf_hip.so
+    tensor_device = "cpu"
+
     def __init__(self, lib, voxel_size, sdf_trunc, space_carving=False, min_range=0.0,
                  max_range=math.inf, max_bricks=1 << 20, max_points=1 << 18, device_id=0,
                  max_batch=32, pipeline=False, semantics="vdbfusion", allow_clear=True,
-                 use_weight_dropoff=True, max_weight=10000.0):
+                 use_weight_dropoff=True, max_weight=10000.0, n_sectors=0, sector=0,
+                 sector_yaw0=0.0):
         self._lib = lib
         if semantics not in _abi.SEMANTICS:
             raise ValueError("semantics must be one of %s" % sorted(_abi.SEMANTICS))
@@ -70,6 +75,9 @@ class TSDFVolume:
         p.allow_clear = 1 if allow_clear else 0
         p.use_weight_dropoff = 1 if use_weight_dropoff else 0
         p.max_weight = float(max_weight)
+        p.n_sectors = int(n_sectors)
+        p.sector = int(sector)
+        p.sector_yaw0 = float(sector_yaw0)
         self.params = p
         self.semantics = semantics
         rc = lib.tsdf_create(C.byref(p), C.byref(self._ctx))
@@ -215,6 +223,30 @@ class TSDFVolume:
                 raise ValueError("checkpoint voxel_size differs")
             self.import_bricks(z["coords"], z["sdf"], z["weight"])
 
+    # -- border-brick reduce (multi-GPU read-out; tsdf_map.distributed drives it) ---------------
+    def brick_keys_into(self, d_keys_ptr, cap):
+        """Write this volume's packed brick keys to `tensor_device` memory; returns the count."""
+        n = C.c_uint64()
+        self._check(self._lib.tsdf_brick_keys_device(self._ctx, C.c_void_p(int(d_keys_ptr)),
+                                                     int(cap), C.byref(n)), "brick_keys")
+        return n.value
+
+    def border_pack(self, d_all_keys_ptr, counts, stride, world, rank, d_send_ptr, cap_rows):
+        """Pack (and reset) the bricks a lower rank owns; returns the rows per destination."""
+        cnt = np.ascontiguousarray(counts, np.uint64)
+        out = np.zeros(int(world), np.uint64)
+        self._check(self._lib.tsdf_border_pack_device(
+            self._ctx, C.c_void_p(int(d_all_keys_ptr)), cnt.ctypes.data_as(_abi.U64P),
+            int(stride), int(world), int(rank), C.c_void_p(int(d_send_ptr)), int(cap_rows),
+            out.ctypes.data_as(_abi.U64P)), "border_pack")
+        return [int(x) for x in out]
+
+    def border_merge(self, d_recv_ptr, recv_counts):
+        cnt = np.ascontiguousarray(recv_counts, np.uint64)
+        self._check(self._lib.tsdf_border_merge_device(
+            self._ctx, C.c_void_p(int(d_recv_ptr)), cnt.ctypes.data_as(_abi.U64P), cnt.shape[0]),
+            "border_merge")
+
     # -- stats ----------------------------------------------------------------------------------
     def stats(self):
         st = _abi.TsdfStats()
@@ -241,6 +273,7 @@ class HipTSDFVolume(TSDFVolume):
 
     def __init__(self, voxel_size, sdf_trunc, space_carving=False, **kw):
         super().__init__(load_hip_library(), voxel_size, sdf_trunc, space_carving, **kw)
+        self.tensor_device = "cuda:%d" % self.params.device_id
 
     def integrate_device(self, d_xyz_ptr, n, extrinsic):
         o = _origin_of(extrinsic)
@@ -302,6 +335,40 @@ class SimpleTsdfIntegrator:
         pc = np.asarray(points_C, np.float64).reshape(-1, 3)
         pts_g = (pc @ T[:3, :3].T + T[:3, 3]).astype(np.float32)
         self.volume.integrate(pts_g, T)
+
+
+def sector_ids(points, origin, n_sectors, yaw0=0.0):
+    """The azimuth sector of every point (include/tsdf_hip.h tsdf_sector_of), in numpy fp32: the
+    pseudo-angle of (x - ox, y - oy) against the sector starts.  -1 for NaN points."""
+    pts = np.asarray(points, np.float32).reshape(-1, 3)
+    o = _origin_of(origin)
+    if n_sectors <= 1:
+        return np.where(np.isnan(pts[:, :2]).any(1), -1, 0)
+    dx = pts[:, 0] - np.float32(o[0])
+    dy = pts[:, 1] - np.float32(o[1])
+    a = pseudo_angle(dx, dy)
+    starts = np.array([pseudo_angle(np.float32(math.cos(t)), np.float32(math.sin(t)))
+                       for t in (yaw0 + 2 * math.pi * k / n_sectors for k in range(n_sectors))],
+                      np.float32)
+    sec = np.full(pts.shape[0], -1, np.int64)
+    for k in range(n_sectors):
+        lo, hi = starts[k], starts[(k + 1) % n_sectors]
+        m = (a >= lo) & (a < hi) if hi > lo else (a >= lo) | (a < hi)
+        sec[m] = k
+    return sec
+
+
+def pseudo_angle(x, y):
+    """fp32 pseudo-angle in [0, 4) (monotone in atan2), the sector rule's azimuth."""
+    x = np.asarray(x, np.float32)
+    y = np.asarray(y, np.float32)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        d = x + y
+        q1 = np.where(d > 0, y / np.where(d > 0, d, np.float32(1)), np.float32(0))
+        q2 = np.float32(1) - x / (y - x)
+        q3 = np.float32(2) - y / (-x - y)
+        q4 = np.float32(3) + x / (x - y)
+    return np.where(y >= 0, np.where(x >= 0, q1, q2), np.where(x < 0, q3, q4)).astype(np.float32)
 
 
 def select_sector(points, origin, sector, n_sectors, yaw0=0.0):

@@ -67,6 +67,10 @@ struct tsdf_ctx {
     float vs, inv_vs, tau;
     float bg;   /* background distance: tau (VDBFusion) or 0 (Voxblox TsdfVoxel) */
     int sem;    /* TSDF_SEM_* */
+    /* azimuth-sector filter (tsdf_params.n_sectors > 1): pseudo-angle interval [sec_lo, sec_hi),
+     * cyclic when sec_wrap (include/tsdf_hip.h tsdf_sector_of) */
+    int sec_on, sec_wrap;
+    float sec_lo, sec_hi;
     vox_t* tab;
     uint64_t cap, n;
     uint32_t* touched; /* indices into tab of voxels touched this scan */
@@ -102,6 +106,50 @@ static int set_err(tsdf_ctx* c, int code, const char* msg) {
 }
 
 static int grow(tsdf_ctx* c);
+
+/* ---- azimuth sectors (include/tsdf_hip.h tsdf_sector_of: the multi-GPU shard rule) ---------- */
+
+/* fp32 pseudo-angle of (x, y) in [0, 4), monotone in atan2; one IEEE division */
+static float pseudo_angle(float x, float y) {
+    if (y >= 0.0f) {
+        if (x >= 0.0f) {
+            const float d = x + y;
+            return d > 0.0f ? y / d : 0.0f;
+        }
+        return 1.0f - x / (y - x);
+    }
+    if (x < 0.0f) return 2.0f - y / (-x - y);
+    return 3.0f + x / (x - y);
+}
+
+/* sector k of n starts at the pseudo-angle of yaw0 + 2 pi k / n (cos/sin in double) */
+static float sector_start(double yaw0, uint32_t k, uint32_t n) {
+    const double th = yaw0 + 6.283185307179586476925286766559 * (double)k / (double)n;
+    return pseudo_angle((float)cos(th), (float)sin(th));
+}
+
+typedef struct { int on, wrap; float lo, hi; } sector_t;
+
+static sector_t sector_bounds(double yaw0, uint32_t sector, uint32_t n) {
+    sector_t r = {0, 0, 0.0f, 0.0f};
+    if (n <= 1) return r;
+    r.on = 1;
+    r.lo = sector_start(yaw0, sector, n);
+    r.hi = sector_start(yaw0, (sector + 1) % n, n);
+    r.wrap = r.hi <= r.lo;
+    return r;
+}
+
+static int sector_has(const sector_t* r, float dx, float dy) {
+    if (!r->on) return 1;
+    const float a = pseudo_angle(dx, dy);
+    return r->wrap ? (a >= r->lo || a < r->hi) : (a >= r->lo && a < r->hi);
+}
+
+static int ctx_in_sector(const tsdf_ctx* c, float dx, float dy) {
+    const sector_t r = {c->sec_on, c->sec_wrap, c->sec_lo, c->sec_hi};
+    return sector_has(&r, dx, dy);
+}
 
 /* find-or-insert voxel (x,y,z); returns index or -1 on allocation failure */
 static int64_t vox_get(tsdf_ctx* c, int32_t x, int32_t y, int32_t z) {
@@ -190,7 +238,9 @@ int tsdf_create(const tsdf_params* params, tsdf_ctx** out) {
     if (!(params->voxel_size > 0) || !(params->sdf_trunc > 0) ||
         params->brick_side != TSDF_BRICK_SIDE || params->weight_mode != TSDF_WEIGHT_CONSTANT ||
         (params->semantics != TSDF_SEM_VDBFUSION && params->semantics != TSDF_SEM_VOXBLOX) ||
-        (params->semantics == TSDF_SEM_VOXBLOX && !(params->max_weight > 0.0f)))
+        (params->semantics == TSDF_SEM_VOXBLOX && !(params->max_weight > 0.0f)) ||
+        (params->n_sectors > 1 && params->sector >= params->n_sectors) ||
+        !isfinite(params->sector_yaw0))
         return TSDF_EINVAL;
     tsdf_ctx* c = (tsdf_ctx*)calloc(1, sizeof *c);
     if (!c) return TSDF_ENOMEM;
@@ -201,6 +251,10 @@ int tsdf_create(const tsdf_params* params, tsdf_ctx** out) {
     c->sem = params->semantics;
     c->bg = c->sem == TSDF_SEM_VOXBLOX ? 0.0f : c->tau;
     c->mode = ORACLE_MODE_SCAN_FUSED;
+    {
+        const sector_t r = sector_bounds(params->sector_yaw0, params->sector, params->n_sectors);
+        c->sec_on = r.on; c->sec_wrap = r.wrap; c->sec_lo = r.lo; c->sec_hi = r.hi;
+    }
     *out = c;
     return TSDF_OK;
 }
@@ -239,6 +293,7 @@ static int64_t walk_ray(tsdf_ctx* c, float px, float py, float pz, float ox, flo
                         visit_fn visit, void* user) {
     const float vs = c->vs, inv_vs = c->inv_vs, tau = c->tau;
     const float dx = px - ox, dy = py - oy, dz = pz - oz;
+    if (!ctx_in_sector(c, dx, dy)) return -1; /* another GPU's azimuth sector */
     const float depth = sqrtf(dx * dx + dy * dy + dz * dz);
     /* range filter (VDBFusion pipelines drop r < min_range / r > max_range before Integrate);
      * NaN / zero-length rays are dropped (Ouster r = 0 -> (0,0,0), cartesian.h:64-65) */
@@ -338,6 +393,7 @@ static int64_t walk_ray_vb(tsdf_ctx* c, float px, float py, float pz, float ox, 
                            float oz, visit_fn visit, void* user) {
     const float vs = c->vs, inv_vs = c->inv_vs, tau = c->tau;
     const float dx = px - ox, dy = py - oy, dz = pz - oz;
+    if (!ctx_in_sector(c, dx, dy)) return -1; /* another GPU's azimuth sector */
     /* Eigen's fixed-size-3 reductions (squaredNorm, dot) associate as x + (y + z) */
     const float depth = sqrtf(dx * dx + (dy * dy + dz * dz));
     if (!(depth > 0.0f)) return -1;
@@ -869,24 +925,144 @@ int64_t tsdf_oracle_ray_voxels(tsdf_ctx* c, const float p[3], const double origi
 }
 
 /* Host-side azimuth sector selection (same contract as the GPU library's). */
+int32_t tsdf_sector_of(float px, float py, const double origin[3], double yaw0,
+                       uint32_t n_sectors) {
+    if (!origin || n_sectors == 0) return -1;
+    const float dx = px - (float)origin[0], dy = py - (float)origin[1];
+    if (dx != dx || dy != dy) return -1;
+    if (n_sectors == 1) return 0;
+    for (uint32_t k = 0; k < n_sectors; k++) {
+        const sector_t r = sector_bounds(yaw0, k, n_sectors);
+        if (sector_has(&r, dx, dy)) return (int32_t)k;
+    }
+    return -1;
+}
+
 int tsdf_select_sector(const float* xyz, uint64_t n, const double origin[3], double yaw0,
                        uint32_t sector, uint32_t n_sectors, float* out_xyz, uint64_t* n_out) {
     if (!xyz || !origin || !out_xyz || !n_out || n_sectors == 0 || sector >= n_sectors)
         return TSDF_EINVAL;
+    const sector_t r = sector_bounds(yaw0, sector, n_sectors);
+    const float ox = (float)origin[0], oy = (float)origin[1];
     uint64_t k = 0;
-    const double two_pi = 6.283185307179586476925286766559;
     for (uint64_t i = 0; i < n; i++) {
-        double az = atan2((double)xyz[3 * i + 1] - origin[1], (double)xyz[3 * i] - origin[0]) - yaw0;
-        az = fmod(az, two_pi);
-        if (az < 0) az += two_pi;
-        uint32_t s = (uint32_t)(az / two_pi * n_sectors);
-        if (s >= n_sectors) s = n_sectors - 1;
-        if (s == sector) {
-            out_xyz[3 * k] = xyz[3 * i]; out_xyz[3 * k + 1] = xyz[3 * i + 1]; out_xyz[3 * k + 2] = xyz[3 * i + 2];
-            k++;
-        }
+        if (!sector_has(&r, xyz[3 * i] - ox, xyz[3 * i + 1] - oy)) continue;
+        out_xyz[3 * k] = xyz[3 * i]; out_xyz[3 * k + 1] = xyz[3 * i + 1]; out_xyz[3 * k + 2] = xyz[3 * i + 2];
+        k++;
     }
     *n_out = k;
+    return TSDF_OK;
+}
+
+/* ---- border-brick reduce (include/tsdf_hip.h; the GPU's tsdf_border.hip restated) ------------
+ * The "device" buffers of the ABI are host memory here.  Bricks are the voxel map's bricks with
+ * an observed voxel (list_bricks); a reset brick's voxels go to (bg, 0), so it drops out of the
+ * list — the GPU keeps its (empty) brick allocated, which sends zero-weight tiles that merge as
+ * no-ops: the two agree on the merged field. */
+#define TILE_WORDS TSDF_TILE_WORDS
+
+static uint64_t pack_key(const int32_t b[3]) {
+    return (uint64_t)(b[0] + (1 << 20)) | ((uint64_t)(b[1] + (1 << 20)) << 21) |
+           ((uint64_t)(b[2] + (1 << 20)) << 42);
+}
+
+static int cmp_u64(const void* a, const void* b) {
+    const uint64_t x = *(const uint64_t*)a, y = *(const uint64_t*)b;
+    return x < y ? -1 : (x > y);
+}
+
+int tsdf_brick_keys_device(tsdf_ctx* c, uint64_t* keys, uint64_t cap, uint64_t* n_out) {
+    if (!c || !n_out) return TSDF_EINVAL;
+    uint64_t nb = 0;
+    brick_ent* e = list_bricks(c, &nb);
+    if (!e) return TSDF_ENOMEM;
+    *n_out = nb;
+    if (nb > cap) { free(e); return set_err(c, TSDF_EOVERFLOW, "key buffer too small"); }
+    for (uint64_t i = 0; i < nb; i++) keys[i] = pack_key(e[i].b);
+    free(e);
+    return TSDF_OK;
+}
+
+int tsdf_border_pack_device(tsdf_ctx* c, const uint64_t* all_keys, const uint64_t* counts,
+                            uint64_t stride, uint32_t world, uint32_t rank, uint32_t* send,
+                            uint64_t cap_rows, uint64_t* send_counts) {
+    if (!c || !counts || !send_counts || world == 0 || world > TSDF_MAX_WORLD || rank >= world)
+        return set_err(c, TSDF_EINVAL, "bad world/rank or null counts");
+    if (c->n_thr > 1) return set_err(c, TSDF_EINVAL, "border reduce needs the serial mode");
+    for (uint32_t r = 0; r < world; r++) {
+        if (counts[r] > stride) return set_err(c, TSDF_EINVAL, "counts[r] > stride");
+        send_counts[r] = 0;
+    }
+    uint64_t nb = 0;
+    brick_ent* e = list_bricks(c, &nb);
+    if (!e) return TSDF_ENOMEM;
+    uint32_t* owner = (uint32_t*)malloc((nb ? nb : 1) * sizeof(uint32_t));
+    uint64_t* sorted = (uint64_t*)malloc((stride ? stride : 1) * sizeof(uint64_t));
+    if (!owner || !sorted) { free(e); free(owner); free(sorted); return TSDF_ENOMEM; }
+    for (uint64_t i = 0; i < nb; i++) owner[i] = rank;
+    for (uint32_t r = rank; r-- > 0;) { /* descending, so the lowest holder wins */
+        memcpy(sorted, all_keys + r * stride, counts[r] * sizeof(uint64_t));
+        qsort(sorted, counts[r], sizeof(uint64_t), cmp_u64);
+        for (uint64_t i = 0; i < nb; i++) {
+            const uint64_t k = pack_key(e[i].b);
+            if (bsearch(&k, sorted, counts[r], sizeof(uint64_t), cmp_u64)) owner[i] = r;
+        }
+    }
+    uint64_t rows = 0;
+    for (uint64_t i = 0; i < nb; i++)
+        if (owner[i] != rank) { send_counts[owner[i]]++; rows++; }
+    int rc = TSDF_OK;
+    if (send && rows > cap_rows) rc = set_err(c, TSDF_EOVERFLOW, "send buffer too small");
+    if (send && rc == TSDF_OK) {
+        uint64_t row = 0;
+        for (uint32_t d = 0; d < rank; d++)
+            for (uint64_t i = 0; i < nb; i++) {
+                if (owner[i] != d) continue;
+                uint32_t* t = send + row * TILE_WORDS;
+                float* ts = (float*)t;
+                float* tw = (float*)(t + 512);
+                for (int l = 0; l < 512; l++) {
+                    const int32_t x = e[i].b[0] * 8 + (l & 7), y = e[i].b[1] * 8 + ((l >> 3) & 7),
+                                  z = e[i].b[2] * 8 + (l >> 6);
+                    int64_t k = -1;
+                    const vox_t* v = vox_find(c, x, y, z);
+                    if (v) k = v - c->tab;
+                    ts[l] = v ? v->S : c->bg;
+                    tw[l] = v ? v->W : 0.0f;
+                    if (k >= 0) { c->tab[k].S = c->bg; c->tab[k].W = 0.0f; } /* mass moves out */
+                }
+                const uint64_t key = pack_key(e[i].b);
+                t[1024] = (uint32_t)key; t[1025] = (uint32_t)(key >> 32); t[1026] = 0; t[1027] = 0;
+                row++;
+            }
+    }
+    free(e); free(owner); free(sorted);
+    return rc;
+}
+
+int tsdf_border_merge_device(tsdf_ctx* c, const uint32_t* recv, const uint64_t* recv_counts,
+                             uint32_t world) {
+    if (!c || !recv_counts || world == 0 || world > TSDF_MAX_WORLD)
+        return set_err(c, TSDF_EINVAL, "bad world or null counts");
+    if (c->n_thr > 1) return set_err(c, TSDF_EINVAL, "border reduce needs the serial mode");
+    uint64_t total = 0;
+    for (uint32_t r = 0; r < world; r++) total += recv_counts[r];
+    for (uint64_t row = 0; row < total; row++) { /* rows are grouped by source, ascending */
+        const uint32_t* t = recv + row * TILE_WORDS;
+        const uint64_t key = (uint64_t)t[1024] | ((uint64_t)t[1025] << 32);
+        const int32_t b[3] = {(int32_t)(key & 0x1FFFFF) - (1 << 20),
+                              (int32_t)((key >> 21) & 0x1FFFFF) - (1 << 20),
+                              (int32_t)((key >> 42) & 0x1FFFFF) - (1 << 20)};
+        int held = 0;
+        for (int l = 0; l < 512 && !held; l++) {
+            const vox_t* v = vox_find(c, b[0] * 8 + (l & 7), b[1] * 8 + ((l >> 3) & 7),
+                                      b[2] * 8 + (l >> 6));
+            held = v && v->W > 0.0f;
+        }
+        if (!held) return set_err(c, TSDF_EINVAL, "border merge: a tile's brick is not held here");
+        const int rc = tsdf_import_bricks(c, b, (const float*)t, (const float*)(t + 512), 1);
+        if (rc != TSDF_OK) return rc;
+    }
     return TSDF_OK;
 }
 

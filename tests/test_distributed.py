@@ -1,6 +1,6 @@
 """The N>1 path on CPU: world_size-2 gloo ranks, each integrating its azimuth sector into its own
-partial field (the oracle stands in for the GPU volume here), then the border-brick all-to-all
-merge of tsdf_map.distributed.  The union of the ranks' merged shares must equal the
+partial field (the oracle stands in for the GPU volume here: same ABI, same sector filter), then
+the border-brick reduce of tsdf_map.distributed (the GPU's code path, on host buffers), twice.  The union of the ranks' merged shares must equal the
 single-volume field: same bricks/voxels, weights exact, |dSDF| <= 1e-5 m, single-owner voxels
 bit-exact."""
 import os
@@ -34,22 +34,22 @@ def _worker(rank, world, port, out_dir):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     sim = OusterSim()
-    vol = oracle.OracleTSDFVolume(0.05, 0.15)
-    # same sector rule as tsdf_select_sector
+    # the sector filter inside the integrate (tsdf_params.n_sectors / sector), as on the GPUs
+    vol = oracle.OracleTSDFVolume(0.05, 0.15, n_sectors=world, sector=rank, sector_yaw0=0.3)
     for k in (0, 3):
         pts, org = sim.scan(k)
-        pts = pts[::8]
-        az = np.mod(np.arctan2(pts[:, 1].astype(np.float64) - org[1],
-                               pts[:, 0].astype(np.float64) - org[0]), 2 * np.pi)
-        sec = np.minimum((az / (2 * np.pi) * world).astype(np.int64), world - 1)
-        vol.integrate(np.ascontiguousarray(pts[sec == rank]), org)
+        vol.integrate(np.ascontiguousarray(pts[::8]), org)
+    c, s, w = merged_bricks(vol)
+    # a second reduce after more integration moves only the new partial mass
+    pts, org = sim.scan(6)
+    vol.integrate(np.ascontiguousarray(pts[::8]), org)
     c, s, w = merged_bricks(vol)
     np.savez(os.path.join(out_dir, "rank%d.npz" % rank), coords=c, sdf=s, weight=w)
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
+@pytest.mark.parametrize("world", [2, 3])
 def test_sector_sharded_merge_gloo(world, tmp_path):
     mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world,
                        join=True, start_method="spawn")
@@ -65,7 +65,7 @@ def test_sector_sharded_merge_gloo(world, tmp_path):
                                   np.concatenate([p["weight"] for p in parts]))
     sim = OusterSim()
     ref = oracle.OracleTSDFVolume(0.05, 0.15)
-    for k in (0, 3):
+    for k in (0, 3, 6):
         pts, org = sim.scan(k)
         ref.integrate(np.ascontiguousarray(pts[::8]), org)
     ri, rs, rw = ref.export_voxels()

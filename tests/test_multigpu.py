@@ -1,0 +1,197 @@
+"""The multi-GPU path on one MI355X: azimuth-sector filtering inside the walk kernels and the
+device-resident border-brick reduce, against the oracle running the same ABI.
+
+* sector filter: a context with n_sectors/sector integrates exactly the oracle's sector rays,
+  bit for bit;
+* border reduce, one process: the collective is emulated (all-gather = stack, all-to-all =
+  slicing) over 3 GPU contexts and over 3 oracle contexts; after the reduce every GPU rank's field
+  equals its oracle twin BIT FOR BIT, and the union equals the single-volume field (weights exact,
+  |dSDF| <= 1e-5 m: fp32 weighted means of partial fields);
+* border reduce, two processes: tsdf_map.distributed.border_reduce itself, gloo ranks sharing the
+  GPU (tiles staged through host memory; RCCL needs one GPU per rank).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from conftest import REPO
+
+pytestmark = pytest.mark.gpu
+
+VS, TAU = 0.05, 0.15
+TILE = 1028
+
+
+def hip(**kw):
+    from tsdf_map import HipTSDFVolume
+    return HipTSDFVolume(VS, TAU, **kw)
+
+
+def ora(**kw):
+    return oracle.OracleTSDFVolume(VS, TAU, **kw)
+
+
+def voxels_equal_bitwise(a, b):
+    ai, as_, aw = a
+    bi, bs, bw = b
+    return (ai.shape == bi.shape and np.array_equal(ai, bi) and np.array_equal(aw, bw)
+            and np.array_equal(as_.view(np.uint32), bs.view(np.uint32)))
+
+
+@pytest.mark.parametrize("n,yaw0", [(4, 0.0), (3, 0.7)])
+def test_sector_filter_bitwise(sim, n, yaw0):
+    scans = [sim.scan(k) for k in (0, 5)]
+    rays = 0
+    for k in range(n):
+        g = hip(n_sectors=n, sector=k, sector_yaw0=yaw0)
+        o = ora(n_sectors=n, sector=k, sector_yaw0=yaw0)
+        for pts, org in scans:
+            g.integrate(pts, org)
+            o.integrate(pts, org)
+        g.sync()
+        assert voxels_equal_bitwise(g.export_voxels(), o.export_voxels())
+        rays += g.stats()["n_rays_total"]
+    assert rays == sum(p.shape[0] for p, _ in scans)
+
+
+def emulated_reduce(vols, dev):
+    """border_reduce's four steps for all ranks of one process (the collective emulated)."""
+    world = len(vols)
+    keys, counts = [], []
+    for v in vols:
+        k = torch.empty(max(v.num_bricks(), 1), dtype=torch.int64, device=dev)
+        torch.cuda.synchronize()
+        counts.append(v.brick_keys_into(k.data_ptr(), k.numel()))
+        keys.append(k)
+    stride = max(counts)
+    allk = torch.full((world, stride), -1, dtype=torch.int64, device=dev)
+    for r in range(world):
+        allk[r, :counts[r]] = keys[r][:counts[r]]
+    sends, splits = [], []
+    for r, v in enumerate(vols):
+        s = torch.empty((max(counts[r], 1), TILE), dtype=torch.int32, device=dev)
+        torch.cuda.synchronize()
+        sc = v.border_pack(allk.data_ptr(), counts, stride, world, r, s.data_ptr(), s.shape[0])
+        sends.append(s)
+        splits.append(sc)
+    for d, v in enumerate(vols):  # rank d receives block d of every source, sources ascending
+        parts, rc = [], []
+        for r in range(world):
+            off = sum(splits[r][:d])
+            parts.append(sends[r][off:off + splits[r][d]])
+            rc.append(splits[r][d])
+        recv = torch.cat(parts).contiguous() if sum(rc) else torch.empty((1, TILE), dtype=torch.int32,
+                                                                          device=dev)
+        torch.cuda.synchronize()
+        v.border_merge(recv.data_ptr(), rc)
+    return splits
+
+
+def emulated_reduce_host(vols):
+    """The same on host buffers for oracle contexts (numpy pointers)."""
+    world = len(vols)
+    keys = [np.empty(max(v.num_bricks(), 1), np.int64) for v in vols]
+    counts = [v.brick_keys_into(k.ctypes.data, k.size) for v, k in zip(vols, keys)]
+    stride = max(counts)
+    allk = np.full((world, stride), -1, np.int64)
+    for r in range(world):
+        allk[r, :counts[r]] = keys[r][:counts[r]]
+    sends, splits = [], []
+    for r, v in enumerate(vols):
+        s = np.empty((max(counts[r], 1), TILE), np.int32)
+        splits.append(v.border_pack(allk.ctypes.data, counts, stride, world, r, s.ctypes.data,
+                                    s.shape[0]))
+        sends.append(s)
+    for d, v in enumerate(vols):
+        parts, rc = [], []
+        for r in range(world):
+            off = sum(splits[r][:d])
+            parts.append(sends[r][off:off + splits[r][d]])
+            rc.append(splits[r][d])
+        recv = np.ascontiguousarray(np.concatenate(parts)) if sum(rc) else np.empty((1, TILE), np.int32)
+        v.border_merge(recv.ctypes.data, rc)
+    return splits
+
+
+def test_border_reduce_matches_oracle_bitwise(sim):
+    from tsdf_map import bricks_to_voxels
+    world, yaw0 = 3, 0.25
+    dev = torch.device("cuda", 0)
+    g = [hip(n_sectors=world, sector=r, sector_yaw0=yaw0) for r in range(world)]
+    o = [ora(n_sectors=world, sector=r, sector_yaw0=yaw0) for r in range(world)]
+    ref = ora()
+    rounds = [(0, 1), (2, 40)]
+    for i, ks in enumerate(rounds):
+        for k in ks:
+            pts, org = sim.scan(k)
+            pts = np.ascontiguousarray(pts[::2])
+            for v in g + o + [ref]:
+                v.integrate(pts, org)
+        gs = emulated_reduce(g, dev)
+        os_ = emulated_reduce_host(o)
+        assert sum(map(sum, gs)) > 100  # border bricks exist
+        for r in range(world):
+            assert voxels_equal_bitwise(g[r].export_voxels(), o[r].export_voxels()), (i, r)
+    # the union of the ranks' fields is the single-volume field
+    parts = [v.export_bricks() for v in g]
+    keep = [(w.reshape(len(c), -1) > 0).any(1) for c, _, w in parts]
+    coords = np.concatenate([c[k] for (c, _, _), k in zip(parts, keep)])
+    assert len({tuple(x) for x in coords.tolist()}) == coords.shape[0]  # each brick once
+    mi, ms, mw = bricks_to_voxels(coords, np.concatenate([s[k] for (_, s, _), k in zip(parts, keep)]),
+                                  np.concatenate([w[k] for (_, _, w), k in zip(parts, keep)]))
+    ri, rs, rw = ref.export_voxels()
+    assert np.array_equal(mi, ri) and np.array_equal(mw, rw)
+    assert np.max(np.abs(ms - rs)) <= 1e-5
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out_dir):
+    import sys
+    for p in (os.path.join(REPO, "noetic-slam_amd"), os.path.join(REPO, "oracle")):
+        sys.path.insert(0, p)
+    import torch.distributed as dist
+    from tsdf_map import HipTSDFVolume
+    from tsdf_map.distributed import merged_bricks
+    from tsdf_map.scan_gen import OusterSim
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sim = OusterSim()
+    vol = HipTSDFVolume(VS, TAU, n_sectors=world, sector=rank, device_id=0)
+    for k in (0, 3):
+        vol.integrate(*sim.scan(k))
+    c, s, w = merged_bricks(vol, device="cpu")
+    np.savez(os.path.join(out_dir, "rank%d.npz" % rank), coords=c, sdf=s, weight=w)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_border_reduce_two_processes(tmp_path, sim):
+    import torch.multiprocessing as mp
+    from tsdf_map import bricks_to_voxels
+    world = 2
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+                       join=True, start_method="spawn")
+    parts = [np.load(str(tmp_path / ("rank%d.npz" % r))) for r in range(world)]
+    coords = np.concatenate([p["coords"] for p in parts])
+    assert len({tuple(x) for x in coords.tolist()}) == coords.shape[0]
+    mi, ms, mw = bricks_to_voxels(coords, np.concatenate([p["sdf"] for p in parts]),
+                                  np.concatenate([p["weight"] for p in parts]))
+    ref = ora()
+    for k in (0, 3):
+        ref.integrate(*sim.scan(k))
+    ri, rs, rw = ref.export_voxels()
+    assert np.array_equal(mi, ri) and np.array_equal(mw, rw)
+    assert np.max(np.abs(ms - rs)) <= 1e-5
