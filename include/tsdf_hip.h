@@ -93,6 +93,13 @@ typedef struct tsdf_params {
     uint32_t n_sectors;  /* 0 or 1: no sharding (default) */
     uint32_t sector;     /* 0 .. n_sectors - 1 */
     double sector_yaw0;  /* radians */
+    /* ABI v4: capacity growth.  max_bricks is the INITIAL pool; when a batch overflows the brick
+     * pool / hash table / work lists, the context grows them (x2 or more, up to max_bricks_hard
+     * bricks and device memory) and re-runs the batches from the failed one, so no update is lost
+     * (DESIGN.md §4b).  0 = no limit but device memory; max_bricks_hard == max_bricks = fixed
+     * capacity: an overflow then drops the updates that do not fit and tsdf_sync reports
+     * TSDF_ENOMEM. */
+    uint64_t max_bricks_hard;
 } tsdf_params;
 
 /* Batching.  Scans are integrated in call order and the field after any sequence of calls is
@@ -115,6 +122,10 @@ typedef struct tsdf_stats {
     uint64_t n_batches;        /* GPU batches launched since reset */
     double kernel_ms[8];       /* per-kernel-kind accumulated device time when profiling is on */
     uint64_t kernel_launches[8];
+    /* ABI v4 */
+    uint64_t n_grows;          /* capacity growths since create */
+    uint64_t n_replayed;       /* batches re-run after a growth since create */
+    uint64_t max_bricks;       /* current brick pool capacity */
 } tsdf_stats;
 
 /* kernel kinds reported in tsdf_stats.kernel_ms (profiling on) */
@@ -147,12 +158,15 @@ int tsdf_integrate_device(tsdf_ctx* ctx, const float* d_xyz, uint64_t n, const d
 
 /* n_scans scans in device memory, integrated in order, max_batch scans per GPU batch.  Scan s is
  * the points d_xyz[3*scan_offsets[s] .. 3*scan_offsets[s+1]) (offsets in points, host array of
- * n_scans+1) seen from origins[3*s .. 3*s+3) (host array).  d_xyz must stay valid until the
- * work completes (tsdf_sync). */
+ * n_scans+1) seen from origins[3*s .. 3*s+3) (host array).  d_xyz must stay valid and unchanged
+ * until the next tsdf_sync (or read-out call) returns: a batch that overflowed the capacity is
+ * re-run from it after growing (tsdf_params.max_bricks_hard). */
 int tsdf_integrate_batch_device(tsdf_ctx* ctx, const float* d_xyz, const uint64_t* scan_offsets,
                                 uint32_t n_scans, const double* origins);
 
-/* Block until all queued work finished; reports a deferred capacity overflow as TSDF_ENOMEM. */
+/* Block until all queued work finished (growing capacity and re-running overflowed batches first,
+ * see tsdf_params.max_bricks_hard); reports an overflow that could not be grown away as
+ * TSDF_ENOMEM. */
 int tsdf_sync(tsdf_ctx* ctx);
 
 /* Dense read-out of voxels lo..hi-1 (voxel index coordinates, voxel i spans [i*vs, (i+1)*vs)),

@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdarg>
+#include <cstddef>
 #include <cstdio>
 #include <cstring>
 #include <numeric>
@@ -116,6 +117,7 @@ struct tsdf_ctx {
     uint32_t max_batch = 0;
     uint64_t batch_points = 0;  // pair-slot capacity / maxp: points one batch may hold
     uint32_t max_blocks = 0;    // k_count / k_place workgroups one batch may need
+    uint64_t slots = 0;         // pair slots of one batch
     // host-pointer path: pinned double buffer per scan; the pending batch's points are staged in
     // stage2[batch parity]
     float* h_stage[2] = {nullptr, nullptr};
@@ -136,6 +138,14 @@ struct tsdf_ctx {
     uint64_t n_scans = 0, n_batches = 0, n_points_in = 0;
     EventTimer* timer = nullptr;
     std::string err;
+    // Capacity growth: batches launched since the last check, replayable from their
+    // still-valid input (caller device memory until tsdf_sync; host scans in stage2 until the
+    // staging of batch id + 2, where a checkpoint runs first).
+    struct Logged { uint64_t id; const float* xyz; BatchDesc D; };
+    std::vector<Logged> log;
+    bool can_grow = false;  // G->retry: overflowed batches are skipped and replayed
+    bool in_replay = false;
+    uint64_t n_grows = 0, n_replayed = 0;
 };
 
 static int fail(tsdf_ctx* c, int code, const char* fmt, ...) {
@@ -180,8 +190,17 @@ static uint32_t samples_per_ray(const tsdf_params& p) {
 }
 
 // Launch one batch (desc offsets relative to d_xyz); fills the workgroup prefix of D.
+static int check_and_replay(tsdf_ctx* c);
+static int drain_all(tsdf_ctx* c);
+
 static int launch(tsdf_ctx* c, const float* d_xyz, BatchDesc& D) {
     if (D.n_scans == 0) return TSDF_OK;
+    if (c->can_grow && !c->in_replay && c->log.size() >= 1024) {
+        // device-pointer batches stay replayable until a check: bound the log
+        int rc = drain_all(c);
+        if (!rc) rc = check_and_replay(c);
+        if (rc) return rc;
+    }
     D.blk[0] = 0;
     for (uint32_t s = 0; s < D.n_scans; s++)
         D.blk[s + 1] = D.blk[s] + (D.off[s + 1] - D.off[s] + RPB - 1) / RPB;
@@ -238,8 +257,9 @@ static int launch(tsdf_ctx* c, const float* d_xyz, BatchDesc& D) {
 #endif
         if (tm) tm->end(KIND_INTEGRATE, st);
     }
-    HIPCHK(c, launch_finish(c->G, par, st));
+    HIPCHK(c, launch_finish(c->G, par, (uint32_t)c->batch_id, st));
     HIPCHK(c, hipEventRecord(c->ev_integ[par], st));
+    if (c->can_grow) c->log.push_back({c->batch_id, d_xyz, D});
     c->batch_id++;
     c->n_batches++;
     c->n_scans += D.n_scans;
@@ -271,6 +291,230 @@ static int flush(tsdf_ctx* c) {
 static int settle(tsdf_ctx* c) {
     const int rc = flush(c);
     return rc ? rc : join(c);
+}
+
+// ---- capacity: brick pool, hash table and per-brick work lists -----------------
+
+struct Capacity {
+    uint64_t max_bricks = 0, cap = 0;
+    uint32_t max_active = 0;
+    uint64_t* keys = nullptr;
+    uint32_t* slots = nullptr;
+    uint32_t* touched = nullptr;
+    uint64_t* brick_keys = nullptr;
+    float* sdf = nullptr;
+    float* weight = nullptr;
+    uint32_t* cell[2] = {nullptr, nullptr};
+    uint4* active[2] = {nullptr, nullptr};
+    uint4* active_ord[2] = {nullptr, nullptr};
+    uint4* cagg[2] = {nullptr, nullptr};
+
+    void free_all() {
+        void* d[] = {keys, slots, touched, brick_keys, sdf, weight, cell[0], cell[1], active[0],
+                     active[1], active_ord[0], active_ord[1], cagg[0], cagg[1]};
+        for (void* q : d)
+            if (q) (void)hipFree(q);
+        *this = Capacity{};
+    }
+};
+
+// Allocate (and clear: empty table, zero cells) the capacity-dependent buffers for max_bricks bricks;
+// the pool's contents are the caller's.  Allocation failure is TSDF_ENOMEM with nothing leaked.
+static int alloc_capacity(tsdf_ctx* c, uint64_t max_bricks, Capacity& K) {
+    K = Capacity{};
+    K.max_bricks = max_bricks;
+    K.cap = next_pow2(2 * max_bricks);
+    K.max_active = (uint32_t)std::min<uint64_t>(K.cap, c->slots);
+    const size_t cells = K.cap * c->T.cell_stride * sizeof(uint32_t);
+    hipError_t e = hipMalloc(&K.keys, K.cap * sizeof(uint64_t));
+    if (e == hipSuccess) e = hipMalloc(&K.slots, K.cap * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc(&K.touched, K.cap * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc(&K.brick_keys, max_bricks * sizeof(uint64_t));
+    if (e == hipSuccess) e = hipMalloc(&K.sdf, max_bricks * BRICK_VOX * sizeof(float));
+    if (e == hipSuccess) e = hipMalloc(&K.weight, max_bricks * BRICK_VOX * sizeof(float));
+    for (int q = 0; q < 2 && e == hipSuccess; q++) {
+        e = hipMalloc(&K.cell[q], cells);
+        if (e == hipSuccess) e = hipMalloc(&K.active[q], (size_t)K.max_active * sizeof(uint4));
+        if (e == hipSuccess) e = hipMalloc(&K.active_ord[q], (size_t)K.max_active * sizeof(uint4));
+        if (e == hipSuccess) e = hipMalloc(&K.cagg[q], compact_chunks(K.cap) * 2 * sizeof(uint4));
+    }
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        K.free_all();
+        return fail(c, TSDF_ENOMEM, "device allocation for %llu bricks failed",
+                    (unsigned long long)max_bricks);
+    }
+    e = launch_fill_u64(K.keys, EMPTY_KEY, K.cap, c->stream);
+    if (e == hipSuccess) e = launch_fill_u32(K.slots, UNASSIGNED, K.cap, c->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(K.touched, 0, K.cap * sizeof(uint32_t), c->stream);
+    for (int q = 0; q < 2 && e == hipSuccess; q++) e = hipMemsetAsync(K.cell[q], 0, cells, c->stream);
+    if (e != hipSuccess) {
+        K.free_all();
+        return fail(c, TSDF_EHIP, "capacity init: %s", hipGetErrorString(e));
+    }
+    return TSDF_OK;
+}
+
+// Make K the context's capacity (the previous buffers are freed; K is emptied).
+static void install_capacity(tsdf_ctx* c, Capacity& K) {
+    Capacity old;
+    old.keys = c->T.keys; old.slots = c->T.slots; old.touched = c->T.touched;
+    old.brick_keys = c->T.brick_keys; old.sdf = c->Pl.sdf; old.weight = c->Pl.weight;
+    for (int q = 0; q < 2; q++) {
+        old.cell[q] = c->cell2[q];
+        old.active[q] = c->W2[q].active;
+        old.active_ord[q] = c->W2[q].active_ord;
+        old.cagg[q] = c->W2[q].cagg;
+    }
+    old.free_all();
+    c->cap = K.cap;
+    c->T.keys = K.keys; c->T.slots = K.slots; c->T.touched = K.touched;
+    c->T.brick_keys = K.brick_keys;
+    c->T.mask = K.cap - 1;
+    c->T.max_bricks = (uint32_t)K.max_bricks;
+    c->T.cell = K.cell[0];
+    c->Pl.sdf = K.sdf; c->Pl.weight = K.weight;
+    c->Wk.max_active = K.max_active;
+    for (int q = 0; q < 2; q++) {
+        c->cell2[q] = K.cell[q];
+        c->W2[q].active = K.active[q];
+        c->W2[q].active_ord = K.active_ord[q];
+        c->W2[q].cagg = K.cagg[q];
+        c->W2[q].max_active = K.max_active;
+    }
+    K = Capacity{};
+}
+
+// Grow the pool (and table, cells, lists) to hold at least `need` bricks: x2 or more, capped by
+// max_bricks_hard.  Every batch must be complete.  The pool keeps its bricks (same slots); the
+// table is rebuilt from the slot -> key map.  TSDF_ENOMEM: no growth possible.
+static int grow_capacity(tsdf_ctx* c, uint64_t need) {
+    const uint64_t old = c->T.max_bricks;
+    uint64_t nb = std::max<uint64_t>(2 * old, need + need / 4);
+    if (c->p.max_bricks_hard) nb = std::min<uint64_t>(nb, c->p.max_bricks_hard);
+    nb = std::min<uint64_t>(nb, 0xFFFFFFEFull);
+    if (nb <= old) return fail(c, TSDF_ENOMEM, "brick pool at its hard limit (%llu bricks)",
+                               (unsigned long long)old);
+    uint32_t pc = 0;
+    HIPCHK(c, hipMemcpy(&pc, &c->G->pool_count, 4, hipMemcpyDeviceToHost));
+    const uint64_t valid = std::min<uint64_t>(pc, old);
+    Capacity K;
+    int rc = alloc_capacity(c, nb, K);
+    if (rc) return rc;
+    hipError_t e = hipSuccess;
+    if (valid) {
+        e = hipMemcpyAsync(K.sdf, c->Pl.sdf, valid * BRICK_VOX * 4, hipMemcpyDeviceToDevice, c->stream);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(K.weight, c->Pl.weight, valid * BRICK_VOX * 4, hipMemcpyDeviceToDevice,
+                               c->stream);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(K.brick_keys, c->T.brick_keys, valid * 8, hipMemcpyDeviceToDevice,
+                               c->stream);
+    }
+    if (e == hipSuccess) e = launch_fill(K.sdf + valid * BRICK_VOX, c->R.bg, (nb - valid) * BRICK_VOX, c->stream);
+    if (e == hipSuccess)
+        e = hipMemsetAsync(K.weight + valid * BRICK_VOX, 0, (nb - valid) * BRICK_VOX * 4, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);  // the old pool is read before the free
+    if (e != hipSuccess) {
+        K.free_all();
+        return fail(c, TSDF_EHIP, "grow: %s", hipGetErrorString(e));
+    }
+    install_capacity(c, K);
+    HIPCHK(c, launch_rehash(c->T, (uint32_t)valid, c->G, c->stream));
+    // the failed batches' counters and flags go; the pool keeps its valid bricks
+    const uint32_t pcv = (uint32_t)valid;
+    HIPCHK(c, hipMemsetAsync(c->G, 0, offsetof(Globals, tot_vox), c->stream));
+    HIPCHK(c, hipMemcpyAsync(&c->G->pool_count, &pcv, 4, hipMemcpyHostToDevice, c->stream));
+    const uint32_t retry = 1u;
+    HIPCHK(c, hipMemcpyAsync(&c->G->retry, &retry, 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->n_grows++;
+    return TSDF_OK;
+}
+
+// Double the fallback-pair lists (OVF_FB) of both batch parities, up to the 26-bit index space.
+static int grow_fb(tsdf_ctx* c) {
+    const uint64_t nf = std::min<uint64_t>(2ull * c->Wk.max_fb, 1ull << 26);
+    if (nf <= c->Wk.max_fb) return fail(c, TSDF_ENOMEM, "fallback pair list at its limit");
+    uint4* f[2] = {nullptr, nullptr};
+    hipError_t e = hipMalloc(&f[0], nf * sizeof(uint4));
+    if (e == hipSuccess) e = hipMalloc(&f[1], nf * sizeof(uint4));
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        for (auto q : f) if (q) (void)hipFree(q);
+        return fail(c, TSDF_ENOMEM, "fallback pair list allocation failed");
+    }
+    for (int q = 0; q < 2; q++) {
+        (void)hipFree(c->W2[q].fb);
+        c->W2[q].fb = f[q];
+        c->W2[q].max_fb = (uint32_t)nf;
+    }
+    c->Wk.max_fb = (uint32_t)nf;
+    return TSDF_OK;
+}
+
+// Every launched batch complete: the context stream waits for them and drains.
+static int drain_all(tsdf_ctx* c) {
+    int rc = join(c);
+    if (rc) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return TSDF_OK;
+}
+
+// With every batch complete: if a batch overflowed, grow the capacity it lacked and re-run the
+// batches from it (their inputs are still valid), until a round succeeds.  Without growth (hard
+// limit, or a non-growable overflow) the batches are re-run committing what fits, and tsdf_sync
+// reports the overflow.
+static int check_and_replay(tsdf_ctx* c) {
+    for (int round = 0; round < 64; round++) {
+        struct { uint32_t pool_count, overflow, failed, retry, fail_id; } g;
+        HIPCHK(c, hipMemcpy(&g, c->G, sizeof g, hipMemcpyDeviceToHost));
+        if (!g.failed) {
+            c->log.clear();
+            return TSDF_OK;
+        }
+        if (!c->can_grow) {  // committed anyway (G->retry = 0): the overflow stays for tsdf_sync
+            const uint32_t z[2] = {0u, 0u};
+            HIPCHK(c, hipMemcpy(&c->G->failed, z, 4, hipMemcpyHostToDevice));
+            c->log.clear();
+            return TSDF_OK;
+        }
+        int rc = TSDF_ENOMEM;
+        if (!(g.overflow & OVF_PAIRS)) {  // pair slots per ray are a geometric bound, not a capacity
+            rc = TSDF_OK;
+            if (g.overflow & (OVF_TABLE | OVF_POOL | OVF_ACTIVE))
+                rc = grow_capacity(c, std::max<uint64_t>(g.pool_count, c->T.max_bricks + 1));
+            if (rc == TSDF_OK && (g.overflow & OVF_FB)) rc = grow_fb(c);
+            if (rc == TSDF_EHIP) return rc;
+        }
+        // the replay: from the first failed batch on, in order
+        size_t first = 0;
+        while (first < c->log.size() && (uint32_t)c->log[first].id != g.fail_id) first++;
+        if (first == c->log.size()) first = 0;
+        std::vector<tsdf_ctx::Logged> rep(c->log.begin() + first, c->log.end());
+        c->log.clear();
+        if (rc != TSDF_OK) {  // cannot grow: commit what fits from now on
+            c->can_grow = false;
+            const uint32_t z[2] = {0u, 0u};  // failed, retry
+            HIPCHK(c, hipMemcpy(&c->G->failed, z, 8, hipMemcpyHostToDevice));
+        } else {
+            const uint32_t z = 0u;
+            HIPCHK(c, hipMemcpy(&c->G->failed, &z, 4, hipMemcpyHostToDevice));
+        }
+        c->in_replay = true;
+        for (auto& L : rep) {
+            c->n_scans -= L.D.n_scans;
+            c->n_batches--;
+            c->n_replayed++;
+            rc = launch(c, L.xyz, L.D);
+            if (rc) break;
+        }
+        c->in_replay = false;
+        if (rc) return rc;
+        rc = drain_all(c);
+        if (rc) return rc;
+    }
+    return fail(c, TSDF_ENOMEM, "capacity growth did not converge");
 }
 
 // Marching-cubes case table, generated (the same construction as the oracle's
@@ -477,12 +721,9 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
     c->max_points = p->max_points;
     c->batch_points = bp;
     const uint64_t slots = bp * maxp;
-    c->cap = next_pow2(2 * p->max_bricks);
-    c->T.mask = c->cap - 1;
-    c->T.max_bricks = (uint32_t)p->max_bricks;
+    c->slots = slots;
     c->T.cell_stride = (c->max_batch + 3u) & ~3u;
     c->Wk.maxp = maxp;
-    c->Wk.max_active = (uint32_t)std::min<uint64_t>(c->cap, slots);
     c->Wk.max_smp = (uint32_t)std::min<uint64_t>(bp * spr, 0xFFFFFFF0ull);
     // fallback pairs (a workgroup's LDS brick hash is full): rare without carving, the rule with it
     // (the fallback index has 26 bits; past it pairs are dropped and OVF_FB reported)
@@ -490,44 +731,39 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
         p->space_carving ? slots : std::max<uint64_t>(slots / 16, 1u << 20), 1u << 26);
     c->max_blocks = (uint32_t)(c->batch_points / RPB + MAX_BATCH + 1);
 
-    HIPCHK(c, hipMalloc(&c->T.keys, c->cap * sizeof(uint64_t)));
-    HIPCHK(c, hipMalloc(&c->T.slots, c->cap * sizeof(uint32_t)));
-    HIPCHK(c, hipMalloc(&c->T.touched, c->cap * sizeof(uint32_t)));
-    HIPCHK(c, hipMemsetAsync(c->T.touched, 0, c->cap * sizeof(uint32_t), c->stream));
-    HIPCHK(c, hipMalloc(&c->T.brick_keys, p->max_bricks * sizeof(uint64_t)));
-    HIPCHK(c, hipMalloc(&c->Pl.sdf, p->max_bricks * BRICK_VOX * sizeof(float)));
-    HIPCHK(c, hipMalloc(&c->Pl.weight, p->max_bricks * BRICK_VOX * sizeof(float)));
-    for (int q = 0; q < 2; q++) {  // one set per batch parity
+    for (int q = 0; q < 2; q++) {  // one set per batch parity (capacity-independent part)
         Work& W = c->W2[q];
-        W = c->Wk;  // capacities
+        W = c->Wk;
         HIPCHK(c, hipMalloc(&W.pair, slots * sizeof(uint32_t)));
         HIPCHK(c, hipMalloc(&W.blk, (size_t)c->max_blocks * 2 * HCAP * sizeof(uint4)));
         HIPCHK(c, hipMalloc(&W.blk_n, (size_t)c->max_blocks * 2 * sizeof(uint32_t)));
         HIPCHK(c, hipMalloc(&W.fb, (size_t)W.max_fb * sizeof(uint4)));
         HIPCHK(c, hipMalloc(&W.smp, (size_t)W.max_smp * sizeof(uint2)));
-        HIPCHK(c, hipMalloc(&W.active, (size_t)W.max_active * sizeof(uint4)));
-        HIPCHK(c, hipMalloc(&W.active_ord, (size_t)W.max_active * sizeof(uint4)));
         HIPCHK(c, hipMalloc(&W.ord_hist, 64 * 32 * sizeof(uint32_t)));
-        HIPCHK(c, hipMalloc(&W.cagg, compact_chunks(c->cap) * 2 * sizeof(uint4)));
-        HIPCHK(c, hipMalloc(&c->cell2[q], c->cap * c->T.cell_stride * sizeof(uint32_t)));
-        HIPCHK(c, hipMemsetAsync(c->cell2[q], 0, c->cap * c->T.cell_stride * sizeof(uint32_t),
-                                 c->stream));
         HIPCHK(c, hipMalloc(&c->stage2[q], c->batch_points * 3 * sizeof(float)));
     }
-    c->T.cell = c->cell2[0];
     HIPCHK(c, hipMalloc(&c->G, sizeof(Globals)));
+    HIPCHK(c, hipMemsetAsync(c->G, 0, sizeof(Globals), c->stream));
+    // the brick pool, hash table and per-brick work lists (grown later by grow_capacity)
+    {
+        Capacity K;
+        const int rc = alloc_capacity(c, p->max_bricks, K);
+        if (rc) return rc;
+        HIPCHK(c, launch_fill(K.sdf, c->R.bg, p->max_bricks * BRICK_VOX, c->stream));
+        HIPCHK(c, hipMemsetAsync(K.weight, 0, p->max_bricks * BRICK_VOX * sizeof(float), c->stream));
+        install_capacity(c, K);
+    }
+    c->T.cell = c->cell2[0];
     for (int i = 0; i < 2; i++) {
         HIPCHK(c, hipHostMalloc(&c->h_stage[i], c->max_points * 3 * sizeof(float),
                                 hipHostMallocDefault));
         HIPCHK(c, hipEventCreateWithFlags(&c->stage_done[i], hipEventDisableTiming));
     }
-    // background: (sdf_trunc, 0) VDBFusion, (0, 0) Voxblox TsdfVoxel
-    HIPCHK(c, launch_fill_u64(c->T.keys, EMPTY_KEY, c->cap, c->stream));
-    HIPCHK(c, launch_fill_u32(c->T.slots, UNASSIGNED, c->cap, c->stream));
-    HIPCHK(c, launch_fill(c->Pl.sdf, c->R.bg, p->max_bricks * BRICK_VOX, c->stream));
-    HIPCHK(c, hipMemsetAsync(c->Pl.weight, 0, p->max_bricks * BRICK_VOX * sizeof(float),
-                             c->stream));
-    HIPCHK(c, hipMemsetAsync(c->G, 0, sizeof(Globals), c->stream));
+    c->can_grow = p->max_bricks_hard == 0 || p->max_bricks_hard > p->max_bricks;
+    {
+        const uint32_t retry = c->can_grow ? 1u : 0u;
+        HIPCHK(c, hipMemcpyAsync(&c->G->retry, &retry, 4, hipMemcpyHostToDevice, c->stream));
+    }
     HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, upload_mc_table(mc_table().tab, mc_table().edge));
     return TSDF_OK;
@@ -542,7 +778,8 @@ int tsdf_create(const tsdf_params* p, tsdf_ctx** out) {
         !(p->max_range > p->min_range) || p->max_batch == 0 || p->max_batch > TSDF_MAX_BATCH ||
         (p->semantics != TSDF_SEM_VDBFUSION && p->semantics != TSDF_SEM_VOXBLOX) ||
         (p->semantics == TSDF_SEM_VOXBLOX && !(p->max_weight > 0.0f)) ||
-        (p->n_sectors > 1 && p->sector >= p->n_sectors) || !std::isfinite(p->sector_yaw0))
+        (p->n_sectors > 1 && p->sector >= p->n_sectors) || !std::isfinite(p->sector_yaw0) ||
+        (p->max_bricks_hard && p->max_bricks_hard < p->max_bricks))
         return TSDF_EINVAL;
     if (p->space_carving && !std::isfinite(p->max_range)) return TSDF_EINVAL;
     tsdf_ctx* c = new (std::nothrow) tsdf_ctx();
@@ -601,9 +838,28 @@ int tsdf_integrate(tsdf_ctx* c, const void* pts, uint64_t n, uint32_t point_step
     }
     BatchDesc& D = c->pend;
     const uint32_t s = D.n_scans;
-    const int sp = (int)(c->batch_id & 1);  // the pending batch's parity
-    if (s == 0 && c->batch_id >= 2)  // stage2[sp] was last read by batch batch_id - 2
-        HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_integ[sp], 0));
+    if (s == 0 && c->batch_id >= 2) {  // stage2[batch_id & 1] was last read by batch batch_id - 2
+        const int sp = (int)(c->batch_id & 1);
+        if (c->can_grow) {
+            // checkpoint: batch batch_id - 2 must have committed before its staged input goes
+            // (an overflowed batch is re-run from it after growing)
+            HIPCHK(c, hipEventSynchronize(c->ev_integ[sp]));
+            uint32_t failed = 0;
+            HIPCHK(c, hipMemcpy(&failed, &c->G->failed, 4, hipMemcpyDeviceToHost));
+            if (failed) {
+                int rc = drain_all(c);
+                if (!rc) rc = check_and_replay(c);
+                if (rc) return rc;
+            } else {
+                const uint64_t done = c->batch_id - 2;
+                size_t k = 0;
+                while (k < c->log.size() && c->log[k].id <= done) k++;
+                c->log.erase(c->log.begin(), c->log.begin() + k);
+            }
+        }
+        HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_integ[c->batch_id & 1], 0));
+    }
+    const int sp = (int)(c->batch_id & 1);  // the pending batch's parity (after any replay)
     if (n) {
         HIPCHK(c, hipMemcpyAsync(c->stage2[sp] + 3 * (uint64_t)D.off[s], h, n * 12,
                                  hipMemcpyHostToDevice, c->stream));
@@ -661,9 +917,11 @@ int tsdf_integrate_device(tsdf_ctx* c, const float* d_xyz, uint64_t n, const dou
 int tsdf_sync(tsdf_ctx* c) {
     if (!c) return TSDF_EINVAL;
     HIPCHK(c, hipSetDevice(c->device));
-    const int rc = settle(c);
+    int rc = settle(c);
     if (rc) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    rc = check_and_replay(c);
+    if (rc) return rc;
     if (c->timer) c->timer->harvest();
     uint32_t ovf = 0;
     HIPCHK(c, hipMemcpy(&ovf, &c->G->overflow, sizeof ovf, hipMemcpyDeviceToHost));
@@ -683,9 +941,11 @@ int tsdf_sync(tsdf_ctx* c) {
 // flush + drain, ignoring (but keeping) the overflow flag for read-out calls
 static int drain(tsdf_ctx* c) {
     HIPCHK(c, hipSetDevice(c->device));
-    const int rc = settle(c);
+    int rc = settle(c);
     if (rc) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    rc = check_and_replay(c);
+    if (rc) return rc;
     if (c->timer) c->timer->harvest();
     return TSDF_OK;
 }
@@ -722,7 +982,7 @@ static int pool_bricks(tsdf_ctx* c, uint64_t* n) {
     if (rc) return rc;
     uint32_t pc = 0;
     HIPCHK(c, hipMemcpy(&pc, &c->G->pool_count, sizeof pc, hipMemcpyDeviceToHost));
-    *n = std::min<uint64_t>(pc, c->p.max_bricks);
+    *n = std::min<uint64_t>(pc, c->T.max_bricks);
     return TSDF_OK;
 }
 
@@ -943,6 +1203,14 @@ int tsdf_import_bricks(tsdf_ctx* c, const int32_t* coords, const float* sdf, con
     }
     int rc = drain(c);
     if (rc) return rc;
+    {  // room for n new bricks (import is not a replayable batch: grow first)
+        uint32_t pc = 0;
+        HIPCHK(c, hipMemcpy(&pc, &c->G->pool_count, 4, hipMemcpyDeviceToHost));
+        if (c->can_grow && (uint64_t)pc + n > c->T.max_bricks) {
+            rc = grow_capacity(c, (uint64_t)pc + n);
+            if (rc == TSDF_EHIP) return rc;
+        }
+    }
     int32_t* dc = nullptr;
     float *ds = nullptr, *dw = nullptr;
     uint32_t* dt = nullptr;
@@ -975,7 +1243,10 @@ int tsdf_get_stats(tsdf_ctx* c, tsdf_stats* out) {
     out->n_scans = c->n_scans;
     out->n_batches = c->n_batches;
     out->n_points_in = c->n_points_in;
-    out->n_bricks = std::min<uint64_t>(g.pool_count, c->p.max_bricks);
+    out->n_bricks = std::min<uint64_t>(g.pool_count, c->T.max_bricks);
+    out->n_grows = c->n_grows;
+    out->n_replayed = c->n_replayed;
+    out->max_bricks = c->T.max_bricks;
     if (c->batch_id) {
         const Counters& L = g.last;
         out->n_active_last = L.n_active;

@@ -155,7 +155,7 @@ struct Counters {
     uint32_t n_active;
     uint32_t cursor;
     uint32_t n_fb;
-    uint32_t pad0;
+    uint32_t ovf;  // OVF_* raised by this batch's kernels
     unsigned long long n_vox[8];    // sum over scans of U_vox, sharded by blockIdx & 7
     unsigned long long n_rays[8];   // valid rays
     unsigned long long n_pairs[8];
@@ -163,10 +163,16 @@ struct Counters {
 };
 
 // persistent device globals (one allocation, zeroed at create)
+// Capacity growth: with `retry` set (the context can still grow), a batch that
+// raised an overflow — or any batch after it — does not commit: k_integrate skips its field writes
+// and k_finish its stats, so the host can grow the buffers and replay the batches from `fail_id`.
 struct Globals {
     uint32_t pool_count;
-    uint32_t overflow;
-    uint32_t pad[2];
+    uint32_t overflow;  // OVF_* of every batch since the host's last check (sticky)
+    uint32_t failed;    // a batch raised an overflow since the host's last check
+    uint32_t retry;     // host: failed batches will be replayed (skip their writes)
+    uint32_t fail_id;   // host batch id of the first failed batch
+    uint32_t pad[3];
     Counters ctr[2];
     unsigned long long tot_vox[8];  // running totals since the last stats reset (sharded)
     unsigned long long tot_rays[8];
@@ -193,7 +199,9 @@ hipError_t launch_compact(const BatchDesc& D, const Table& T, const Work& Wk, Gl
                           int parity, hipStream_t st);
 hipError_t launch_place(const float* d_xyz, const BatchDesc& D, const RayConst& R, const Table& T,
                         const Work& Wk, hipStream_t st);
-hipError_t launch_finish(Globals* G, int parity, hipStream_t st);
+hipError_t launch_finish(Globals* G, int parity, uint32_t batch_id, hipStream_t st);
+// capacity growth: re-insert pool slots [0, n) of the new table from brick_keys
+hipError_t launch_rehash(const Table& T, uint32_t n, Globals* G, hipStream_t st);
 // Orders the batch's active bricks by size class, largest first (k_integrate's load balance).
 hipError_t launch_order(const Work& Wk, Globals* G, int parity, hipStream_t st);
 hipError_t launch_integrate(const BatchDesc& D, const RayConst& R, const Table& T, const Work& Wk,

@@ -90,6 +90,9 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchDesc D, Table T,
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const uint32_t n_active = min(C->n_active, Wk.max_active);
     const uint32_t ns = D.n_scans;
+    // a batch that overflowed (or follows one) is replayed after the host grows the buffers: its
+    // field writes are skipped, everything else (cell clean-up) runs
+    const bool commit = !(G->retry && (C->ovf || G->failed));
     sMask[tid] = 0;
     sMask[tid + 256] = 0;
     uint32_t nvox = 0, ndirty = 0, par = 0;
@@ -397,7 +400,7 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchDesc D, Table T,
             PHASE(6);
             t0 = t1;
         }
-        if (has_slot) {
+        if (has_slot && commit) {
             if (dirty & 1u) {
                 Sg[2 * tid] = sS[2 * tid];
                 Wg[2 * tid] = sW[2 * tid];
@@ -432,14 +435,8 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchDesc D, Table T,
     const unsigned long long v = wave_sum<unsigned long long>(nvox);
     const unsigned long long d = wave_sum<unsigned long long>(ndirty);
     if (lane == 0) {
-        if (v) {
-            atomicAdd(&C->n_vox[blockIdx.x & 7], v);
-            atomicAdd(&G->tot_vox[blockIdx.x & 7], v);
-        }
-        if (d) {
-            atomicAdd(&C->n_dirty[blockIdx.x & 7], d);
-            atomicAdd(&G->tot_dirty[blockIdx.x & 7], d);
-        }
+        if (v) atomicAdd(&C->n_vox[blockIdx.x & 7], v);  // -> G->tot_vox at k_finish
+        if (d) atomicAdd(&C->n_dirty[blockIdx.x & 7], d);
     }
 }
 

@@ -109,10 +109,10 @@ __global__ __launch_bounds__(CNT_THREADS) void k_count(const float* __restrict__
         }
         const uint32_t f = atomicAdd(&C->n_fb, 1u);  // LDS hash full: the global path
         if (f >= Wk.max_fb) {
-            atomicOr(&G->overflow, OVF_FB);
+            atomicOr(&C->ovf, OVF_FB);
             return PAIR_DEAD;
         }
-        const int64_t hx = table_insert(T, bkey, &G->overflow);
+        const int64_t hx = table_insert(T, bkey, &C->ovf);
         if (hx < 0) return PAIR_DEAD;
         const uint32_t h = (uint32_t)hx;
         T.touched[h] = 1u;
@@ -174,7 +174,7 @@ __global__ __launch_bounds__(CNT_THREADS) void k_count(const float* __restrict__
                     np++;
                 }
             }
-            if (np > maxp) atomicOr(&G->overflow, OVF_PAIRS);  // beyond the geometric bound
+            if (np > maxp) atomicOr(&C->ovf, OVF_PAIRS);  // beyond the geometric bound
             k = min(np, maxp);
             uint4 code = make_uint4(NO_PAIR, NO_PAIR, NO_PAIR, NO_PAIR);
             const uint32_t hf = i - r0 >= (uint32_t)(RPB / 2) ? 1u : 0u;
@@ -196,7 +196,7 @@ __global__ __launch_bounds__(CNT_THREADS) void k_count(const float* __restrict__
                 uint32_t curc = ~0u, ccount = 0;
                 auto emit = [&](uint64_t bkey, uint32_t cnt_in) {
                     if (k >= maxp) {
-                        atomicOr(&G->overflow, OVF_PAIRS);
+                        atomicOr(&C->ovf, OVF_PAIRS);
                         return;
                     }
                     pc[k++] = pair_code(bkey, cnt_in, i - r0 >= (uint32_t)(RPB / 2) ? 1u : 0u);
@@ -282,7 +282,7 @@ __global__ __launch_bounds__(CNT_THREADS) void k_count(const float* __restrict__
     for (int j = 0; j < SPT; j++) {
         hx[j] = -1;
         if (key[j] != EMPTY_KEY)
-            hx[j] = k0[j] == key[j] ? (int64_t)h0[j] : table_insert(T, key[j], &G->overflow);
+            hx[j] = k0[j] == key[j] ? (int64_t)h0[j] : table_insert(T, key[j], &C->ovf);
     }
     uint32_t old[SPT];
 #pragma unroll
@@ -328,14 +328,8 @@ __global__ __launch_bounds__(CNT_THREADS) void k_count(const float* __restrict__
         v = 0;
         q = 0;
         for (int w = 0; w < CNT_THREADS / 64; w++) { v += red[0][w]; q += red[1][w]; }
-        if (v) {
-            atomicAdd(&C->n_rays[blockIdx.x & 7], v);
-            atomicAdd(&G->tot_rays[blockIdx.x & 7], v);
-        }
-        if (q) {
-            atomicAdd(&C->n_pairs[blockIdx.x & 7], q);
-            atomicAdd(&G->tot_pairs[blockIdx.x & 7], q);
-        }
+        if (v) atomicAdd(&C->n_rays[blockIdx.x & 7], v);  // -> G->tot_rays at k_finish
+        if (q) atomicAdd(&C->n_pairs[blockIdx.x & 7], q);
     }
 }
 
@@ -460,13 +454,14 @@ __global__ __launch_bounds__(CMP_SCAN_THREADS) void k_compact_scan(uint32_t nch,
         C->n_active = s_carry[0];
         C->cursor = s_carry[1];
         G->pool_count = s_carry[2];
-        if (s_carry[1] > Wk.max_smp) atomicOr(&G->overflow, OVF_PAIRS);
-        if (s_carry[0] > Wk.max_active) atomicOr(&G->overflow, OVF_ACTIVE);
+        if (s_carry[1] > Wk.max_smp) atomicOr(&C->ovf, OVF_PAIRS);
+        if (s_carry[0] > Wk.max_active) atomicOr(&C->ovf, OVF_ACTIVE);
     }
 }
 
 __global__ __launch_bounds__(CMP_THREADS) void k_compact_write(uint32_t n_scans, uint32_t nch,
-                                                               Table T, Work Wk, Globals* G) {
+                                                               Table T, Work Wk, Globals* G,
+                                                               int parity) {
     __shared__ uint32_t s_w[CMP_THREADS / 64];
     __shared__ uint32_t s_h[CMP_CHUNK];
     __shared__ uint32_t s_n[CMP_CHUNK];  // the bricks' samples, then their segment starts
@@ -509,7 +504,7 @@ __global__ __launch_bounds__(CMP_THREADS) void k_compact_write(uint32_t n_scans,
                     T.brick_keys[slot] = T.keys[h];
                 } else {
                     slot = INVALID_SLOT;
-                    atomicOr(&G->overflow, OVF_POOL);
+                    atomicOr(&G->ctr[parity].ovf, OVF_POOL);
                 }
                 T.slots[h] = slot;
             }
@@ -911,7 +906,7 @@ hipError_t launch_compact(const BatchDesc& D, const Table& T, const Work& Wk, Gl
     const uint32_t nch = (uint32_t)compact_chunks(T.mask + 1);
     k_compact_sum<<<nch, CMP_THREADS, 0, st>>>(D.n_scans, T, Wk);
     k_compact_scan<<<1, CMP_SCAN_THREADS, 0, st>>>(nch, Wk, G, parity);
-    k_compact_write<<<nch, CMP_THREADS, 0, st>>>(D.n_scans, nch, T, Wk, G);
+    k_compact_write<<<nch, CMP_THREADS, 0, st>>>(D.n_scans, nch, T, Wk, G, parity);
     return hipGetLastError();
 }
 
@@ -1008,11 +1003,33 @@ hipError_t launch_order(const Work& Wk, Globals* G, int parity, hipStream_t st) 
     return hipGetLastError();
 }
 
-// End of a batch: keep its counters as the "last batch" snapshot and zero them for the next batch
-// of the same parity (the same stream, so ordered after every reader of this batch).
-__global__ void k_finish(Globals* G, int parity) {
+// End of a batch: fold its counters into the running totals (if it committed), keep them as the
+// "last batch" snapshot and zero them for the next batch of the same parity (the same stream, so
+// ordered after every reader of this batch).  A batch that raised an overflow marks the context
+// failed (its id kept for the host's replay); with G->retry, it and every later batch until the
+// host's check do not commit.
+__global__ void k_finish(Globals* G, int parity, uint32_t batch_id) {
     constexpr int NW = sizeof(Counters) / 4;
-    uint32_t* src = reinterpret_cast<uint32_t*>(&G->ctr[parity]);
+    Counters* C = &G->ctr[parity];
+    const uint32_t ovf = C->ovf, failed = G->failed;
+    const bool commit = !(G->retry && (ovf || failed));
+    __syncthreads();  // every lane read the flags before lane 0 updates them
+    if (threadIdx.x < 8 && commit) {
+        const int k = threadIdx.x;
+        G->tot_rays[k] += C->n_rays[k];
+        G->tot_pairs[k] += C->n_pairs[k];
+        G->tot_vox[k] += C->n_vox[k];
+        G->tot_dirty[k] += C->n_dirty[k];
+    }
+    if (threadIdx.x == 0 && ovf) {
+        G->overflow |= ovf;
+        if (!failed) {
+            G->failed = 1u;
+            G->fail_id = batch_id;
+        }
+    }
+    __syncthreads();
+    uint32_t* src = reinterpret_cast<uint32_t*>(C);
     uint32_t* dst = reinterpret_cast<uint32_t*>(&G->last);
     for (int j = threadIdx.x; j < NW; j += blockDim.x) {
         dst[j] = src[j];
@@ -1020,8 +1037,23 @@ __global__ void k_finish(Globals* G, int parity) {
     }
 }
 
-hipError_t launch_finish(Globals* G, int parity, hipStream_t st) {
-    k_finish<<<1, 64, 0, st>>>(G, parity);
+hipError_t launch_finish(Globals* G, int parity, uint32_t batch_id, hipStream_t st) {
+    k_finish<<<1, 64, 0, st>>>(G, parity, batch_id);
+    return hipGetLastError();
+}
+
+// Capacity growth: the grown table is rebuilt from the pool's slot -> key map (bricks the failed
+// batch inserted without a slot are dropped; the replay inserts them again).
+__global__ void k_rehash(Table T, uint32_t n, Globals* G) {
+    for (uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x; slot < n;
+         slot += gridDim.x * blockDim.x) {
+        const int64_t h = table_insert(T, T.brick_keys[slot], &G->overflow);
+        if (h >= 0) T.slots[h] = slot;
+    }
+}
+
+hipError_t launch_rehash(const Table& T, uint32_t n, Globals* G, hipStream_t st) {
+    if (n) k_rehash<<<grid_for(n, 256, 4096), 256, 0, st>>>(T, n, G);
     return hipGetLastError();
 }
 

@@ -50,6 +50,7 @@ class TsdfParams(C.Structure):
         ("n_sectors", C.c_uint32),
         ("sector", C.c_uint32),
         ("sector_yaw0", C.c_double),
+        ("max_bricks_hard", C.c_uint64),
     ]
 
 
@@ -67,6 +68,10 @@ class TsdfStats(C.Structure):
         ("n_batches", C.c_uint64),
         ("kernel_ms", C.c_double * 8),
         ("kernel_launches", C.c_uint64 * 8),
+        # ABI v4
+        ("n_grows", C.c_uint64),
+        ("n_replayed", C.c_uint64),
+        ("max_bricks", C.c_uint64),
     ]
 
     def as_dict(self):
@@ -154,7 +159,7 @@ def default_params(lib=None, **kw):
         p.max_bricks, p.max_points, p.max_pairs = 1 << 20, 1 << 18, 0
         p.device_id, p.brick_side, p.max_batch = 0, BRICK_SIDE, 32
         p.semantics, p.allow_clear, p.use_weight_dropoff, p.max_weight = SEM_VDBFUSION, 1, 1, 1e4
-        p.n_sectors, p.sector, p.sector_yaw0 = 0, 0, 0.0
+        p.n_sectors, p.sector, p.sector_yaw0, p.max_bricks_hard = 0, 0, 0.0, 0
     for k, v in kw.items():
         if not hasattr(p, k):
             raise TypeError("unknown tsdf_params field %r" % k)

@@ -330,7 +330,7 @@ def test_sector_shards_merge_to_single_gpu_field(scan0):
 def test_pool_exhaustion_reports_enomem(scan0):
     from tsdf_map import TsdfError
     from tsdf_map import _abi
-    g = hip(max_bricks=64)
+    g = hip(max_bricks=64, max_bricks_hard=64)  # fixed capacity: no growth
     g.integrate(*scan0)
     with pytest.raises(TsdfError) as e:
         g.sync()

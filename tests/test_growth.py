@@ -1,0 +1,105 @@
+"""Capacity growth with batch replay (SURVEY §5 failure row): a context that starts
+with a brick pool far too small grows its pool / hash table / work lists when a batch overflows and
+re-runs the batches from the failed one, so the field ends BIT-EXACT to the oracle's and no
+TSDF_ENOMEM is raised.  A fixed capacity (max_bricks_hard == max_bricks) keeps the old contract
+(tests/test_gpu_parity.py::test_pool_exhaustion_reports_enomem)."""
+import numpy as np
+import pytest
+
+import oracle
+from conftest import decimate
+
+pytestmark = pytest.mark.gpu
+
+VS, TAU = 0.05, 0.15
+
+
+def hip(**kw):
+    from tsdf_map import HipTSDFVolume
+    return HipTSDFVolume(kw.pop("voxel_size", VS), kw.pop("sdf_trunc", TAU), **kw)
+
+
+def ora(**kw):
+    kw.pop("max_batch", None)
+    kw.pop("pipeline", None)
+    return oracle.OracleTSDFVolume(kw.pop("voxel_size", VS), kw.pop("sdf_trunc", TAU), **kw)
+
+
+def bitwise(g, o):
+    gi, gs, gw = g.export_voxels()
+    oi, os_, ow = o.export_voxels()
+    return (gi.shape == oi.shape and np.array_equal(gi, oi) and np.array_equal(gw, ow)
+            and np.array_equal(gs.view(np.uint32), os_.view(np.uint32)))
+
+
+def test_full_c1_scan_from_64_bricks(scan0):
+    g = hip(max_bricks=64)
+    g.integrate(*scan0)
+    g.sync()  # no TSDF_ENOMEM
+    o = ora()
+    o.integrate(*scan0)
+    assert bitwise(g, o)
+    st = g.stats()
+    assert st["n_grows"] >= 1 and st["n_replayed"] >= 1
+    assert st["n_bricks"] == o.num_bricks() <= st["max_bricks"]
+    assert st["n_rays_total"] == scan0[0].shape[0]  # replayed batches are counted once
+
+
+@pytest.mark.parametrize("pipeline", [False, True])
+@pytest.mark.parametrize("semantics", ["vdbfusion", "voxblox"])
+def test_host_path_sequence_grows(sim, pipeline, semantics):
+    """Host-pointer scans in 2-scan batches: the staging checkpoint replays before overwriting."""
+    kw = dict(max_bricks=128, max_batch=2, pipeline=pipeline, semantics=semantics)
+    if semantics == "voxblox":
+        kw.update(max_range=40.0)
+    g, o = hip(**kw), ora(**kw)
+    for k in (0, 1, 2, 3, 10, 20, 30):
+        pts, org = sim.scan(k)
+        pts = decimate(pts, 4)
+        g.integrate(pts, org)
+        o.integrate(pts, org)
+    g.sync()
+    assert bitwise(g, o)
+    assert g.stats()["n_grows"] >= 2
+
+
+def test_device_batches_grow(sim):
+    import torch
+    scans = [sim.scan(k) for k in (0, 5, 9, 14, 22)]
+    allp = np.concatenate([p for p, _ in scans])
+    offs = np.cumsum([0] + [p.shape[0] for p, _ in scans]).astype(np.uint64)
+    org = np.stack([o for _, o in scans])
+    d = torch.from_numpy(allp).to("cuda:0")
+    torch.cuda.synchronize()
+    g = hip(max_bricks=1000, max_batch=2)
+    g.integrate_batch_device(d.data_ptr(), offs, org)
+    g.sync()
+    o = ora()
+    for p, q in scans:
+        o.integrate(p, q)
+    assert bitwise(g, o)
+    assert g.stats()["n_grows"] >= 1
+
+
+def test_growth_respects_hard_limit(scan0):
+    from tsdf_map import TsdfError, _abi
+    g = hip(max_bricks=64, max_bricks_hard=4096)
+    g.integrate(*scan0)
+    with pytest.raises(TsdfError) as e:
+        g.sync()
+    assert e.value.code == _abi.TSDF_ENOMEM
+    st = g.stats()
+    assert st["max_bricks"] == 4096 and st["n_bricks"] == 4096
+    g.sync()  # reported once; the context stays usable
+    g.integrate(decimate(scan0[0], 64), scan0[1])
+    with pytest.raises(TsdfError):
+        g.sync()
+
+
+def test_import_grows(scan0):
+    a = hip()
+    a.integrate(*scan0)
+    b = hip(max_bricks=16)
+    b.import_bricks(*a.export_bricks())
+    for x, y in zip(a.export_bricks(), b.export_bricks()):
+        assert np.array_equal(x, y)
