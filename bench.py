@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--hz", type=float, default=10.0)
     ap.add_argument("--max-bricks", type=int, default=1 << 20,
                     help="brick pool capacity (4 KiB per brick)")
-    ap.add_argument("--semantics", default="vdbfusion", choices=("vdbfusion", "voxblox"),
+    ap.add_argument("--semantics", default="vdbfusion", choices=("vdbfusion", "voxblox", "vdbfusion_f64"),
                     help="fusion rule (tsdf_params.semantics); the headline metric is vdbfusion")
     ap.add_argument("--no-profile", action="store_true",
                     help="do not record per-kernel HIP events in the timed region")

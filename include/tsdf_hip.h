@@ -60,6 +60,11 @@ extern "C" {
  *                       max_weight, background (distance 0, weight 0). */
 #define TSDF_SEM_VDBFUSION 0
 #define TSDF_SEM_VOXBLOX 1
+/* VDBFusion at upstream's own precisions: the Ray<float> built from double points
+ * and mapped to index space through the grid transform, openvdb's float DDA, GetVoxelCenter /
+ * ComputeSDF in double.  Same touched voxels and weights as VDBVolume::Integrate; the GPU's fp64
+ * sample arithmetic makes it slower than TSDF_SEM_VDBFUSION (the fp32 restatement). */
+#define TSDF_SEM_VDBFUSION_F64 2
 
 typedef struct tsdf_params {
     double voxel_size;     /* metres (VDBVolume voxel_size) */
@@ -79,7 +84,8 @@ typedef struct tsdf_params {
                               bit for bit); 0 (default): batches run one after another, so per-kernel
                               timings (tsdf_stats.kernel_ms) are not shared with another batch */
     /* ABI v3: backend semantics */
-    int32_t semantics;          /* TSDF_SEM_VDBFUSION (default) or TSDF_SEM_VOXBLOX */
+    int32_t semantics;          /* TSDF_SEM_VDBFUSION (default), TSDF_SEM_VOXBLOX or
+                                   TSDF_SEM_VDBFUSION_F64 */
     int32_t allow_clear;        /* Voxblox allow_clear: a ray longer than max_range becomes a
                                    clearing ray of length min(max(d - tau, 0), max_range) (default 1) */
     int32_t use_weight_dropoff; /* Voxblox use_weight_dropoff: w *= (tau + sdf) / (tau - voxel_size)

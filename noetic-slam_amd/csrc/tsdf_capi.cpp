@@ -101,6 +101,28 @@ void sector_bounds(double yaw0, uint32_t sector, uint32_t n, RayConst& R) {
     R.sec_wrap = R.sec_hi <= R.sec_lo ? 1 : 0;
 }
 
+// The smallest double x >= 0 with (float)sqrt(x) >= tau (bisection over the ordered bit patterns
+// of non-negative doubles): behind the hit, VDBFusion's gate -(float)dist > -tau holds iff
+// d2 < this threshold (TSDF_SEM_VDBFUSION_F64; the oracle gates on the sqrt itself).
+double gate_threshold(float tau) {
+    auto ok = [&](uint64_t b) {
+        double x;
+        std::memcpy(&x, &b, 8);
+        return (float)std::sqrt(x) >= tau;
+    };
+    double hi_d = 4.0 * (double)tau * (double)tau + 1.0;
+    uint64_t lo = 0, hi;
+    std::memcpy(&hi, &hi_d, 8);
+    while (hi - lo > 1) {  // ok(lo) false, ok(hi) true
+        const uint64_t mid = lo + (hi - lo) / 2;
+        if (ok(mid)) hi = mid;
+        else lo = mid;
+    }
+    double x;
+    std::memcpy(&x, &hi, 8);
+    return x;
+}
+
 }  // namespace
 
 struct tsdf_ctx {
@@ -696,6 +718,9 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
     c->R.bg = p->semantics == TSDF_SEM_VOXBLOX ? 0.0f : c->R.tau;
     c->R.tau_m_vs = c->R.tau - c->R.vs;
     sector_bounds(p->sector_yaw0, p->sector, p->n_sectors, c->R);
+    c->R.vs_d = (double)c->R.vs;  // VDBVolume keeps voxel_size as float
+    c->R.inv_s_d = 1.0 / c->R.vs_d;
+    c->R.gate_d2 = gate_threshold(c->R.tau);
     {
         const double band = p->space_carving ? (p->max_range + p->sdf_trunc) / p->voxel_size
                                              : 2.0 * p->sdf_trunc / p->voxel_size;
@@ -776,7 +801,8 @@ int tsdf_create(const tsdf_params* p, tsdf_ctx** out) {
         p->weight_mode != TSDF_WEIGHT_CONSTANT || p->max_bricks == 0 ||
         p->max_bricks >= 0xFFFFFFF0ull || p->max_points == 0 || !(p->min_range >= 0) ||
         !(p->max_range > p->min_range) || p->max_batch == 0 || p->max_batch > TSDF_MAX_BATCH ||
-        (p->semantics != TSDF_SEM_VDBFUSION && p->semantics != TSDF_SEM_VOXBLOX) ||
+        (p->semantics != TSDF_SEM_VDBFUSION && p->semantics != TSDF_SEM_VOXBLOX &&
+         p->semantics != TSDF_SEM_VDBFUSION_F64) ||
         (p->semantics == TSDF_SEM_VOXBLOX && !(p->max_weight > 0.0f)) ||
         (p->n_sectors > 1 && p->sector >= p->n_sectors) || !std::isfinite(p->sector_yaw0) ||
         (p->max_bricks_hard && p->max_bricks_hard < p->max_bricks))
@@ -798,6 +824,9 @@ static void set_origin(BatchDesc& D, uint32_t s, const double o[3]) {
     D.ox[s] = (float)o[0];
     D.oy[s] = (float)o[1];
     D.oz[s] = (float)o[2];
+    D.odx[s] = o[0];
+    D.ody[s] = o[1];
+    D.odz[s] = o[2];
 }
 
 int tsdf_integrate(tsdf_ctx* c, const void* pts, uint64_t n, uint32_t point_step,

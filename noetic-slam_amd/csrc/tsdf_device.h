@@ -84,6 +84,9 @@ struct RayConst {
     // [sec_lo, sec_hi), or outside [sec_hi, sec_lo) when the sector wraps past 4 (sec_wrap)
     int sec_on, sec_wrap;
     float sec_lo, sec_hi;
+    // TSDF_SEM_VDBFUSION_F64: vs and 1/vs in double, and the gate's threshold on
+    // the squared distance behind the hit: (float)sqrt(d2) < tau  <=>  d2 < gate_d2
+    double vs_d, inv_s_d, gate_d2;
 };
 
 // fp32 pseudo-angle of (x, y) in [0, 4), monotone in atan2 (include/tsdf_hip.h tsdf_sector_of):
@@ -114,6 +117,7 @@ struct BatchDesc {
     uint32_t off[MAX_BATCH + 1];
     uint32_t blk[MAX_BATCH + 1];
     float ox[MAX_BATCH], oy[MAX_BATCH], oz[MAX_BATCH];
+    double odx[MAX_BATCH], ody[MAX_BATCH], odz[MAX_BATCH];  // the origins as given (TSDF_SEM_VDBFUSION_F64)
 };
 
 struct Table {

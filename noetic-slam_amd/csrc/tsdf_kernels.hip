@@ -124,8 +124,8 @@ __global__ __launch_bounds__(CNT_THREADS) void k_count(const float* __restrict__
         uint32_t* pc = Wk.pair + (size_t)i * maxp;
         uint32_t k = 0;
         typename Walk<SEM>::State r;
-        const bool ok = Walk<SEM>::init(R, ox, oy, oz, xyz[3 * (size_t)i], xyz[3 * (size_t)i + 1],
-                                 xyz[3 * (size_t)i + 2], r);
+        const bool ok = Walk<SEM>::init(R, D, t, xyz[3 * (size_t)i], xyz[3 * (size_t)i + 1],
+                                        xyz[3 * (size_t)i + 2], r);
         valid += ok ? 1u : 0u;
         // One pair per distinct brick; a line visits a brick in one contiguous run of DDA voxels,
         // so a pair closes when the next gated voxel's brick differs.
@@ -598,7 +598,7 @@ __global__ __launch_bounds__(PLC_THREADS) void k_place(const float* __restrict__
                                : NO_PAIR;
     const float ox = D.ox[t], oy = D.oy[t], oz = D.oz[t];
     typename Walk<SEM>::State r;
-    const bool ok = i < r1 && Walk<SEM>::init(R, ox, oy, oz, px, py, pz, r);
+    const bool ok = i < r1 && Walk<SEM>::init(R, D, t, px, py, pz, r);
     for (int j = threadIdx.x; j < PLC_WORDS; j += PLC_THREADS) s_bits[j] = 0u;
     if (threadIdx.x == 0) s_nst = 0u;
     __syncthreads();
@@ -897,6 +897,7 @@ static int grid_for(uint64_t items, int per_block, int cap) {
 hipError_t launch_count(const float* d_xyz, const BatchDesc& D, const RayConst& R, const Table& T,
                         const Work& Wk, Globals* G, int parity, hipStream_t st) {
     if (R.sem == 1) k_count<1><<<D.n_blocks, CNT_THREADS, 0, st>>>(d_xyz, D, R, T, Wk, G, parity);
+    else if (R.sem == 2) k_count<2><<<D.n_blocks, CNT_THREADS, 0, st>>>(d_xyz, D, R, T, Wk, G, parity);
     else k_count<0><<<D.n_blocks, CNT_THREADS, 0, st>>>(d_xyz, D, R, T, Wk, G, parity);
     return hipGetLastError();
 }
@@ -913,6 +914,7 @@ hipError_t launch_compact(const BatchDesc& D, const Table& T, const Work& Wk, Gl
 hipError_t launch_place(const float* d_xyz, const BatchDesc& D, const RayConst& R, const Table& T,
                         const Work& Wk, hipStream_t st) {
     if (R.sem == 1) k_place<1><<<2 * D.n_blocks, PLC_THREADS, 0, st>>>(d_xyz, D, R, T, Wk);
+    else if (R.sem == 2) k_place<2><<<2 * D.n_blocks, PLC_THREADS, 0, st>>>(d_xyz, D, R, T, Wk);
     else k_place<0><<<2 * D.n_blocks, PLC_THREADS, 0, st>>>(d_xyz, D, R, T, Wk);
     return hipGetLastError();
 }

@@ -273,9 +273,9 @@ struct Walk;
 template <>
 struct Walk<0> {  // TSDF_SEM_VDBFUSION
     typedef RayState State;
-    __device__ static __forceinline__ bool init(const RayConst& R, float ox, float oy, float oz,
+    __device__ static __forceinline__ bool init(const RayConst& R, const BatchDesc& D, uint32_t t,
                                                 float px, float py, float pz, State& r) {
-        return ray_init(R, ox, oy, oz, px, py, pz, r);
+        return ray_init(R, D.ox[t], D.oy[t], D.oz[t], px, py, pz, r);
     }
     __device__ static __forceinline__ bool gate(const RayConst& R, float ox, float oy, float oz,
                                                 const State& r, bool check = true) {
@@ -301,9 +301,9 @@ struct Walk<0> {  // TSDF_SEM_VDBFUSION
 template <>
 struct Walk<1> {  // TSDF_SEM_VOXBLOX
     typedef VbState State;
-    __device__ static __forceinline__ bool init(const RayConst& R, float ox, float oy, float oz,
+    __device__ static __forceinline__ bool init(const RayConst& R, const BatchDesc& D, uint32_t t,
                                                 float px, float py, float pz, State& r) {
-        return vb_init(R, ox, oy, oz, px, py, pz, r);
+        return vb_init(R, D.ox[t], D.oy[t], D.oz[t], px, py, pz, r);
     }
     __device__ static __forceinline__ bool gate(const RayConst& R, float ox, float oy, float oz,
                                                 const State& r, bool check = true) {
@@ -324,6 +324,139 @@ struct Walk<1> {  // TSDF_SEM_VOXBLOX
         return m < VOX_LIMIT - R.band_vox;
     }
     __device__ static __forceinline__ bool step(State& r) { return vb_step(r); }
+};
+
+// ------------------------------------------------------------------------------------------------
+// VDBFusion at upstream's own precisions (TSDF_SEM_VDBFUSION_F64; the bit-exact twin of
+// oracle/tsdf_oracle.c walk_ray_vdb): the Ray<float> VDBVolume::Integrate builds
+// from double points and maps to index space (double scale), openvdb's float DDA, and
+// GetVoxelCenter / ComputeSDF in double (Eigen's x + (y + z) reductions).  No contraction; double
+// division and sqrt are IEEE (LLVM's correctly rounded f64 expansions).
+
+struct VdbState : RayState {
+    double pxd, pyd, pzd;  // the point
+    double oxd, oyd, ozd;  // the origin as given
+};
+
+__device__ __forceinline__ void vdb_axis(float di, float inv, float pos, float t0i, int v,
+                                         float& tn, float& td, int& st) {
+    if (di == 0.0f) {  // math::isZero: the axis is disabled
+        st = 0;
+        tn = 3.402823466e+38f;
+        td = 3.402823466e+38f;
+    } else if (inv > 0.0f) {
+        st = 1;
+        tn = t0i + ((float)(v + 1) - pos) * inv;
+        td = inv;
+    } else {
+        st = -1;
+        tn = t0i + ((float)v - pos) * inv;
+        td = -inv;
+    }
+}
+
+__device__ __forceinline__ bool vdb_init(const RayConst& R, const BatchDesc& D, uint32_t t,
+                                         float px, float py, float pz, VdbState& r) {
+    if (!in_sector(R, px - D.ox[t], py - D.oy[t])) return false;  // another GPU's azimuth sector
+    r.oxd = D.odx[t];
+    r.oyd = D.ody[t];
+    r.ozd = D.odz[t];
+    r.pxd = px;
+    r.pyd = py;
+    r.pzd = pz;
+    const double dx = r.pxd - r.oxd, dy = r.pyd - r.oyd, dz = r.pzd - r.ozd;
+    const float depth = (float)__builtin_sqrt(dx * dx + (dy * dy + dz * dz));  // direction.norm()
+    if (!(depth > 0.0f)) return false;
+    if (!(depth >= R.min_range) || !(depth <= R.max_range)) return false;
+    const double il = 1.0 / __builtin_sqrt((dx * dx + dy * dy) + dz * dz);  // Vec3R::normalize
+    const float t0 = R.carving ? 0.0f : depth - R.tau;
+    const float t1 = depth + R.tau;
+    // Ray<float>(eye, dir, t0, t1).worldToIndex(grid)
+    const float ex = (float)((double)D.ox[t] * R.inv_s_d);
+    const float ey = (float)((double)D.oy[t] * R.inv_s_d);
+    const float ez = (float)((double)D.oz[t] * R.inv_s_d);
+    const float jx = (float)((double)(float)(dx * il) * R.inv_s_d);
+    const float jy = (float)((double)(float)(dy * il) * R.inv_s_d);
+    const float jz = (float)((double)(float)(dz * il) * R.inv_s_d);
+    const float L = __builtin_sqrtf((jx * jx + jy * jy) + jz * jz);
+    const float dix = jx / L, diy = jy / L, diz = jz / L;
+    const float t0i = L * t0;
+    r.t1i = L * t1;
+    // math::DDA::init
+    const float qx = ex + dix * t0i, qy = ey + diy * t0i, qz = ez + diz * t0i;
+    r.vx = (int)__builtin_floorf(qx);
+    r.vy = (int)__builtin_floorf(qy);
+    r.vz = (int)__builtin_floorf(qz);
+    vdb_axis(dix, 1.0f / dix, qx, t0i, r.vx, r.tnx, r.tdx, r.sx);
+    vdb_axis(diy, 1.0f / diy, qy, t0i, r.vy, r.tny, r.tdy, r.sy);
+    vdb_axis(diz, 1.0f / diz, qz, t0i, r.vz, r.tnz, r.tdz, r.sz);
+    r.px = px;
+    r.py = py;
+    r.pz = pz;
+    return true;
+}
+
+// GetVoxelCenter + ComputeSDF in double at the current voxel: proj and the squared distance
+__device__ __forceinline__ void vdb_geom(const RayConst& R, const VdbState& r, double& proj,
+                                         double& d2) {
+    const double cx = (double)r.vx * R.vs_d + R.vs_d / 2.0;
+    const double cy = (double)r.vy * R.vs_d + R.vs_d / 2.0;
+    const double cz = (double)r.vz * R.vs_d + R.vs_d / 2.0;
+    const double ax = cx - r.oxd, ay = cy - r.oyd, az = cz - r.ozd;
+    const double bx = r.pxd - cx, by = r.pyd - cy, bz = r.pzd - cz;
+    proj = ax * bx + (ay * by + az * bz);
+    d2 = bx * bx + (by * by + bz * bz);
+}
+
+__device__ __forceinline__ bool vdb_inside(const VdbState& r) {
+    return r.vx > -VOX_LIMIT && r.vx < VOX_LIMIT && r.vy > -VOX_LIMIT && r.vy < VOX_LIMIT &&
+           r.vz > -VOX_LIMIT && r.vz < VOX_LIMIT;
+}
+
+template <>
+struct Walk<2> {  // TSDF_SEM_VDBFUSION_F64
+    typedef VdbState State;
+    __device__ static __forceinline__ bool init(const RayConst& R, const BatchDesc& D, uint32_t t,
+                                                float px, float py, float pz, State& r) {
+        return vdb_init(R, D, t, px, py, pz, r);
+    }
+    __device__ static __forceinline__ bool gate(const RayConst& R, float, float, float,
+                                                const State& r, bool check = true) {
+        if (check && !vdb_inside(r)) return false;
+        double proj, d2;
+        vdb_geom(R, r, proj, d2);
+        if (proj > 0.0) return true;
+        if (!(proj < 0.0)) return false;
+        return d2 < R.gate_d2;  // (float)sqrt(d2) < tau, i.e. -dist > -tau
+    }
+    __device__ static __forceinline__ bool sample(const RayConst& R, float, float, float,
+                                                  const State& r, float& s, bool check = true) {
+        if (check && !vdb_inside(r)) return false;
+        double proj, d2;
+        vdb_geom(R, r, proj, d2);
+        if (!(proj > 0.0 || proj < 0.0)) return false;
+        const float dist = (float)__builtin_sqrt(d2);
+        const float sdf = proj > 0.0 ? dist : -dist;
+        if (!(sdf > -R.tau)) return false;
+        s = sdf < R.tau ? sdf : R.tau;
+        return true;
+    }
+    __device__ static __forceinline__ bool sample_sel(const RayConst& R, float ox, float oy,
+                                                      float oz, const State& r, float& s,
+                                                      bool check = true) {
+        const bool inl = !check || vdb_inside(r);
+        double proj, d2;
+        vdb_geom(R, r, proj, d2);
+        const float dist = (float)__builtin_sqrt(d2);
+        const float sdf = proj > 0.0 ? dist : -dist;
+        s = sdf < R.tau ? sdf : R.tau;
+        return inl && (proj > 0.0 || proj < 0.0) && sdf > -R.tau;
+    }
+    __device__ static __forceinline__ bool inside(const RayConst& R, const State& r) {
+        const int m = max(max(abs(r.vx), abs(r.vy)), abs(r.vz));
+        return m < VOX_LIMIT - R.band_vox;
+    }
+    __device__ static __forceinline__ bool step(State& r) { return ray_step(r); }
 };
 
 __device__ __forceinline__ uint64_t pack_brick(int bx, int by, int bz) {

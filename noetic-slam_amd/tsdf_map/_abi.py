@@ -21,7 +21,9 @@ TILE_WORDS = 1028  # TSDF_TILE_WORDS: u32 words of one border-brick tile
 MAX_WORLD = 64
 SEM_VDBFUSION = 0
 SEM_VOXBLOX = 1
-SEMANTICS = {"vdbfusion": SEM_VDBFUSION, "voxblox": SEM_VOXBLOX}
+SEM_VDBFUSION_F64 = 2
+SEMANTICS = {"vdbfusion": SEM_VDBFUSION, "voxblox": SEM_VOXBLOX,
+             "vdbfusion_f64": SEM_VDBFUSION_F64}
 
 KERNEL_KINDS = ("count", "compact", "place", "integrate")  # k_<kind>, KernelKind order
 

@@ -33,6 +33,11 @@
  *   ORACLE_MODE_SEQUENTIAL — VDBFusion's literal per-sample fp32 running average, in input order.
  *     Equal to SCAN_FUSED in exact arithmetic; the fp32 difference is the parity tolerance
  *     reported against "the reference CPU backend" (DESIGN.md §4).
+ *   ORACLE_MODE_VDB_LITERAL — VDBFusion's Integrate with upstream's own precisions (walk_ray_vdb):
+ *     double points / origin, the Ray<float> built from them and mapped to index space through the
+ *     grid transform (double scale), openvdb's DDA in float, GetVoxelCenter / ComputeSDF in double,
+ *     and the per-sample float running average in input order.  The distance of the GPU field from
+ *     this mode is what "matches VDBFusion" means quantitatively (tests/test_literal.py).
  *
  * Parity pinning: no reference test pins values at this boundary, so this oracle
  * is pinned by closed-form known-answer tests (tests/test_oracle_kat.py: single rays, planes,
@@ -48,6 +53,7 @@
 
 #define ORACLE_MODE_SCAN_FUSED 0
 #define ORACLE_MODE_SEQUENTIAL 1
+#define ORACLE_MODE_VDB_LITERAL 2
 
 /* voxel domain: |index| < 2^23 on every axis (the GPU packs 21-bit brick coordinates) */
 #define VOX_LIMIT (1 << 23)
@@ -237,7 +243,8 @@ int tsdf_create(const tsdf_params* params, tsdf_ctx** out) {
     if (!params || !out) return TSDF_EINVAL;
     if (!(params->voxel_size > 0) || !(params->sdf_trunc > 0) ||
         params->brick_side != TSDF_BRICK_SIDE || params->weight_mode != TSDF_WEIGHT_CONSTANT ||
-        (params->semantics != TSDF_SEM_VDBFUSION && params->semantics != TSDF_SEM_VOXBLOX) ||
+        (params->semantics != TSDF_SEM_VDBFUSION && params->semantics != TSDF_SEM_VOXBLOX &&
+         params->semantics != TSDF_SEM_VDBFUSION_F64) ||
         (params->semantics == TSDF_SEM_VOXBLOX && !(params->max_weight > 0.0f)) ||
         (params->n_sectors > 1 && params->sector >= params->n_sectors) ||
         !isfinite(params->sector_yaw0))
@@ -275,8 +282,10 @@ void tsdf_destroy(tsdf_ctx* c) {
 const char* tsdf_last_error(const tsdf_ctx* c) { return c ? c->err : "null context"; }
 
 int tsdf_oracle_set_mode(tsdf_ctx* c, int mode) {
-    if (!c || (mode != ORACLE_MODE_SCAN_FUSED && mode != ORACLE_MODE_SEQUENTIAL))
+    if (!c || (mode != ORACLE_MODE_SCAN_FUSED && mode != ORACLE_MODE_SEQUENTIAL &&
+               mode != ORACLE_MODE_VDB_LITERAL))
         return TSDF_EINVAL;
+    if (mode == ORACLE_MODE_VDB_LITERAL && c->sem == TSDF_SEM_VOXBLOX) return TSDF_EINVAL;
     if (c->n_thr > 1 && mode != ORACLE_MODE_SCAN_FUSED) return TSDF_EINVAL;
     c->mode = mode;
     return TSDF_OK;
@@ -353,6 +362,97 @@ static int64_t walk_ray(tsdf_ctx* c, float px, float py, float pz, float ox, flo
         if (!(tn[a] <= t1i)) break;
         tn[a] += td[a];
         v[a] += st[a];
+    }
+    return visited;
+}
+
+/* ---- VDBFusion's Integrate body at upstream's own precisions (ORACLE_MODE_VDB_LITERAL) -------
+ *
+ * PRBonn/vdbfusion VDBVolume::Integrate (unpinned; not in /root/reference — SURVEY §8a8) on
+ * std::vector<Eigen::Vector3d> points, restated step by step:
+ *   direction = point - origin (double);  depth = (float)direction.norm()  (Eigen: x + (y + z))
+ *   Vec3R dir = direction; dir.normalize()  (openvdb: len = sqrt((x x + y y) + z z), dir *= 1/len)
+ *   t0 = carving ? 0 : depth - tau;  t1 = depth + tau  (float)
+ *   Ray<float>(eye, dir, t0, t1): eye, dir rounded to float;  .worldToIndex(grid):
+ *       eye_i = (float)(eye * (1/vs)), d = (float)(dir * (1/vs)) (double scale map), L = |d| (float),
+ *       dir_i = d / L, t0_i = L t0, t1_i = L t1, inv = 1 / dir_i (float)
+ *   math::DDA: pos = eye_i + dir_i t0_i; v = floor(pos); per axis: dir_i == 0 -> next = FLT_MAX;
+ *       inv > 0 -> next = t0_i + ((v + 1) - pos) inv, delta = inv; else next = t0_i + (v - pos) inv,
+ *       delta = -inv;  step(): a = MinIndex(next) (ties -> higher axis); stop when next[a] > t1_i
+ *   GetVoxelCenter: c = v vs + vs / 2 (double);  ComputeSDF: sign((c - o).(p - c)) |p - c| (double,
+ *       Eigen x + (y + z) reductions), cast to float;  gate sdf > -tau, then the float update.
+ * All float ops are evaluated without contraction (-ffp-contract=off), as an x86-64 build without
+ * FMA instructions evaluates them. */
+static int64_t walk_ray_vdb(tsdf_ctx* c, const double p[3], const double o[3], visit_fn visit,
+                            void* user) {
+    const float tau = c->tau;
+    const double vs_d = (double)c->vs;
+    const double dx = p[0] - o[0], dy = p[1] - o[1], dz = p[2] - o[2];
+    if (!ctx_in_sector(c, (float)p[0] - (float)o[0], (float)p[1] - (float)o[1])) return -1;
+    const float depth = (float)sqrt(dx * dx + (dy * dy + dz * dz));
+    if (!(depth > 0.0f)) return -1;
+    if (!(depth >= (float)c->p.min_range) || !(depth <= (float)c->p.max_range)) return -1;
+    const double len = sqrt((dx * dx + dy * dy) + dz * dz);
+    const double il = 1.0 / len;
+    const double dir_d[3] = {dx * il, dy * il, dz * il};
+    const float t0 = c->p.space_carving ? 0.0f : depth - tau;
+    const float t1 = depth + tau;
+    const double inv_s = 1.0 / vs_d;
+    float eye_i[3], dj[3];
+    for (int a = 0; a < 3; a++) {
+        eye_i[a] = (float)((double)(float)o[a] * inv_s);
+        dj[a] = (float)((double)(float)dir_d[a] * inv_s);
+    }
+    const float L = (float)sqrt((double)((dj[0] * dj[0] + dj[1] * dj[1]) + dj[2] * dj[2]));
+    float dir_i[3], inv[3], pos[3];
+    for (int a = 0; a < 3; a++) {
+        dir_i[a] = dj[a] / L;
+        inv[a] = 1.0f / dir_i[a];
+    }
+    const float t0_i = L * t0, t1_i = L * t1;
+    int32_t v[3], st[3];
+    float tn[3], td[3];
+    for (int a = 0; a < 3; a++) {
+        pos[a] = eye_i[a] + dir_i[a] * t0_i;
+        v[a] = (int32_t)floorf(pos[a]);
+    }
+    for (int a = 0; a < 3; a++) {
+        if (dir_i[a] == 0.0f) {
+            st[a] = 0;
+            tn[a] = 3.402823466e+38f;
+            td[a] = 3.402823466e+38f;
+        } else if (inv[a] > 0.0f) {
+            st[a] = 1;
+            tn[a] = t0_i + ((float)(v[a] + 1) - pos[a]) * inv[a];
+            td[a] = inv[a];
+        } else {
+            st[a] = -1;
+            tn[a] = t0_i + ((float)v[a] - pos[a]) * inv[a];
+            td[a] = -inv[a];
+        }
+    }
+    int64_t visited = 0;
+    for (int it = 0; it < MAX_DDA_STEPS; it++) {
+        visited++;
+        if (v[0] > -VOX_LIMIT && v[0] < VOX_LIMIT && v[1] > -VOX_LIMIT && v[1] < VOX_LIMIT &&
+            v[2] > -VOX_LIMIT && v[2] < VOX_LIMIT) {
+            double cc[3], va[3], vb[3];
+            for (int a = 0; a < 3; a++) {
+                cc[a] = (double)v[a] * vs_d + vs_d / 2.0;
+                va[a] = cc[a] - o[a];
+                vb[a] = p[a] - cc[a];
+            }
+            const double dist = sqrt(vb[0] * vb[0] + (vb[1] * vb[1] + vb[2] * vb[2]));
+            const double proj = va[0] * vb[0] + (va[1] * vb[1] + va[2] * vb[2]);
+            const float sdf = (float)((proj / fabs(proj)) * dist);
+            if (sdf > -tau) visit(c, v[0], v[1], v[2], tau < sdf ? tau : sdf, 1.0f, user);
+        }
+        int a; /* math::MinIndex */
+        if (tn[0] < tn[1] && tn[0] < tn[2]) a = 0;
+        else a = (tn[1] < tn[2]) ? 1 : 2;
+        if (tn[a] > t1_i) break;
+        v[a] += st[a];
+        tn[a] += td[a];
     }
     return visited;
 }
@@ -483,7 +583,7 @@ static void visit_accum(tsdf_ctx* c, int32_t x, int32_t y, int32_t z, float s, f
         if (v->stamp != c->scan_id) { v->stamp = c->scan_id; c->st.n_voxels_last++; }
         return;
     }
-    if (c->mode == ORACLE_MODE_SEQUENTIAL) {
+    if (c->mode != ORACLE_MODE_SCAN_FUSED) { /* SEQUENTIAL / VDB_LITERAL: VDBVolume's update */
         const float nw = v->W + w;
         v->S = (v->S * v->W + s * w) / nw;
         v->W = nw;
@@ -555,6 +655,7 @@ typedef struct {
     uint32_t point_step, xyz_offset;
     int32_t xyz_is_f64;
     float ox, oy, oz;
+    const double* origin;
     uint64_t rays;
     int fail;
 } mt_job;
@@ -593,10 +694,18 @@ static void* mt_walk(void* arg) {
     tsdf_ctx* c = j->c;
     for (uint64_t i = j->i0; i < j->i1 && !j->fail; i++) {
         float px, py, pz;
-        mt_point(j->base + i * j->point_step + j->xyz_offset, j->xyz_is_f64, &px, &py, &pz);
-        const int64_t r = c->sem == TSDF_SEM_VOXBLOX
-                              ? walk_ray_vb(c, px, py, pz, j->ox, j->oy, j->oz, visit_bucket, j)
-                              : walk_ray(c, px, py, pz, j->ox, j->oy, j->oz, visit_bucket, j);
+        const char* q = j->base + i * j->point_step + j->xyz_offset;
+        mt_point(q, j->xyz_is_f64, &px, &py, &pz);
+        int64_t r;
+        if (c->sem == TSDF_SEM_VDBFUSION_F64) {
+            double pd[3] = {px, py, pz};
+            if (j->xyz_is_f64) memcpy(pd, q, sizeof pd);
+            r = walk_ray_vdb(c, pd, j->origin, visit_bucket, j);
+        } else {
+            r = c->sem == TSDF_SEM_VOXBLOX
+                    ? walk_ray_vb(c, px, py, pz, j->ox, j->oy, j->oz, visit_bucket, j)
+                    : walk_ray(c, px, py, pz, j->ox, j->oy, j->oz, visit_bucket, j);
+        }
         if (r >= 0) j->rays++;
     }
     return NULL;
@@ -620,14 +729,15 @@ static void* mt_fuse(void* arg) {
 }
 
 static int mt_integrate(tsdf_ctx* c, const char* base, uint64_t n, uint32_t point_step,
-                        uint32_t xyz_offset, int32_t xyz_is_f64, float ox, float oy, float oz) {
+                        uint32_t xyz_offset, int32_t xyz_is_f64, float ox, float oy, float oz,
+                        const double* origin) {
     const int T = c->n_thr;
     mt_job job[64];
     pthread_t th[64];
     for (int phase = 0; phase < 2; phase++) {
         for (int t = 0; t < T; t++) {
             job[t] = (mt_job){c, t, base, n * (uint64_t)t / T, n * (uint64_t)(t + 1) / T,
-                              point_step, xyz_offset, xyz_is_f64, ox, oy, oz, 0, 0};
+                              point_step, xyz_offset, xyz_is_f64, ox, oy, oz, origin, 0, 0};
             if (pthread_create(&th[t], NULL, phase ? mt_fuse : mt_walk, &job[t])) {
                 for (int k = 0; k < t; k++) pthread_join(th[k], NULL);
                 return set_err(c, TSDF_ENOMEM, "oracle thread creation failed");
@@ -692,14 +802,29 @@ int tsdf_integrate(tsdf_ctx* c, const void* pts, uint64_t n, uint32_t point_step
     int fail = 0;
     const char* base = (const char*)pts;
     if (c->n_thr > 1) {
-        const int rc = mt_integrate(c, base, n, point_step, xyz_offset, xyz_is_f64, ox, oy, oz);
+        const int rc = mt_integrate(c, base, n, point_step, xyz_offset, xyz_is_f64, ox, oy, oz,
+                                     origin);
         if (rc != TSDF_OK) return rc;
         c->st.n_scans++;
         c->st.n_points_in += n;
         c->st.n_voxels_total += c->st.n_voxels_last;
         return TSDF_OK;
     }
-    for (uint64_t i = 0; i < n && !fail; i++) {
+    /* TSDF_SEM_VDBFUSION_F64 (scan-fused or sequential) and the VDB_LITERAL mode walk as upstream */
+    const int vdb_walk = c->sem == TSDF_SEM_VDBFUSION_F64 || c->mode == ORACLE_MODE_VDB_LITERAL;
+    for (uint64_t i = 0; i < n && !fail && vdb_walk; i++) {
+        const char* q = base + i * point_step + xyz_offset;
+        double pd[3];
+        if (xyz_is_f64) {
+            memcpy(pd, q, sizeof pd);
+        } else {
+            float f[3];
+            memcpy(f, q, sizeof f);
+            pd[0] = f[0]; pd[1] = f[1]; pd[2] = f[2];
+        }
+        if (walk_ray_vdb(c, pd, origin, visit_accum, &fail) >= 0) c->st.n_rays_total++;
+    }
+    for (uint64_t i = 0; i < n && !fail && !vdb_walk; i++) {
         const char* q = base + i * point_step + xyz_offset;
         float px, py, pz;
         if (xyz_is_f64) {
@@ -917,8 +1042,11 @@ int64_t tsdf_oracle_ray_voxels(tsdf_ctx* c, const float p[3], const double origi
                                int32_t* ijk, float* sdf, uint64_t cap) {
     ray_rec r = {ijk, sdf, 0, cap};
     const float ox = (float)origin[0], oy = (float)origin[1], oz = (float)origin[2];
+    const double pd[3] = {p[0], p[1], p[2]};
     int64_t v = c->sem == TSDF_SEM_VOXBLOX
                     ? walk_ray_vb(c, p[0], p[1], p[2], ox, oy, oz, visit_record, &r)
+                : c->mode == ORACLE_MODE_VDB_LITERAL
+                    ? walk_ray_vdb(c, pd, origin, visit_record, &r)
                     : walk_ray(c, p[0], p[1], p[2], ox, oy, oz, visit_record, &r);
     if (v < 0) return -1;
     return (int64_t)r.n;
