@@ -201,6 +201,14 @@ int tsdf_reset_stats(tsdf_ctx* ctx);
 /* Record HIP events around every kernel (per-kind device time in tsdf_stats.kernel_ms). */
 int tsdf_set_profiling(tsdf_ctx* ctx, int32_t on);
 
+/* Append one JSON line per finished GPU batch to the file at `path` (NULL: stop), written at
+ * tsdf_sync / read-outs (and every ~250 batches): batch id, scans, points, valid rays, (ray, brick)
+ * pairs, voxel updates (sum over its scans of U_vox), dirty voxels, active and new bricks, pool
+ * size, overflow bits, whether it committed (a batch re-run after a capacity growth reports
+ * committed: false first), SURVEY §8d's algorithmic bytes, and with profiling on the per-kernel
+ * times, path time and GB/s.  With max_batch = 1 every line is one scan (SURVEY §5 metrics). */
+int tsdf_set_metrics_log(tsdf_ctx* ctx, const char* path);
+
 /* Marching-cubes triangle mesh of the field (VDBFusion VDBVolume::extract_triangle_mesh; SURVEY
  * §8f.1): every 2x2x2 voxel cube whose 8 voxels are observed (W > 0 and W >= min_weight) is
  * meshed at S = 0.  Output: a triangle soup, 9 floats (3 vertices x, y, z, metres) per triangle,

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdarg>
 #include <cstddef>
@@ -29,7 +30,10 @@ static_assert(TSDF_TILE_WORDS == TILE_WORDS && TSDF_MAX_WORLD == MAX_WORLD, "bor
 namespace {
 
 struct EventTimer final : KernelTimer {
-    struct Rec { int kind; hipEvent_t a, b; };
+    struct Rec { int kind; uint64_t batch; hipEvent_t a, b; };
+    uint64_t cur_batch = 0;  // the batch being launched (set by launch())
+    bool per_batch = false;  // keep per-batch times for the metrics log
+    std::vector<std::pair<uint64_t, std::array<double, KIND_N>>> batch_ms;
     std::vector<hipEvent_t> free_ev;
     std::vector<Rec> pending;
     hipEvent_t open_ev[KIND_N] = {};
@@ -54,7 +58,7 @@ struct EventTimer final : KernelTimer {
         hipEvent_t e = get();
         if (!e || !open_ev[kind]) return;
         (void)hipEventRecord(e, st);
-        pending.push_back({kind, open_ev[kind], e});
+        pending.push_back({kind, cur_batch, open_ev[kind], e});
         open_ev[kind] = nullptr;
     }
     // call only after the stream drained
@@ -64,6 +68,11 @@ struct EventTimer final : KernelTimer {
             if (hipEventElapsedTime(&t, r.a, r.b) == hipSuccess) {
                 ms[r.kind] += t;
                 launches[r.kind]++;
+                if (per_batch) {
+                    if (batch_ms.empty() || batch_ms.back().first != r.batch)
+                        batch_ms.push_back({r.batch, std::array<double, KIND_N>{}});
+                    batch_ms.back().second[r.kind] += t;
+                }
             }
             free_ev.push_back(r.a);
             free_ev.push_back(r.b);
@@ -167,6 +176,11 @@ struct tsdf_ctx {
     std::vector<Logged> log;
     bool can_grow = false;  // G->retry: overflowed batches are skipped and replayed
     bool in_replay = false;
+    // metrics log (tsdf_set_metrics_log): one JSON line per finished batch
+    FILE* metrics = nullptr;
+    uint64_t metrics_next = 0;  // the next batch id to report
+    struct BatchInfo { uint64_t id; uint32_t scans; uint64_t points; };
+    std::vector<BatchInfo> metrics_info;  // host-side facts of the batches not yet reported
     uint64_t n_grows = 0, n_replayed = 0;
 };
 
@@ -214,9 +228,16 @@ static uint32_t samples_per_ray(const tsdf_params& p) {
 // Launch one batch (desc offsets relative to d_xyz); fills the workgroup prefix of D.
 static int check_and_replay(tsdf_ctx* c);
 static int drain_all(tsdf_ctx* c);
+static int emit_metrics(tsdf_ctx* c);
 
 static int launch(tsdf_ctx* c, const float* d_xyz, BatchDesc& D) {
     if (D.n_scans == 0) return TSDF_OK;
+    if (c->metrics && !c->in_replay && c->batch_id - c->metrics_next >= METRIC_RING - 8) {
+        int rc = drain_all(c);  // the device ring of batch records would wrap
+        if (!rc) rc = check_and_replay(c);
+        if (!rc) rc = emit_metrics(c);
+        if (rc) return rc;
+    }
     if (c->can_grow && !c->in_replay && c->log.size() >= 1024) {
         // device-pointer batches stay replayable until a check: bound the log
         int rc = drain_all(c);
@@ -242,6 +263,8 @@ static int launch(tsdf_ctx* c, const float* d_xyz, BatchDesc& D) {
     T.cell = c->cell2[par];
     const Work& W = c->W2[par];
     EventTimer* tm = c->timer;
+    if (tm) tm->cur_batch = c->batch_id;
+    if (c->metrics) c->metrics_info.push_back({c->batch_id, D.n_scans, D.off[D.n_scans]});
     // staging uploads, imports, ... (an idle context stream has nothing to order against)
     if (hipStreamQuery(c->stream) != hipSuccess) {
         HIPCHK(c, hipEventRecord(c->ev_main, c->stream));
@@ -539,6 +562,59 @@ static int check_and_replay(tsdf_ctx* c) {
     return fail(c, TSDF_ENOMEM, "capacity growth did not converge");
 }
 
+// Metrics log: one JSON line per finished batch, from the device ring of batch records (k_finish)
+// and the host's facts (points) and kernel times (profiling on).  Called with every batch done.
+static int emit_metrics(tsdf_ctx* c) {
+    if (!c->metrics) return TSDF_OK;
+    if (c->timer) c->timer->harvest();
+    const uint64_t end = c->batch_id;
+    if (end == c->metrics_next) return TSDF_OK;
+    std::vector<BatchRecord> ring(METRIC_RING);
+    HIPCHK(c, hipMemcpy(ring.data(), c->G->ring, sizeof(BatchRecord) * METRIC_RING,
+                        hipMemcpyDeviceToHost));
+    size_t ti = 0;
+    for (uint64_t b = std::max<uint64_t>(c->metrics_next, end > METRIC_RING ? end - METRIC_RING : 0);
+         b < end; b++) {
+        const BatchRecord& r = ring[b % METRIC_RING];
+        if (r.batch_id != (uint32_t)b) continue;  // not written (ring wrapped)
+        uint32_t scans = 0;
+        uint64_t points = 0;
+        for (auto& i : c->metrics_info)
+            if (i.id == b) { scans = i.scans; points = i.points; }
+        const double bytes = 12.0 * (double)r.rays + 16.0 * (double)r.vox;  // SURVEY §8d B_scan
+        fprintf(c->metrics,
+                "{\"batch\": %llu, \"scans\": %u, \"points\": %llu, \"rays\": %llu, \"pairs\": %llu, "
+                "\"voxel_updates\": %llu, \"dirty_voxels\": %llu, \"active_bricks\": %u, "
+                "\"new_bricks\": %u, \"bricks\": %u, \"overflow\": %u, \"committed\": %s, "
+                "\"algorithmic_bytes\": %.0f",
+                (unsigned long long)b, scans, (unsigned long long)points,
+                (unsigned long long)r.rays, (unsigned long long)r.pairs, (unsigned long long)r.vox,
+                (unsigned long long)r.dirty, r.n_active, r.n_new,
+                std::min<uint32_t>(r.pool_count, c->T.max_bricks), r.ovf,
+                r.committed ? "true" : "false", bytes);
+        const std::array<double, KIND_N>* ms = nullptr;
+        if (c->timer) {
+            auto& bm = c->timer->batch_ms;
+            while (ti < bm.size() && bm[ti].first < b) ti++;
+            if (ti < bm.size() && bm[ti].first == b) ms = &bm[ti].second;
+        }
+        if (ms) {
+            const double path = (*ms)[0] + (*ms)[1] + (*ms)[2] + (*ms)[3];
+            fprintf(c->metrics,
+                    ", \"kernel_ms\": {\"count\": %.5f, \"compact\": %.5f, \"place\": %.5f, "
+                    "\"integrate\": %.5f}, \"path_ms\": %.5f, \"gbs\": %.2f",
+                    (*ms)[0], (*ms)[1], (*ms)[2], (*ms)[3], path,
+                    path > 0 ? bytes / (path * 1e-3) / 1e9 : 0.0);
+        }
+        fprintf(c->metrics, "}\n");
+    }
+    fflush(c->metrics);
+    c->metrics_next = end;
+    c->metrics_info.clear();
+    if (c->timer) c->timer->batch_ms.clear();
+    return TSDF_OK;
+}
+
 // Marching-cubes case table, generated (the same construction as the oracle's
 // mc_build): per cube face the sign-change edges are paired into segments (ambiguous faces pair the
 // crossings around their inside corners, so neighbouring cubes agree), each directed with the
@@ -660,6 +736,7 @@ void tsdf_destroy(tsdf_ctx* c) {
                 if (c->bst[q]) (void)hipStreamSynchronize(c->bst[q]);
         }
     }
+    if (c->metrics) fclose(c->metrics);
     delete c->timer;
     void* dev[] = {c->T.keys,        c->T.slots,
                    c->T.touched,
@@ -952,6 +1029,8 @@ int tsdf_sync(tsdf_ctx* c) {
     rc = check_and_replay(c);
     if (rc) return rc;
     if (c->timer) c->timer->harvest();
+    rc = emit_metrics(c);
+    if (rc) return rc;
     uint32_t ovf = 0;
     HIPCHK(c, hipMemcpy(&ovf, &c->G->overflow, sizeof ovf, hipMemcpyDeviceToHost));
     if (ovf) {
@@ -976,7 +1055,7 @@ static int drain(tsdf_ctx* c) {
     rc = check_and_replay(c);
     if (rc) return rc;
     if (c->timer) c->timer->harvest();
-    return TSDF_OK;
+    return emit_metrics(c);
 }
 
 int tsdf_query_dense(tsdf_ctx* c, const int32_t lo[3], const int32_t hi[3], float* sdf,
@@ -1313,9 +1392,30 @@ int tsdf_set_profiling(tsdf_ctx* c, int32_t on) {
     if (!c) return TSDF_EINVAL;
     const int rc = drain(c);
     if (rc) return rc;
-    if (on && !c->timer) c->timer = new (std::nothrow) EventTimer();
+    if (on && !c->timer) {
+        c->timer = new (std::nothrow) EventTimer();
+        if (c->timer) c->timer->per_batch = c->metrics != nullptr;
+    }
     if (!on && c->timer) { delete c->timer; c->timer = nullptr; }
     return (on && !c->timer) ? TSDF_ENOMEM : TSDF_OK;
+}
+
+int tsdf_set_metrics_log(tsdf_ctx* c, const char* path) {
+    if (!c) return TSDF_EINVAL;
+    int rc = drain(c);  // report (or drop) what came before
+    if (rc) return rc;
+    if (c->metrics) {
+        fclose(c->metrics);
+        c->metrics = nullptr;
+    }
+    if (c->timer) c->timer->per_batch = false;
+    c->metrics_info.clear();
+    c->metrics_next = c->batch_id;
+    if (!path || !*path) return TSDF_OK;
+    c->metrics = fopen(path, "a");
+    if (!c->metrics) return fail(c, TSDF_EINVAL, "cannot open metrics log %s", path);
+    if (c->timer) c->timer->per_batch = true;
+    return TSDF_OK;
 }
 
 int32_t tsdf_sector_of(float px, float py, const double origin[3], double yaw0,

@@ -160,6 +160,8 @@ struct Counters {
     uint32_t cursor;
     uint32_t n_fb;
     uint32_t ovf;  // OVF_* raised by this batch's kernels
+    uint32_t n_new;  // bricks the batch allocated (k_compact_scan)
+    uint32_t pad1[3];
     unsigned long long n_vox[8];    // sum over scans of U_vox, sharded by blockIdx & 7
     unsigned long long n_rays[8];   // valid rays
     unsigned long long n_pairs[8];
@@ -167,6 +169,15 @@ struct Counters {
 };
 
 // persistent device globals (one allocation, zeroed at create)
+// One finished batch, as the metrics log reports it (tsdf_set_metrics_log; k_finish writes it to
+// Globals::ring[batch_id % METRIC_RING], the host drains the ring at its checks).
+constexpr uint32_t METRIC_RING = 256;
+struct BatchRecord {
+    uint32_t batch_id, n_active, n_new, ovf;
+    uint32_t committed, pool_count, pad[2];
+    unsigned long long rays, pairs, vox, dirty;
+};
+
 // Capacity growth: with `retry` set (the context can still grow), a batch that
 // raised an overflow — or any batch after it — does not commit: k_integrate skips its field writes
 // and k_finish its stats, so the host can grow the buffers and replay the batches from `fail_id`.
@@ -183,6 +194,7 @@ struct Globals {
     unsigned long long tot_pairs[8];
     unsigned long long tot_dirty[8];
     Counters last;  // the last finished batch's counters (k_finish)
+    BatchRecord ring[METRIC_RING];  // per-batch records (k_finish), drained by the host's metrics log
 };
 
 enum KernelKind { KIND_COUNT = 0, KIND_COMPACT = 1, KIND_PLACE = 2, KIND_INTEGRATE = 3, KIND_N = 4 };

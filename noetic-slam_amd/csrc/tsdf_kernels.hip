@@ -453,6 +453,7 @@ __global__ __launch_bounds__(CMP_SCAN_THREADS) void k_compact_scan(uint32_t nch,
     if (threadIdx.x == 0) {
         C->n_active = s_carry[0];
         C->cursor = s_carry[1];
+        C->n_new = s_carry[2] - G->pool_count;
         G->pool_count = s_carry[2];
         if (s_carry[1] > Wk.max_smp) atomicOr(&C->ovf, OVF_PAIRS);
         if (s_carry[0] > Wk.max_active) atomicOr(&C->ovf, OVF_ACTIVE);
@@ -1029,6 +1030,24 @@ __global__ void k_finish(Globals* G, int parity, uint32_t batch_id) {
             G->failed = 1u;
             G->fail_id = batch_id;
         }
+    }
+    if (threadIdx.x == 0) {  // the batch's metrics record
+        BatchRecord r;
+        r.batch_id = batch_id;
+        r.n_active = C->n_active;
+        r.n_new = C->n_new;
+        r.ovf = ovf;
+        r.committed = commit ? 1u : 0u;
+        r.pool_count = G->pool_count;
+        r.pad[0] = r.pad[1] = 0u;
+        r.rays = r.pairs = r.vox = r.dirty = 0ull;
+        for (int k = 0; k < 8; k++) {
+            r.rays += C->n_rays[k];
+            r.pairs += C->n_pairs[k];
+            r.vox += C->n_vox[k];
+            r.dirty += C->n_dirty[k];
+        }
+        G->ring[batch_id % METRIC_RING] = r;
     }
     __syncthreads();
     uint32_t* src = reinterpret_cast<uint32_t*>(C);

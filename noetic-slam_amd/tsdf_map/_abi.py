@@ -117,6 +117,7 @@ SIGNATURES = {
     "tsdf_get_stats": (C.c_int, [P, C.POINTER(TsdfStats)]),
     "tsdf_reset_stats": (C.c_int, [P]),
     "tsdf_set_profiling": (C.c_int, [P, C.c_int32]),
+    "tsdf_set_metrics_log": (C.c_int, [P, C.c_char_p]),
     "tsdf_select_sector": (C.c_int, [FP, C.c_uint64, D3, C.c_double, C.c_uint32, C.c_uint32, FP,
                                      U64P]),
     "tsdf_sector_of": (C.c_int32, [C.c_float, C.c_float, D3, C.c_double, C.c_uint32]),

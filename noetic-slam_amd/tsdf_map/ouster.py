@@ -87,6 +87,44 @@ def split_frames(packets, fmt, packet_bytes):
     return frames
 
 
+# ouster_ros::Point (reference include/ouster_ros/os_point.h:20-44): PCL_ADD_POINT4D (x, y, z, 1),
+# intensity, t (ns since the scan), reflectivity, ring, ambient, range (mm); EIGEN_ALIGN16 -> 48 B.
+OUSTER_POINT = np.dtype({
+    "names": ["x", "y", "z", "w", "intensity", "t", "reflectivity", "ring", "ambient", "range"],
+    "formats": [np.float32, np.float32, np.float32, np.float32, np.float32, np.uint32, np.uint16,
+                np.uint16, np.uint16, np.uint32],
+    "offsets": [0, 4, 8, 12, 16, 20, 24, 26, 28, 32],
+    "itemsize": 48})
+
+
+def destaggered_cloud(xyz, rng, signal, reflectivity, near_ir, pixel_shift_by_row,
+                      timestamps=None, scan_ts=0):
+    """The organized cloud of ouster_ros' copy_scan_to_cloud_destaggered (reference
+    src/ouster/src/os_ros.cpp:195-229): point (u, v) of the h x w cloud (row u = beam, tgt index
+    u w + v) takes pixel v_shift = (v + w - pixel_shift_by_row[u]) % w of the staggered images and
+    of `xyz` (h w x 3, staggered row-major, as the LUT projection gives it); t = column
+    timestamp - scan_ts (0 if earlier); ring = u.  Host arrays in, a 48-B OUSTER_POINT array out
+    (tsdf_integrate with point_step 48, xyz_offset 0 takes it as is)."""
+    rng = np.asarray(rng)
+    h, w = rng.shape
+    shift = np.asarray(pixel_shift_by_row, np.int64).reshape(h)
+    v = np.arange(w)
+    v_shift = (v[None, :] + w - shift[:, None]) % w           # (h, w)
+    src = (np.arange(h)[:, None] * w + v_shift).reshape(-1)   # staggered source of each target
+    out = np.zeros(h * w, OUSTER_POINT)
+    p = np.asarray(xyz, np.float32).reshape(h * w, 3)[src]
+    out["x"], out["y"], out["z"], out["w"] = p[:, 0], p[:, 1], p[:, 2], 1.0
+    out["intensity"] = np.asarray(signal).reshape(-1)[src].astype(np.float32)
+    if timestamps is not None:
+        ts = np.asarray(timestamps, np.uint64)[v_shift].reshape(-1)
+        out["t"] = np.where(ts > scan_ts, ts - np.uint64(scan_ts), 0).astype(np.uint32)
+    out["reflectivity"] = np.asarray(reflectivity).reshape(-1)[src].astype(np.uint16)
+    out["ring"] = np.repeat(np.arange(h, dtype=np.uint16), w)
+    out["ambient"] = np.asarray(near_ir).reshape(-1)[src].astype(np.uint16)
+    out["range"] = rng.reshape(-1)[src].astype(np.uint32)
+    return out
+
+
 class OusterFrontend:
     """Packets of one frame -> device field images -> world points -> the volume, on the GPU.
     `volume` is a HipTSDFVolume; the work runs on its context's stream, so call sync() before

@@ -293,6 +293,11 @@ class HipTSDFVolume(TSDFVolume):
     def set_profiling(self, on=True):
         self._check(self._lib.tsdf_set_profiling(self._ctx, 1 if on else 0), "set_profiling")
 
+    def set_metrics_log(self, path):
+        """One JSON line per finished GPU batch appended to `path` (None: stop)."""
+        self._check(self._lib.tsdf_set_metrics_log(
+            self._ctx, None if path is None else str(path).encode()), "set_metrics_log")
+
 
 class TsdfIntegratorConfig:
     """voxblox TsdfIntegratorBase::Config (the fields this backend implements; defaults as

@@ -24,6 +24,7 @@ MODE_SCAN_FUSED = 0
 MODE_SEQUENTIAL = 1
 MODE_VDB_LITERAL = 2  # VDBFusion's own precisions (double sdf, Ray<float> DDA), per-sample update
 HOST_ONLY = ("tsdf_integrate_device", "tsdf_integrate_batch_device", "tsdf_set_profiling",
+             "tsdf_set_metrics_log",
              "tsdf_os_packet_bytes", "tsdf_os_decode_device", "tsdf_os_cartesian_device")
 
 _lib = None

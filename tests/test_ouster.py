@@ -121,3 +121,56 @@ def test_gpu_points_and_field_bitwise():
     assert o.export_voxels()[0].shape[0] > 10000
     for x, y in zip(vol.export_voxels(), o.export_voxels()):
         assert np.array_equal(x, y)
+
+
+def test_destaggered_cloud_layout_and_order():
+    """48-B ouster_ros::Point records (os_point.h:20-44) in copy_scan_to_cloud_destaggered order."""
+    from tsdf_map.ouster import OUSTER_POINT, destaggered_cloud
+    assert OUSTER_POINT.itemsize == 48
+    assert [OUSTER_POINT.fields[k][1] for k in ("x", "intensity", "t", "reflectivity", "ring",
+                                                "ambient", "range")] == [0, 16, 20, 24, 26, 28, 32]
+    h, w = 4, 8
+    rng = np.arange(h * w, dtype=np.uint32).reshape(h, w) + 100
+    xyz = np.stack([rng.reshape(-1)] * 3, 1).astype(np.float32)
+    shift = [3, 1, 0, 5]
+    ts = np.arange(w, dtype=np.uint64) * 10 + 1000
+    c = destaggered_cloud(xyz, rng, rng, rng, rng, shift, ts, scan_ts=1020)
+    for u in range(h):
+        for v in range(w):
+            vs = (v + w - shift[u]) % w
+            r = c[u * w + v]
+            assert r["range"] == rng[u, vs] and r["x"] == rng[u, vs] and r["ring"] == u
+            assert r["t"] == max(int(ts[vs]) - 1020, 0) and r["w"] == 1.0
+
+
+@pytest.mark.gpu
+def test_gpu_destaggered_48b_cloud_bitwise():
+    """An organized 48-B cloud of the pinned OS-2-128 frame (destaggered, world frame) integrates
+    through tsdf_integrate(point_step 48) to the same field, bit for bit, as the staggered packed
+    xyz: the per-scan fuse sums each voxel's samples exactly, so point order does not matter."""
+    from tsdf_map import HipTSDFVolume
+    from tsdf_map.ouster import destaggered_cloud
+    js = [f for f in FIXTURES if "OS-2-128" in f][0]
+    meta, fmt, digest, packets = load(js)
+    vol, fe = _frontend(meta)
+    (fid, pk), = fe.frames(packets)
+    ref = R.decode_frames(pk, fmt.profile_name, fmt.h, fmt.w, fmt.columns_per_packet)[0]
+    P = pose(1)
+    imgs = fe.decode(pk)
+    xyz = fe.points(imgs["RANGE"], P)
+    fe.sync()
+    x = xyz.cpu().numpy()
+    cloud = destaggered_cloud(x, ref["RANGE"], ref["SIGNAL"], ref["REFLECTIVITY"], ref["NEAR_IR"],
+                              meta["data_format"]["pixel_shift_by_row"])
+    a = HipTSDFVolume(0.05, 0.15, max_points=1 << 18)
+    a.integrate_cloud(cloud.tobytes(), cloud.shape[0], 48, 0, P[:3, 3])
+    b = HipTSDFVolume(0.05, 0.15, max_points=1 << 18)
+    b.integrate(x, P[:3, 3])
+    a.sync()
+    b.sync()
+    ai, as_, aw = a.export_voxels()
+    bi, bs, bw = b.export_voxels()
+    assert ai.shape[0] > 10000
+    assert np.array_equal(ai, bi) and np.array_equal(aw, bw)
+    assert np.array_equal(as_.view(np.uint32), bs.view(np.uint32))
+    assert a.stats()["n_rays_total"] == np.count_nonzero(ref["RANGE"])  # r = 0 pixels drop
