@@ -7,8 +7,15 @@
 // Input stream (little endian), one record per scan:
 //     u64 n_points, u32 point_step, u32 xyz_offset, i32 xyz_is_f64, f64 origin[3],
 //     n_points * point_step bytes (PointCloud2 data, e.g. dlio::Point records)
-// terminated by end of file.  Output: the map as exported by tsdf_export_bricks:
-//     u64 n_bricks, then n_bricks * (i32 coords[3]), n_bricks * 512 f32 sdf, n_bricks * 512 f32 w.
+// terminated by end of file.  Or, a topic stream (the node's two subscriptions, interleaved in
+// arrival order) starting with the 8 bytes "TSDFSTR2", then records:
+//     'P' i64 stamp_ns, f64 position[3], f64 quaternion[4]            (robot/dlio/odom_node/pose)
+//     'C' i64 stamp_ns, u64 n, u32 point_step, u32 xyz_offset, i32 xyz_is_f64, n * point_step bytes
+//                                                   (robot/dlio/odom_node/pointcloud/deskewed)
+// whose clouds are paired with the pose track at their stamps by tsdf_map::MapCore — the same
+// object tsdf_map_node runs (host/tsdf_map_core.h).  Output: the map as exported by
+// tsdf_export_bricks: u64 n_bricks, then n_bricks * (i32 coords[3]), n_bricks * 512 f32 sdf,
+// n_bricks * 512 f32 w.
 //
 // usage: tsdf_replay <in.scans> <out.bricks> [voxel_size sdf_trunc [semantics]]
 #include <cstdint>
@@ -19,6 +26,7 @@
 #include <vector>
 
 #include "../../include/tsdf_hip.h"
+#include "tsdf_map_core.h"
 
 namespace {
 
@@ -69,7 +77,54 @@ int main(int argc, char** argv) {
     // the points before returning, so the buffer is reused at once)
     std::vector<uint8_t> cloud;
     uint64_t n_scans = 0;
-    for (;;) {
+    char magic[8] = {0};
+    const bool topics = std::fread(magic, 1, 8, in.f) == 8 && std::memcmp(magic, "TSDFSTR2", 8) == 0;
+    if (!topics) std::rewind(in.f);
+    tsdf_map::MapCore core(ctx);
+    for (; topics;) {  // the node's subscriptions, in arrival order
+        char type = 0;
+        int64_t t = 0;
+        if (std::fread(&type, 1, 1, in.f) != 1) break;
+        if (std::fread(&t, sizeof t, 1, in.f) != 1) break;
+        if (type == 'P') {
+            tsdf_map::Pose ps;
+            ps.t_ns = t;
+            if (std::fread(ps.p, sizeof(double), 3, in.f) != 3 ||
+                std::fread(ps.q, sizeof(double), 4, in.f) != 4)
+                break;
+            rc = core.on_pose(ps);
+        } else if (type == 'C') {
+            uint64_t n = 0;
+            uint32_t step = 0, xoff = 0;
+            int32_t f64 = 0;
+            if (std::fread(&n, sizeof n, 1, in.f) != 1 || std::fread(&step, 4, 1, in.f) != 1 ||
+                std::fread(&xoff, 4, 1, in.f) != 1 || std::fread(&f64, 4, 1, in.f) != 1)
+                break;
+            cloud.resize((size_t)n * step);
+            if (n && std::fread(cloud.data(), step, n, in.f) != n) break;
+            rc = core.on_cloud(t, cloud.data(), n, step, xoff, f64);
+        } else {
+            std::fprintf(stderr, "tsdf_replay: bad record type %d\n", (int)type);
+            tsdf_destroy(ctx);
+            return 1;
+        }
+        if (rc != TSDF_OK) {
+            const int r = die(ctx, "tsdf_integrate", rc);
+            tsdf_destroy(ctx);
+            return r;
+        }
+    }
+    if (topics) {
+        rc = core.flush();
+        if (rc != TSDF_OK) return die(ctx, "tsdf_integrate", rc);
+        n_scans = core.counts().integrated;
+        std::printf("tsdf_replay: paired %llu clouds, dropped %llu (outside the track) %llu (gap) "
+                    "%llu (queue)\n", (unsigned long long)core.counts().integrated,
+                    (unsigned long long)core.counts().dropped_old,
+                    (unsigned long long)core.counts().dropped_gap,
+                    (unsigned long long)core.counts().dropped_queue);
+    }
+    for (; !topics;) {
         uint64_t n = 0;
         uint32_t step = 0, xoff = 0;
         int32_t f64 = 0;

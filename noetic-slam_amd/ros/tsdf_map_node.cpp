@@ -1,0 +1,204 @@
+// tsdf_map_node — the reference's TSDF mapping node (README.md:44-50) with the MI355X backend,
+// MAP_BACKEND_IDX = 4.  ROS1 noetic; built by this directory's CMakeLists.txt inside a catkin
+// workspace only (it needs roscpp, sensor_msgs, geometry_msgs, nav_msgs; nothing else of ROS is
+// used, and no PCL: the PointCloud2 bytes go to the library as they arrive).
+//
+// Subscriptions (the reference's topic names, launch/dlio.launch:15-38):
+//   ~cloud_topic  robot/dlio/odom_node/pointcloud/deskewed  sensor_msgs/PointCloud2 (dlio::Point,
+//                 world frame; the slot of Dliomapping_Node::callback_pcl_deskewed,
+//                 src/dliomapping/dliomapping.cpp:44,64-81)
+//   ~pose_topic   robot/dlio/odom_node/pose                 geometry_msgs/PoseStamped (100 Hz,
+//                 stamped with imu_stamp, src/dlio/src/dlio/odom.cc:318,383)
+//   ~path_topic   (optional) robot/dlio/odom_node/path      nav_msgs/Path (per scan, odom.cc:358-432)
+// Each cloud's ray origin is the pose track at the cloud's stamp (odom.cc:447), interpolated —
+// tsdf_map::MapCore (host/tsdf_map_core.h), the object the headless driver host/tsdf_replay runs in
+// the tests (tests/test_host_replay.py::test_topic_stream_*), so the pairing shipped here is the one
+// tested.  Clouds newer than the newest pose wait for it.
+//
+// On shutdown the map is written like dliomapping's destructor writes its PLY (dliomapping.cpp:53-61):
+// ~map_path (bricks: u64 n, i32 coords[3 n], f32 sdf[512 n], f32 weight[512 n]) and, with
+// ~mesh_path set, a binary PLY triangle soup from tsdf_extract_mesh.
+#include <geometry_msgs/PoseStamped.h>
+#include <nav_msgs/Path.h>
+#include <ros/ros.h>
+#include <sensor_msgs/PointCloud2.h>
+#include <sensor_msgs/PointField.h>
+
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "../../include/tsdf_hip.h"
+#include "../host/tsdf_map_core.h"
+
+namespace {
+
+tsdf_map::Pose to_pose(const std_msgs::Header& h, const geometry_msgs::Pose& p) {
+    tsdf_map::Pose s;
+    s.t_ns = (int64_t)h.stamp.toNSec();
+    s.p[0] = p.position.x;
+    s.p[1] = p.position.y;
+    s.p[2] = p.position.z;
+    s.q[0] = p.orientation.x;
+    s.q[1] = p.orientation.y;
+    s.q[2] = p.orientation.z;
+    s.q[3] = p.orientation.w;
+    return s;
+}
+
+class TsdfMapNode {
+   public:
+    explicit TsdfMapNode(ros::NodeHandle& nh, ros::NodeHandle& pnh) {
+        tsdf_params p;
+        tsdf_default_params(&p);  // 5 cm voxels, 15 cm truncation, no carving
+        pnh.param("voxel_size", p.voxel_size, 0.05);
+        pnh.param("sdf_trunc", p.sdf_trunc, 0.15);
+        bool carving = false;
+        pnh.param("space_carving", carving, false);
+        p.space_carving = carving ? 1 : 0;
+        pnh.param("min_range", p.min_range, 1.0);  // DLIO already crops +-1 m (odom.cc:490-526)
+        int max_batch = 8, device = 0, pipeline = 0;
+        pnh.param("max_batch", max_batch, max_batch);  // scans per GPU batch (latency vs rate)
+        pnh.param("device_id", device, device);
+        pnh.param("pipeline", pipeline, pipeline);
+        p.max_batch = (uint32_t)max_batch;
+        p.device_id = device;
+        p.pipeline = (uint32_t)pipeline;
+        int max_bricks = 1 << 20;
+        pnh.param("max_bricks", max_bricks, max_bricks);  // initial pool; grows on demand
+        p.max_bricks = (uint64_t)max_bricks;
+        std::string sem;
+        pnh.param<std::string>("semantics", sem, "vdbfusion");
+        if (sem == "voxblox") {  // backend idx 2's rule
+            p.semantics = TSDF_SEM_VOXBLOX;
+            pnh.param("max_ray_length_m", p.max_range, 5.0);
+            double mw = 10000.0;
+            pnh.param("max_weight", mw, mw);
+            p.max_weight = (float)mw;
+            bool clear = true, drop = true;
+            pnh.param("allow_clear", clear, clear);
+            pnh.param("use_weight_dropoff", drop, drop);
+            p.allow_clear = clear ? 1 : 0;
+            p.use_weight_dropoff = drop ? 1 : 0;
+        } else if (sem == "vdbfusion_f64") {  // upstream's precisions
+            p.semantics = TSDF_SEM_VDBFUSION_F64;
+        }
+        if (tsdf_create(&p, &ctx_) != TSDF_OK) {
+            ROS_FATAL("tsdf_create failed (see stderr)");
+            ros::shutdown();
+            return;
+        }
+        double max_gap_ms = 50.0;
+        pnh.param("max_pose_gap_ms", max_gap_ms, max_gap_ms);
+        core_ = new tsdf_map::MapCore(ctx_, max_gap_ms);
+        std::string metrics;
+        pnh.param<std::string>("metrics_log", metrics, "");
+        if (!metrics.empty() && tsdf_set_metrics_log(ctx_, metrics.c_str()) != TSDF_OK)
+            ROS_WARN("metrics log: %s", tsdf_last_error(ctx_));
+        pnh.param<std::string>("map_path", map_path_, "tsdf_map.bricks");
+        pnh.param<std::string>("mesh_path", mesh_path_, "");
+        std::string cloud_topic, pose_topic, path_topic;
+        pnh.param<std::string>("cloud_topic", cloud_topic, "robot/dlio/odom_node/pointcloud/deskewed");
+        pnh.param<std::string>("pose_topic", pose_topic, "robot/dlio/odom_node/pose");
+        pnh.param<std::string>("path_topic", path_topic, "");
+        sub_pose_ = nh.subscribe(pose_topic, 1000, &TsdfMapNode::on_pose, this);
+        if (!path_topic.empty()) sub_path_ = nh.subscribe(path_topic, 10, &TsdfMapNode::on_path, this);
+        sub_cloud_ = nh.subscribe(cloud_topic, 100, &TsdfMapNode::on_cloud, this);
+    }
+
+    ~TsdfMapNode() {
+        if (!ctx_) return;
+        core_->flush();
+        save();
+        delete core_;
+        tsdf_destroy(ctx_);
+    }
+
+    void on_pose(const geometry_msgs::PoseStampedConstPtr& m) {
+        check(core_->on_pose(to_pose(m->header, m->pose)), "integrate");
+    }
+
+    void on_path(const nav_msgs::PathConstPtr& m) {
+        if (m->poses.empty()) return;
+        const auto& last = m->poses.back();  // /path grows by one pose per scan
+        check(core_->on_pose(to_pose(last.header, last.pose)), "integrate");
+    }
+
+    // replaces Dliomapping_Node::callback_pcl_deskewed (dliomapping.cpp:64-81): no fromROSMsg,
+    // the library reads x, y, z where the message says they are
+    void on_cloud(const sensor_msgs::PointCloud2ConstPtr& msg) {
+        int xoff = -1, f64 = 0;
+        for (const auto& f : msg->fields)
+            if (f.name == "x") {
+                xoff = (int)f.offset;
+                f64 = f.datatype == sensor_msgs::PointField::FLOAT64;
+            }
+        if (xoff < 0 || msg->is_bigendian) {
+            ROS_WARN_THROTTLE(5.0, "cloud without little-endian x, y, z: skipped");
+            return;
+        }
+        const uint64_t n = (uint64_t)msg->width * msg->height;
+        check(core_->on_cloud((int64_t)msg->header.stamp.toNSec(), msg->data.data(), n,
+                              msg->point_step, (uint32_t)xoff, f64),
+              "integrate");
+    }
+
+   private:
+    void check(int rc, const char* what) {
+        if (rc != TSDF_OK) ROS_ERROR("tsdf %s: %s", what, tsdf_last_error(ctx_));
+    }
+
+    void save() {
+        uint64_t nb = 0;
+        if (tsdf_num_bricks(ctx_, &nb) != TSDF_OK) return;
+        std::vector<int32_t> c(3 * nb);
+        std::vector<float> s(512 * nb), w(512 * nb);
+        uint64_t got = 0;
+        if (tsdf_export_bricks(ctx_, c.data(), s.data(), w.data(), nb, &got) == TSDF_OK) {
+            if (FILE* f = std::fopen(map_path_.c_str(), "wb")) {
+                std::fwrite(&got, 8, 1, f);
+                std::fwrite(c.data(), 4, 3 * got, f);
+                std::fwrite(s.data(), 4, 512 * got, f);
+                std::fwrite(w.data(), 4, 512 * got, f);
+                std::fclose(f);
+                ROS_INFO("saved %llu bricks to %s", (unsigned long long)got, map_path_.c_str());
+            }
+        }
+        if (mesh_path_.empty()) return;
+        uint64_t nt = 0;
+        if (tsdf_extract_mesh(ctx_, 0.0f, nullptr, 0, &nt) != TSDF_OK) return;
+        std::vector<float> tri(9 * nt);
+        if (tsdf_extract_mesh(ctx_, 0.0f, tri.data(), nt, &nt) != TSDF_OK) return;
+        if (FILE* f = std::fopen(mesh_path_.c_str(), "wb")) {  // binary PLY triangle soup
+            std::fprintf(f,
+                         "ply\nformat binary_little_endian 1.0\nelement vertex %llu\n"
+                         "property float x\nproperty float y\nproperty float z\n"
+                         "element face %llu\nproperty list uchar int vertex_indices\nend_header\n",
+                         (unsigned long long)(3 * nt), (unsigned long long)nt);
+            std::fwrite(tri.data(), 4, 9 * nt, f);
+            for (uint64_t t = 0; t < nt; t++) {
+                const unsigned char three = 3;
+                const int32_t v[3] = {(int32_t)(3 * t), (int32_t)(3 * t + 1), (int32_t)(3 * t + 2)};
+                std::fwrite(&three, 1, 1, f);
+                std::fwrite(v, 4, 3, f);
+            }
+            std::fclose(f);
+            ROS_INFO("saved %llu triangles to %s", (unsigned long long)nt, mesh_path_.c_str());
+        }
+    }
+
+    tsdf_ctx* ctx_ = nullptr;
+    tsdf_map::MapCore* core_ = nullptr;
+    ros::Subscriber sub_cloud_, sub_pose_, sub_path_;
+    std::string map_path_, mesh_path_;
+};
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    ros::init(argc, argv, "tsdf_map_node");
+    ros::NodeHandle nh, pnh("~");
+    TsdfMapNode node(nh, pnh);
+    ros::spin();  // single-threaded: one context, one thread (include/tsdf_hip.h)
+    return 0;
+}

@@ -90,3 +90,88 @@ def test_replay_driver_on_gpu_bitwise(tmp_path, sim, semantics):
     assert got[0].shape[0] > 1000
     assert np.array_equal(got[0], ref[0]) and np.array_equal(got[2], ref[2])
     assert np.array_equal(got[1].view(np.uint32), ref[1].view(np.uint32))
+
+
+# ---- the node's two subscriptions: clouds paired with the 100 Hz pose track (host/tsdf_map_core.h)
+
+def topic_stream(sim):
+    """(records, expected clouds with their origins): DLIO-like arrival order — poses at 100 Hz,
+    each cloud stamped 3 ms after a pose sample and arriving before the sample that brackets it;
+    one cloud older than the track and one inside a 60 ms pose gap are dropped."""
+    from tsdf_map.ingest import PoseTrack
+    t0 = 1_000_000_000
+    track = PoseTrack()
+    recs, want = [], []
+
+    def pose(t):
+        a = (t - t0) * 1e-9
+        return (2.0 + 3.0 * np.cos(0.3 * a), -1.0 + 3.0 * np.sin(0.3 * a), 0.05 * a), (0, 0, 0, 1)
+
+    clouds = {0: 0, 1: 1, 2: 5, 3: 9}
+    recs.append(("C", t0 - 5_000_000, decimate(sim.scan(7)[0], 16)))  # before the track: dropped
+    for k in range(4):
+        for j in range(10):
+            t = t0 + (k * 10 + j) * 10_000_000
+            if k == 2 and j in (4, 5, 6, 7, 8):
+                continue  # a 60 ms gap in the pose stream
+            p, q = pose(t)
+            track.add(t, p, q)
+            recs.append(("P", t, (p, q)))
+            if j == 9 or (k == 2 and j == 3):
+                tc = t + 3_000_000 if j == 9 else t + 33_000_000  # the latter falls in the gap
+                pts = decimate(sim.scan(clouds[k])[0], 16)
+                recs.append(("C", tc, pts))
+                if j == 9:
+                    want.append((tc, pts))
+    t = t0 + 40 * 10_000_000
+    p, q = pose(t)
+    track.add(t, p, q)
+    recs.append(("P", t, (p, q)))
+    return recs, [(pts, track.at(tc)[0]) for tc, pts in want]
+
+
+def write_topics(path, recs):
+    with open(path, "wb") as f:
+        f.write(b"TSDFSTR2")
+        for kind, t, v in recs:
+            if kind == "P":
+                f.write(b"P" + struct.pack("<q3d4d", t, *v[0], *v[1]))
+            else:
+                rec = dlio_records(v)
+                f.write(b"C" + struct.pack("<qQIIi", t, rec.shape[0], 32, 0, 0) + rec.tobytes())
+
+
+def test_topic_stream_pairs_poses_like_ingest(tmp_path, sim):
+    """MapCore (the node's logic, C++) pairs every cloud with the pose track at its stamp exactly
+    as tsdf_map.ingest.PoseTrack does: the replay, linked against the oracle library, writes the
+    map of integrating the clouds from those origins."""
+    lib = oracle.load()
+    del lib
+    exe = tmp_path / "tsdf_replay_oracle"
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-o", str(exe),
+                           os.path.join(HOST, "tsdf_replay.cpp"),
+                           "-L" + os.path.dirname(oracle.LIB_PATH), "-ltsdf_oracle",
+                           "-Wl,-rpath," + os.path.dirname(oracle.LIB_PATH)])
+    recs, want = topic_stream(sim)
+    write_topics(tmp_path / "in.topics", recs)
+    out = subprocess.run([str(exe), str(tmp_path / "in.topics"), str(tmp_path / "out.bricks")],
+                         capture_output=True, text=True, check=True)
+    assert "paired 4 clouds, dropped 1 (outside the track) 1 (gap)" in out.stdout
+    got = bricks_to_voxels(*read_bricks(tmp_path / "out.bricks"))
+    ref = oracle_voxels(want)
+    for a, b in zip(got, ref):
+        assert np.array_equal(a, b)
+
+
+@pytest.mark.gpu
+def test_topic_stream_on_gpu_bitwise(tmp_path, sim):
+    exe = os.path.join(REPO, "noetic-slam_amd", "lib", "tsdf_replay")
+    recs, want = topic_stream(sim)
+    write_topics(tmp_path / "in.topics", recs)
+    out = subprocess.run([exe, str(tmp_path / "in.topics"), str(tmp_path / "out.bricks")],
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    got = bricks_to_voxels(*read_bricks(tmp_path / "out.bricks"))
+    ref = oracle_voxels(want)
+    assert np.array_equal(got[0], ref[0]) and np.array_equal(got[2], ref[2])
+    assert np.array_equal(got[1].view(np.uint32), ref[1].view(np.uint32))
