@@ -35,7 +35,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=32)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=64,
-                    help="scans per GPU per step (one GPU batch, <= 64; the field does not depend on it)")
+                    help="scans per GPU per step: with N sector shards a step holds N x batch full "
+                         "scans, integrated by every rank as ONE GPU batch (<= 512 scans; the field "
+                         "does not depend on batching)")
     ap.add_argument("--voxel", type=float, default=0.05)
     ap.add_argument("--trunc", type=float, default=0.15)
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
@@ -55,6 +57,11 @@ def parse():
                     help="brick pool capacity (4 KiB per brick)")
     ap.add_argument("--semantics", default="vdbfusion", choices=("vdbfusion", "voxblox", "vdbfusion_f64"),
                     help="fusion rule (tsdf_params.semantics); the headline metric is vdbfusion")
+    ap.add_argument("--rank-rehearsal", type=int, default=0, metavar="N",
+                    help="one process plays rank 0 of an N-GPU run (sector 0 of N, N x batch full "
+                         "scans per step): its time per step is one rank's; value = N x batch "
+                         "scans / step time, the N-GPU throughput if every rank took as long "
+                         "(rehearsal of the scaling runs on a one-GPU box)")
     ap.add_argument("--no-profile", action="store_true",
                     help="do not record per-kernel HIP events in the timed region")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_r01.json"),
@@ -94,7 +101,8 @@ def main():
     # ---- synthesize every (full) scan of every step, resident in HBM ----------------------------
     sim = TorchOusterSim(dev, beams=args.sensor, hz=args.hz)
     n_steps = args.warmup + args.steps
-    scans_per_step = world * args.batch
+    n_shards = args.rank_rehearsal if (args.rank_rehearsal > 1 and world == 1) else world
+    scans_per_step = n_shards * args.batch
     steps = []
     t_gen = time.time()
     for s in range(n_steps):
@@ -112,9 +120,10 @@ def main():
     max_pts = max(int(np.diff(o).max()) for _, o, _ in steps)
 
     vol = HipTSDFVolume(args.voxel, args.trunc, max_points=max(max_pts, 1 << 17),
-                        max_bricks=args.max_bricks, device_id=local, max_batch=min(args.batch, 64),
+                        max_bricks=args.max_bricks, device_id=local,
+                        max_batch=min(scans_per_step, 512),  # one launch per step (all shards)
                         pipeline=args.pipeline, semantics=args.semantics,
-                        n_sectors=world, sector=rank)  # this rank's azimuth sector of every scan
+                        n_sectors=n_shards, sector=rank)  # this rank's azimuth sector of every scan
 
     def run_step(i):
         x, offs, org = steps[i]
@@ -256,11 +265,13 @@ def main():
                                                                             args.hz)),
                        "voxel_size_m": args.voxel, "sdf_trunc_m": args.trunc,
                        "scans_per_step": scans_per_step, "global_batch": scans_per_step,
-                       "points_per_scan": int(round(rays_per_scan * world)),
+                       "points_per_scan": int(round(rays_per_scan * n_shards)),
                     "scans_per_gpu_batch": args.batch, "pipelined_batches": args.pipeline,
                        "semantics": args.semantics,
-                       "parallelism": "azimuth-sector x%d" % world if world > 1 else "single",
-                       "sector_split": "in-kernel (timed)" if world > 1 else None},
+                       "parallelism": ("azimuth-sector x%d" % world if world > 1 else
+                                       "rank-0 rehearsal of azimuth-sector x%d" % n_shards
+                                       if n_shards > 1 else "single"),
+                       "sector_split": "in-kernel (timed)" if n_shards > 1 else None},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "path_ms_per_scan": round(path_ms_per_scan, 5),

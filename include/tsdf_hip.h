@@ -37,7 +37,7 @@ extern "C" {
 #endif
 
 #define TSDF_ABI_VERSION 4
-#define TSDF_MAX_BATCH 64 /* scans per GPU batch (see tsdf_params.max_batch) */
+#define TSDF_MAX_BATCH 512 /* scans per GPU batch (see tsdf_params.max_batch) */
 #define TSDF_BRICK_SIDE 8 /* voxels per brick edge: a brick is 8^3 = 512 voxels */
 
 /* status codes */

@@ -165,6 +165,13 @@ struct tsdf_ctx {
     hipEvent_t ev_main = nullptr;
     hipEvent_t ev_compact[2] = {nullptr, nullptr}, ev_integ[2] = {nullptr, nullptr};
     BatchDesc pend{};  // pending host scans (points in stage2[batch_id & 1])
+    // batch records for the kernels: a pinned host ring and its device twin (launch() copies a
+    // batch's n_scans + 1 records into the next slot on the batch's stream)
+    static constexpr int RING = 16;
+    ScanRec* h_ring = nullptr;
+    ScanRec* d_ring = nullptr;
+    hipEvent_t ring_ev[RING] = {};
+    uint64_t ring_next = 0;
     uint64_t batch_id = 0;
     uint64_t n_scans = 0, n_batches = 0, n_points_in = 0;
     EventTimer* timer = nullptr;
@@ -244,10 +251,10 @@ static int launch(tsdf_ctx* c, const float* d_xyz, BatchDesc& D) {
         if (!rc) rc = check_and_replay(c);
         if (rc) return rc;
     }
-    D.blk[0] = 0;
+    D.s[0].blk = 0;
     for (uint32_t s = 0; s < D.n_scans; s++)
-        D.blk[s + 1] = D.blk[s] + (D.off[s + 1] - D.off[s] + RPB - 1) / RPB;
-    D.n_blocks = D.blk[D.n_scans];
+        D.s[s + 1].blk = D.s[s].blk + (D.s[s + 1].off - D.s[s].off + RPB - 1) / RPB;
+    D.n_blocks = D.s[D.n_scans].blk;
     if (D.n_blocks > c->max_blocks)
         return fail(c, TSDF_EINVAL, "batch needs %u workgroups > %u", D.n_blocks, c->max_blocks);
     const int par = (int)(c->batch_id & 1);
@@ -264,7 +271,7 @@ static int launch(tsdf_ctx* c, const float* d_xyz, BatchDesc& D) {
     const Work& W = c->W2[par];
     EventTimer* tm = c->timer;
     if (tm) tm->cur_batch = c->batch_id;
-    if (c->metrics) c->metrics_info.push_back({c->batch_id, D.n_scans, D.off[D.n_scans]});
+    if (c->metrics) c->metrics_info.push_back({c->batch_id, D.n_scans, D.s[D.n_scans].off});
     // staging uploads, imports, ... (an idle context stream has nothing to order against)
     if (hipStreamQuery(c->stream) != hipSuccess) {
         HIPCHK(c, hipEventRecord(c->ev_main, c->stream));
@@ -273,12 +280,22 @@ static int launch(tsdf_ctx* c, const float* d_xyz, BatchDesc& D) {
     if (c->batch_id > 0 && cross)  // pipelined: after the previous batch's compact; else after all of it
         HIPCHK(c, hipStreamWaitEvent(st, c->p.pipeline ? c->ev_compact[par ^ 1]
                                                        : c->ev_integ[par ^ 1], 0));
+    // the batch's scan records -> the device (a ring slot; the host slot is reused once its copy ran)
+    const int slot = (int)(c->ring_next++ % tsdf_ctx::RING);
+    HIPCHK(c, hipEventSynchronize(c->ring_ev[slot]));
+    ScanRec* hs = c->h_ring + (size_t)slot * (MAX_BATCH + 1);
+    ScanRec* ds = c->d_ring + (size_t)slot * (MAX_BATCH + 1);
+    std::memcpy(hs, D.s, (D.n_scans + 1) * sizeof(ScanRec));
+    HIPCHK(c, hipMemcpyAsync(ds, hs, (D.n_scans + 1) * sizeof(ScanRec), hipMemcpyHostToDevice, st));
+    HIPCHK(c, hipEventRecord(c->ring_ev[slot], st));
+    const BatchRef B{D.n_scans, D.n_blocks, ds};
     if (D.n_blocks) {
         if (tm) tm->begin(KIND_COUNT, st);
-        HIPCHK(c, launch_count(d_xyz, D, c->R, T, W, c->G, par, st));
+        if (c->R.sec_on) HIPCHK(c, launch_sector_flags(d_xyz, B, c->R, W, c->G, par, st));
+        HIPCHK(c, launch_count(d_xyz, B, c->R, T, W, c->G, par, st));
         if (tm) tm->end(KIND_COUNT, st);
         if (tm) tm->begin(KIND_COMPACT, st);
-        HIPCHK(c, launch_compact(D, T, W, c->G, par, st));
+        HIPCHK(c, launch_compact(B, T, W, c->G, par, st));
 #ifndef TSDF_NO_ORDER
         HIPCHK(c, launch_order(W, c->G, par, st));
 #endif
@@ -287,7 +304,7 @@ static int launch(tsdf_ctx* c, const float* d_xyz, BatchDesc& D) {
     HIPCHK(c, hipEventRecord(c->ev_compact[par], st));
     if (D.n_blocks) {
         if (tm) tm->begin(KIND_PLACE, st);
-        HIPCHK(c, launch_place(d_xyz, D, c->R, T, W, st));
+        HIPCHK(c, launch_place(d_xyz, B, c->R, T, W, c->G, par, st));
         if (tm) tm->end(KIND_PLACE, st);
     }
     if (c->batch_id > 0 && cross) HIPCHK(c, hipStreamWaitEvent(st, c->ev_integ[par ^ 1], 0));
@@ -296,9 +313,9 @@ static int launch(tsdf_ctx* c, const float* d_xyz, BatchDesc& D) {
 #ifndef TSDF_NO_ORDER
         Work Wi = W;
         Wi.active = W.active_ord;  // largest bricks first (k_order)
-        HIPCHK(c, launch_integrate(D, c->R, T, Wi, c->Pl, c->G, par, st));
+        HIPCHK(c, launch_integrate(B, c->R, T, Wi, c->Pl, c->G, par, st));
 #else
-        HIPCHK(c, launch_integrate(D, c->R, T, W, c->Pl, c->G, par, st));
+        HIPCHK(c, launch_integrate(B, c->R, T, W, c->Pl, c->G, par, st));
 #endif
         if (tm) tm->end(KIND_INTEGRATE, st);
     }
@@ -328,7 +345,7 @@ static int flush(tsdf_ctx* c) {
     if (c->pend.n_scans == 0) return TSDF_OK;
     const int rc = launch(c, c->stage2[c->batch_id & 1], c->pend);
     c->pend.n_scans = 0;
-    c->pend.off[0] = 0;
+    c->pend.s[0].off = 0;
     return rc;
 }
 
@@ -510,6 +527,28 @@ static int drain_all(tsdf_ctx* c) {
 // batches from it (their inputs are still valid), until a round succeeds.  Without growth (hard
 // limit, or a non-growable overflow) the batches are re-run committing what fits, and tsdf_sync
 // reports the overflow.
+// Double both parities' sample lists (OVF_SMP), up to the 32-bit sample index.
+static int grow_smp(tsdf_ctx* c) {
+    const uint64_t ns = std::min<uint64_t>(2ull * c->Wk.max_smp, 0xFFFFFFF0ull);
+    if (ns <= c->Wk.max_smp) return fail(c, TSDF_ENOMEM, "sample list at its limit");
+    uint2* f[2] = {nullptr, nullptr};
+    hipError_t e = hipMalloc(&f[0], ns * sizeof(uint2));
+    if (e == hipSuccess) e = hipMalloc(&f[1], ns * sizeof(uint2));
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        for (auto q : f) if (q) (void)hipFree(q);
+        return fail(c, TSDF_ENOMEM, "sample list allocation failed");
+    }
+    for (int q = 0; q < 2; q++) {
+        (void)hipFree(c->W2[q].smp);
+        c->W2[q].smp = f[q];
+        c->W2[q].max_smp = (uint32_t)ns;
+    }
+    c->Wk.max_smp = (uint32_t)ns;
+    c->n_grows++;
+    return TSDF_OK;
+}
+
 static int check_and_replay(tsdf_ctx* c) {
     for (int round = 0; round < 64; round++) {
         struct { uint32_t pool_count, overflow, failed, retry, fail_id; } g;
@@ -530,6 +569,7 @@ static int check_and_replay(tsdf_ctx* c) {
             if (g.overflow & (OVF_TABLE | OVF_POOL | OVF_ACTIVE))
                 rc = grow_capacity(c, std::max<uint64_t>(g.pool_count, c->T.max_bricks + 1));
             if (rc == TSDF_OK && (g.overflow & OVF_FB)) rc = grow_fb(c);
+            if (rc == TSDF_OK && (g.overflow & OVF_SMP)) rc = grow_smp(c);
             if (rc == TSDF_EHIP) return rc;
         }
         // the replay: from the first failed batch on, in order
@@ -542,9 +582,9 @@ static int check_and_replay(tsdf_ctx* c) {
             c->can_grow = false;
             const uint32_t z[2] = {0u, 0u};  // failed, retry
             HIPCHK(c, hipMemcpy(&c->G->failed, z, 8, hipMemcpyHostToDevice));
-        } else {
-            const uint32_t z = 0u;
-            HIPCHK(c, hipMemcpy(&c->G->failed, &z, 4, hipMemcpyHostToDevice));
+        } else {  // grown: the replay re-raises whatever still does not fit
+            const uint32_t z[2] = {0u, 0u};  // overflow, failed
+            HIPCHK(c, hipMemcpy(&c->G->overflow, z, 8, hipMemcpyHostToDevice));
         }
         c->in_replay = true;
         for (auto& L : rep) {
@@ -746,7 +786,7 @@ void tsdf_destroy(tsdf_ctx* c) {
                    c->W2[0].smp,     c->W2[0].active,  c->W2[0].active_ord, c->W2[1].active_ord,
                    c->W2[0].ord_hist, c->W2[1].ord_hist,    c->W2[1].pair,    c->W2[1].blk,
                    c->W2[1].blk_n, c->W2[1].fb,        c->W2[1].smp,     c->W2[1].active,
-                   c->W2[0].cagg,    c->W2[1].cagg};
+                   c->W2[0].cagg,    c->W2[1].cagg,      c->W2[0].act,     c->W2[1].act};
     for (void* d : dev)
         if (d) (void)hipFree(d);
     for (int i = 0; i < 2; i++) {
@@ -759,6 +799,10 @@ void tsdf_destroy(tsdf_ctx* c) {
         if (c->ev_integ[q]) (void)hipEventDestroy(c->ev_integ[q]);
     }
     if (c->ev_main) (void)hipEventDestroy(c->ev_main);
+    for (int k = 0; k < tsdf_ctx::RING; k++)
+        if (c->ring_ev[k]) (void)hipEventDestroy(c->ring_ev[k]);
+    if (c->h_ring) (void)hipHostFree(c->h_ring);
+    if (c->d_ring) (void)hipFree(c->d_ring);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -809,11 +853,12 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
     // the host queue then cuts batches by points.  A single scan must always fit.
     const uint32_t maxp = pairs_per_ray(*p);
     const uint32_t spr = samples_per_ray(*p);
-    const uint64_t smp_budget = 1ull << 30;  // samples per batch (8 GiB of 8-byte records)
+    // sample list: the worst case (spr per ray) of the rays a context keeps — 1 / n_sectors of them
+    // when sharded — capped at 2^30 samples (8 GiB); an overflow grows it (OVF_SMP)
+    const uint64_t smp_budget = 1ull << 30;
     c->max_batch = p->max_batch;
     uint64_t bp = p->max_points * c->max_batch;
     bp = std::min<uint64_t>(bp, 0xFFFFFFF0ull / maxp);
-    bp = std::min<uint64_t>(bp, smp_budget / spr);
     if (p->max_pairs) bp = std::min<uint64_t>(bp, p->max_pairs / maxp);  // caller-imposed cap
     if (bp < p->max_points)
         return fail(c, TSDF_EINVAL,
@@ -826,7 +871,9 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
     c->slots = slots;
     c->T.cell_stride = (c->max_batch + 3u) & ~3u;
     c->Wk.maxp = maxp;
-    c->Wk.max_smp = (uint32_t)std::min<uint64_t>(bp * spr, 0xFFFFFFF0ull);
+    c->Wk.max_smp = (uint32_t)std::min<uint64_t>(
+        std::min<uint64_t>(bp * spr / std::max<uint32_t>(1u, p->n_sectors), smp_budget),
+        0xFFFFFFF0ull);
     // fallback pairs (a workgroup's LDS brick hash is full): rare without carving, the rule with it
     // (the fallback index has 26 bits; past it pairs are dropped and OVF_FB reported)
     c->Wk.max_fb = (uint32_t)std::min<uint64_t>(
@@ -842,9 +889,15 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
         HIPCHK(c, hipMalloc(&W.fb, (size_t)W.max_fb * sizeof(uint4)));
         HIPCHK(c, hipMalloc(&W.smp, (size_t)W.max_smp * sizeof(uint2)));
         HIPCHK(c, hipMalloc(&W.ord_hist, 64 * 32 * sizeof(uint32_t)));
+        HIPCHK(c, hipMalloc(&W.act, (size_t)c->max_blocks * sizeof(uint32_t)));
         HIPCHK(c, hipMalloc(&c->stage2[q], c->batch_points * 3 * sizeof(float)));
     }
     HIPCHK(c, hipMalloc(&c->G, sizeof(Globals)));
+    HIPCHK(c, hipHostMalloc(&c->h_ring, tsdf_ctx::RING * (MAX_BATCH + 1) * sizeof(ScanRec),
+                            hipHostMallocDefault));
+    HIPCHK(c, hipMalloc(&c->d_ring, tsdf_ctx::RING * (MAX_BATCH + 1) * sizeof(ScanRec)));
+    for (int k = 0; k < tsdf_ctx::RING; k++)
+        HIPCHK(c, hipEventCreateWithFlags(&c->ring_ev[k], hipEventDisableTiming));
     HIPCHK(c, hipMemsetAsync(c->G, 0, sizeof(Globals), c->stream));
     // the brick pool, hash table and per-brick work lists (grown later by grow_capacity)
     {
@@ -898,12 +951,12 @@ int tsdf_create(const tsdf_params* p, tsdf_ctx** out) {
 }
 
 static void set_origin(BatchDesc& D, uint32_t s, const double o[3]) {
-    D.ox[s] = (float)o[0];
-    D.oy[s] = (float)o[1];
-    D.oz[s] = (float)o[2];
-    D.odx[s] = o[0];
-    D.ody[s] = o[1];
-    D.odz[s] = o[2];
+    D.s[s].ox = (float)o[0];
+    D.s[s].oy = (float)o[1];
+    D.s[s].oz = (float)o[2];
+    D.s[s].odx = o[0];
+    D.s[s].ody = o[1];
+    D.s[s].odz = o[2];
 }
 
 int tsdf_integrate(tsdf_ctx* c, const void* pts, uint64_t n, uint32_t point_step,
@@ -917,7 +970,7 @@ int tsdf_integrate(tsdf_ctx* c, const void* pts, uint64_t n, uint32_t point_step
         return fail(c, TSDF_EINVAL, "scan of %llu points exceeds max_points %llu",
                     (unsigned long long)n, (unsigned long long)c->max_points);
     HIPCHK(c, hipSetDevice(c->device));
-    if (c->pend.n_scans == c->max_batch || c->pend.off[c->pend.n_scans] + n > c->batch_points) {
+    if (c->pend.n_scans == c->max_batch || c->pend.s[c->pend.n_scans].off + n > c->batch_points) {
         const int rc = flush(c);
         if (rc) return rc;
     }
@@ -967,12 +1020,12 @@ int tsdf_integrate(tsdf_ctx* c, const void* pts, uint64_t n, uint32_t point_step
     }
     const int sp = (int)(c->batch_id & 1);  // the pending batch's parity (after any replay)
     if (n) {
-        HIPCHK(c, hipMemcpyAsync(c->stage2[sp] + 3 * (uint64_t)D.off[s], h, n * 12,
+        HIPCHK(c, hipMemcpyAsync(c->stage2[sp] + 3 * (uint64_t)D.s[s].off, h, n * 12,
                                  hipMemcpyHostToDevice, c->stream));
     }
     HIPCHK(c, hipEventRecord(c->stage_done[b], c->stream));
     set_origin(D, s, origin);
-    D.off[s + 1] = D.off[s] + (uint32_t)n;
+    D.s[s + 1].off = D.s[s].off + (uint32_t)n;
     D.n_scans = s + 1;
     c->n_points_in += n;
     if (D.n_scans == c->max_batch) return flush(c);
@@ -997,18 +1050,18 @@ int tsdf_integrate_batch_device(tsdf_ctx* c, const float* d_xyz, const uint64_t*
     while (s < n_scans) {
         BatchDesc D;
         D.n_scans = 0;
-        D.off[0] = 0;
+        D.s[0].off = 0;
         const uint64_t b0 = offs[s];
         while (s < n_scans && D.n_scans < c->max_batch &&
                offs[s + 1] - b0 <= c->batch_points) {
             set_origin(D, D.n_scans, origins + 3 * (uint64_t)s);
-            D.off[D.n_scans + 1] = (uint32_t)(offs[s + 1] - b0);
+            D.s[D.n_scans + 1].off = (uint32_t)(offs[s + 1] - b0);
             D.n_scans++;
             s++;
         }
         rc = launch(c, d_xyz + 3 * b0, D);
         if (rc) return rc;
-        c->n_points_in += D.off[D.n_scans];
+        c->n_points_in += D.s[D.n_scans].off;
     }
     return TSDF_OK;
 }
@@ -1037,11 +1090,12 @@ int tsdf_sync(tsdf_ctx* c) {
         HIPCHK(c, hipMemset(&c->G->overflow, 0, sizeof ovf));
         if (ovf & ERR_MERGE_KEY)
             return fail(c, TSDF_EINVAL, "border merge: a tile's brick is not held by this context");
-        return fail(c, TSDF_ENOMEM, "capacity overflow (%s%s%s%s): updates were dropped",
+        return fail(c, TSDF_ENOMEM, "capacity overflow (%s%s%s%s%s): updates were dropped",
                     (ovf & OVF_TABLE) ? "hash table full; " : "",
                     (ovf & OVF_POOL) ? "brick pool exhausted; " : "",
                     (ovf & OVF_PAIRS) ? "ray brick-pair slots exceeded; " : "",
-                    (ovf & OVF_ACTIVE) ? "active-brick list full" : "");
+                    (ovf & OVF_ACTIVE) ? "active-brick list full; " : "",
+                    (ovf & OVF_SMP) ? "sample list full" : "");
     }
     return TSDF_OK;
 }

@@ -36,7 +36,7 @@ constexpr int BRICK_VOX = 512;
 constexpr int BRICK_COORD_BIAS = 1 << 20;
 constexpr int VOX_LIMIT = 1 << 23;  // |voxel index| < 2^23 on every axis (same as the oracle)
 constexpr int MAX_DDA_STEPS = 1 << 20;
-constexpr int MAX_BATCH = 64;          // scans per batch
+constexpr int MAX_BATCH = 512;         // scans per batch
 #ifndef TSDF_RPB
 #define TSDF_RPB 1024
 #endif
@@ -63,7 +63,8 @@ static_assert(RPB * MAX_IN_BRICK < (1 << PAIR_LID_SHIFT), "local sample offset o
 static_assert(HCAP <= (1 << (PAIR_CNT_SHIFT - PAIR_LID_SHIFT)), "lid overflows");
 
 // overflow bits (sticky until tsdf_sync reads them)
-constexpr uint32_t OVF_TABLE = 1u, OVF_POOL = 2u, OVF_PAIRS = 4u, OVF_ACTIVE = 8u, OVF_FB = 16u;
+constexpr uint32_t OVF_TABLE = 1u, OVF_POOL = 2u, OVF_PAIRS = 4u, OVF_ACTIVE = 8u, OVF_FB = 16u,
+                   OVF_SMP = 32u;  // the batch's samples exceed the sample list
 // a border tile whose brick this context lacks (tsdf_border_merge_device; sticky like OVF_*)
 constexpr uint32_t ERR_MERGE_KEY = 1u << 8;
 
@@ -109,15 +110,27 @@ __host__ __device__ inline bool in_sector(const RayConst& R, float dx, float dy)
     return R.sec_wrap ? (a >= R.sec_lo || a < R.sec_hi) : (a >= R.sec_lo && a < R.sec_hi);
 }
 
-// one batch: scan s = points [off[s], off[s+1]) seen from (ox[s], oy[s], oz[s]) (fp32);
-// k_count / k_place blocks [blk[s], blk[s+1]) cover scan s, RPB rays each
+// One batch: scan s = points [s[s].off, s[s+1].off) seen from s[s].ox/oy/oz (fp32; the origin as
+// given in odx/ody/odz, TSDF_SEM_VDBFUSION_F64); k_count / k_place blocks [s[s].blk, s[s+1].blk)
+// cover scan s, RPB rays each.  The host fills a BatchDesc; launch() uploads its n_scans + 1 used
+// records to a device ring slot, and the kernels get a BatchRef to them (a batch of up to 512
+// scans does not fit the kernel-argument segment).
+struct ScanRec {
+    uint32_t off, blk;
+    float ox, oy, oz;
+    uint32_t pad;
+    double odx, ody, odz;
+};
+static_assert(sizeof(ScanRec) == 48, "ScanRec layout");
 struct BatchDesc {
     uint32_t n_scans;
     uint32_t n_blocks;
-    uint32_t off[MAX_BATCH + 1];
-    uint32_t blk[MAX_BATCH + 1];
-    float ox[MAX_BATCH], oy[MAX_BATCH], oz[MAX_BATCH];
-    double odx[MAX_BATCH], ody[MAX_BATCH], odz[MAX_BATCH];  // the origins as given (TSDF_SEM_VDBFUSION_F64)
+    ScanRec s[MAX_BATCH + 1];
+};
+struct BatchRef {
+    uint32_t n_scans;
+    uint32_t n_blocks;
+    const ScanRec* __restrict__ s;
 };
 
 struct Table {
@@ -148,6 +161,7 @@ struct Work {
     uint4* active_ord;  // the same records, largest size class first (k_order; k_integrate's list)
     uint32_t* ord_hist; // k_order: per (slice, size class) counts, then first positions
     uint4* cagg;    // k_compact: per table chunk (touched bricks, samples, new bricks), then bases
+    uint32_t* act;  // sector sharding: the k_count blocks holding a ray of this GPU's sector (n_act)
     uint32_t maxp;        // pair slots per ray
     uint32_t max_active;  // capacity of `active`
     uint32_t max_fb;      // capacity of `fb`
@@ -161,7 +175,8 @@ struct Counters {
     uint32_t n_fb;
     uint32_t ovf;  // OVF_* raised by this batch's kernels
     uint32_t n_new;  // bricks the batch allocated (k_compact_scan)
-    uint32_t pad1[3];
+    uint32_t n_act;  // sector sharding: k_count blocks with a ray of this GPU's sector (k_sector_flags)
+    uint32_t pad1[2];
     unsigned long long n_vox[8];    // sum over scans of U_vox, sharded by blockIdx & 7
     unsigned long long n_rays[8];   // valid rays
     unsigned long long n_pairs[8];
@@ -206,21 +221,25 @@ struct KernelTimer {
     virtual ~KernelTimer() {}
 };
 
-hipError_t launch_count(const float* d_xyz, const BatchDesc& D, const RayConst& R, const Table& T,
+hipError_t launch_count(const float* d_xyz, const BatchRef& D, const RayConst& R, const Table& T,
                         const Work& Wk, Globals* G, int parity, hipStream_t st);
 // table chunks of k_compact (Work::cagg holds two uint4 per chunk)
 constexpr uint32_t CMP_CHUNK = 1024;
 inline uint64_t compact_chunks(uint64_t cap) { return (cap + CMP_CHUNK - 1) / CMP_CHUNK; }
-hipError_t launch_compact(const BatchDesc& D, const Table& T, const Work& Wk, Globals* G,
+// Sector sharding (n_sectors > 1): which k_count blocks hold a ray of this GPU's sector; the walk
+// kernels' other workgroups leave after one load.
+hipError_t launch_sector_flags(const float* d_xyz, const BatchRef& D, const RayConst& R,
+                               const Work& Wk, Globals* G, int parity, hipStream_t st);
+hipError_t launch_compact(const BatchRef& D, const Table& T, const Work& Wk, Globals* G,
                           int parity, hipStream_t st);
-hipError_t launch_place(const float* d_xyz, const BatchDesc& D, const RayConst& R, const Table& T,
-                        const Work& Wk, hipStream_t st);
+hipError_t launch_place(const float* d_xyz, const BatchRef& D, const RayConst& R, const Table& T,
+                        const Work& Wk, Globals* G, int parity, hipStream_t st);
 hipError_t launch_finish(Globals* G, int parity, uint32_t batch_id, hipStream_t st);
 // capacity growth: re-insert pool slots [0, n) of the new table from brick_keys
 hipError_t launch_rehash(const Table& T, uint32_t n, Globals* G, hipStream_t st);
 // Orders the batch's active bricks by size class, largest first (k_integrate's load balance).
 hipError_t launch_order(const Work& Wk, Globals* G, int parity, hipStream_t st);
-hipError_t launch_integrate(const BatchDesc& D, const RayConst& R, const Table& T, const Work& Wk,
+hipError_t launch_integrate(const BatchRef& D, const RayConst& R, const Table& T, const Work& Wk,
                             const Pool& Pl, Globals* G, int parity, hipStream_t st);
 hipError_t launch_query_dense(const Table& T, const Pool& Pl, const int lo[3], const int dims[3],
                               float bg, float* d_sdf, float* d_w, hipStream_t st);

@@ -69,8 +69,10 @@ constexpr uint32_t INT_MAX_WIN = TSDF_INT_WIN;       // scans per window (mask b
 // is the running average.  Voxblox (1): a cell holds (sum of trunc(s w 2^32), sum of
 // trunc(w 2^32)), w the sample's dropoff weight recomputed from its stored distance, and the fuse
 // clamps the distance to +-tau and the weight to max_weight.
-template <int SEM>
-__global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchDesc D, Table T, Work Wk, Pool Pl,
+// MAXS: the most scans a batch of this instantiation holds (64: the LDS of the single-GPU batches;
+// 512: the sector-sharded multi-GPU batches, one batch per step).
+template <int SEM, int MAXS>
+__global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchRef D, Table T, Work Wk, Pool Pl,
                                                           Globals* G, int parity, RayConst R) {
     typedef typename std::conditional<SEM == 1, unsigned long long, uint32_t>::type CellB;
     __shared__ unsigned long long cA[INT_CAP];  // live cell: sum of trunc(s w * 2^32)
@@ -82,7 +84,8 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchDesc D, Table T,
     __shared__ uint16_t sLive[BRICK_VOX];  // live voxels of the window
     // brick's per-scan sample prefix, double-buffered by brick parity: a wave may still read the
     // previous brick's prefix while another writes the next one
-    __shared__ uint32_t s_csb[2][MAX_BATCH + 1];
+    __shared__ uint32_t s_csb[2][MAXS + 1];
+    static_assert(MAXS <= 2 * INT_THREADS, "two cells per thread");
     __shared__ uint32_t s_red[INT_THREADS / 64];
     __shared__ uint32_t s_nlive, s_ncell;
     float2* cF = reinterpret_cast<float2*>(cA);  // P4: cells converted to (A 2^-32, B) as f32
@@ -107,7 +110,7 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchDesc D, Table T,
     struct BrickRegs {
         uint2 c[INT_PER];
         float s0, s1, w0, w1;
-        uint32_t cell;
+        uint32_t cell, cell2;
     };
     auto load_brick = [&](const uint4& r, BrickRegs& B) {
         const uint32_t n = r.w, base = r.z;
@@ -122,6 +125,9 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchDesc D, Table T,
         // (made relative to the segment where it is consumed: a use here, or a load inside a
         // branch, would make the compiler wait for this prefetch at once)
         B.cell = T.cell[(size_t)r.x * T.cell_stride + min((uint32_t)tid, T.cell_stride - 1u)];
+        if (MAXS > INT_THREADS)
+            B.cell2 = T.cell[(size_t)r.x * T.cell_stride +
+                             min((uint32_t)tid + INT_THREADS, T.cell_stride - 1u)];
         const float* Sg = Pl.sdf + (size_t)(has ? r.y : 0) * BRICK_VOX;
         const float* Wg = Pl.weight + (size_t)(has ? r.y : 0) * BRICK_VOX;
         B.s0 = has ? Sg[tid] : R.bg;
@@ -156,6 +162,7 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchDesc D, Table T,
         };
         const bool has_slot = cur.y < T.max_bricks;
         if ((uint32_t)tid < ns) s_cs[tid] = B.cell - base;
+        if (MAXS > INT_THREADS && (uint32_t)tid + INT_THREADS < ns) s_cs[tid + INT_THREADS] = B.cell2 - base;
         if (tid == 0) s_cs[ns] = n;
         float* Sg = Pl.sdf + (size_t)(has_slot ? cur.y : 0) * BRICK_VOX;
         float* Wg = Pl.weight + (size_t)(has_slot ? cur.y : 0) * BRICK_VOX;
@@ -412,7 +419,7 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchDesc D, Table T,
         }
         ndirty += __popc(dirty);
         // zero every cell of the brick (k_compact prefixes whole uint4 groups) for the next batch
-        if ((uint32_t)tid < T.cell_stride) T.cell[(size_t)h * T.cell_stride + tid] = 0u;
+        for (uint32_t q = tid; q < T.cell_stride; q += INT_THREADS) T.cell[(size_t)h * T.cell_stride + q] = 0u;
 #ifdef TSDF_PHASE_TIMING
         nb++;
 #endif
@@ -443,15 +450,15 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchDesc D, Table T,
 // Grid = exactly the workgroups the device holds at once (CUs x resident workgroups per CU, from
 // the occupancy API: VGPRs or LDS, whichever binds): every workgroup of the grid-stride loop starts
 // at once, none waits for a second dispatch round.
-template <int SEM>
+template <int SEM, int MAXS>
 static int integrate_grid() {
     static int grid = 0;
     if (grid == 0) {
         int dev = 0, cus = 0, per_cu = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_integrate<SEM>, INT_THREADS, 0) !=
-                hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_integrate<SEM, MAXS>,
+                                                         INT_THREADS, 0) != hipSuccess ||
             cus <= 0 || per_cu <= 0) {
             cus = 256;
             per_cu = INT_BLOCKS_PER_CU;
@@ -461,12 +468,24 @@ static int integrate_grid() {
     return grid;
 }
 
-hipError_t launch_integrate(const BatchDesc& D, const RayConst& R, const Table& T, const Work& Wk,
+template <int SEM, int MAXS>
+static void integrate_sem(const BatchRef& D, const RayConst& R, const Table& T, const Work& Wk,
+                          const Pool& Pl, Globals* G, int parity, hipStream_t st) {
+    k_integrate<SEM, MAXS><<<integrate_grid<SEM, MAXS>(), INT_THREADS, 0, st>>>(D, T, Wk, Pl, G,
+                                                                                parity, R);
+}
+
+hipError_t launch_integrate(const BatchRef& D, const RayConst& R, const Table& T, const Work& Wk,
                             const Pool& Pl, Globals* G, int parity, hipStream_t st) {
-    if (R.sem == 1)
-        k_integrate<1><<<integrate_grid<1>(), INT_THREADS, 0, st>>>(D, T, Wk, Pl, G, parity, R);
-    else
-        k_integrate<0><<<integrate_grid<0>(), INT_THREADS, 0, st>>>(D, T, Wk, Pl, G, parity, R);
+    // SEM 2 (VDBFusion at double precision) fuses like SEM 0
+    const bool big = T.cell_stride > 64;
+    if (R.sem == 1) {
+        if (big) integrate_sem<1, MAX_BATCH>(D, R, T, Wk, Pl, G, parity, st);
+        else integrate_sem<1, 64>(D, R, T, Wk, Pl, G, parity, st);
+    } else {
+        if (big) integrate_sem<0, MAX_BATCH>(D, R, T, Wk, Pl, G, parity, st);
+        else integrate_sem<0, 64>(D, R, T, Wk, Pl, G, parity, st);
+    }
     return hipGetLastError();
 }
 

@@ -38,17 +38,17 @@ namespace tsdf {
 // shared helpers of the batch kernels
 
 // Scan and ray range of k_count / k_place workgroup b (uniform: scalar loads of the descriptor).
-__device__ __forceinline__ void block_range(const BatchDesc& D, uint32_t b, uint32_t& t,
+__device__ __forceinline__ void block_range(const BatchRef& D, uint32_t b, uint32_t& t,
                                             uint32_t& r0, uint32_t& r1) {
     uint32_t lo = 0, hi = D.n_scans;  // blk[lo] <= b < blk[hi]
     while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
-        if (D.blk[mid] <= b) lo = mid;
+        if (D.s[mid].blk <= b) lo = mid;
         else hi = mid;
     }
     t = lo;
-    r0 = D.off[t] + (b - D.blk[t]) * RPB;
-    r1 = min(D.off[t + 1], r0 + RPB);
+    r0 = D.s[t].off + (b - D.s[t].blk) * RPB;
+    r1 = min(D.s[t + 1].off, r0 + RPB);
 }
 
 // LDS brick hash of one k_count workgroup: slot index of key (inserted if new), -1 when no slot
@@ -76,7 +76,7 @@ __device__ __forceinline__ int lds_insert(unsigned long long* s_key, uint64_t ke
 constexpr int CNT_THREADS = TSDF_CNT_THREADS;
 
 template <int SEM>
-__global__ __launch_bounds__(CNT_THREADS) void k_count(const float* __restrict__ xyz, BatchDesc D,
+__global__ __launch_bounds__(CNT_THREADS) void k_count(const float* __restrict__ xyz, BatchRef D,
                                                       RayConst R, Table T, Work Wk, Globals* G,
                                                       int parity) {
     __shared__ unsigned long long s_key[HCAP];
@@ -85,14 +85,22 @@ __global__ __launch_bounds__(CNT_THREADS) void k_count(const float* __restrict__
     __shared__ unsigned long long s_wsum[CNT_THREADS / 64];
     __shared__ uint32_t s_wcnt[CNT_THREADS / 64];
     Counters* C = &G->ctr[parity];  // zeroed by the previous batch of this parity (k_finish)
+    // sector sharding: every GPU sees every scan, and a block of 1024 consecutive rays (~3 degrees
+    // of azimuth) usually lies wholly in one sector; the workgroups take the blocks k_sector_flags
+    // listed, the rest of the grid leaves at once
+    uint32_t bx = blockIdx.x;
+    if (R.sec_on) {
+        if (blockIdx.x >= C->n_act) return;
+        bx = Wk.act[blockIdx.x];
+    }
+    uint32_t t, r0, r1;
+    block_range(D, bx, t, r0, r1);
+    const float ox = D.s[t].ox, oy = D.s[t].oy, oz = D.s[t].oz;
     for (int j = threadIdx.x; j < HCAP; j += CNT_THREADS) {
         s_key[j] = EMPTY_KEY;
         s_cnt[j] = 0u;
     }
     __syncthreads();
-    uint32_t t, r0, r1;
-    block_range(D, blockIdx.x, t, r0, r1);
-    const float ox = D.ox[t], oy = D.oy[t], oz = D.oz[t];
     const uint32_t maxp = Wk.maxp;
     uint32_t valid = 0, npairs = 0;
     // The pair code of (ray, brick run): LDS-hash rank in the workgroup's run for the brick, or a
@@ -229,7 +237,7 @@ __global__ __launch_bounds__(CNT_THREADS) void k_count(const float* __restrict__
     // order) and its index in the workgroup's DENSE run list (slot order = sample order).
     constexpr int SPT = HCAP / CNT_THREADS;
     // two dense run lists per workgroup, one per half (k_place workgroup 2 b + half)
-    uint4* bt0 = Wk.blk + (size_t)blockIdx.x * 2 * HCAP;
+    uint4* bt0 = Wk.blk + (size_t)bx * 2 * HCAP;
     uint4* bt1 = bt0 + HCAP;
     uint32_t n0s = 0, n1s = 0, c01 = 0;
 #pragma unroll
@@ -261,8 +269,8 @@ __global__ __launch_bounds__(CNT_THREADS) void k_count(const float* __restrict__
         idx0 = (exc & 0xFFFFu) + ((ic - c01) & 0xFFFFu);
         idx1 = (exc >> 16) + ((ic - c01) >> 16);
         if (threadIdx.x == CNT_THREADS - 1) {
-            Wk.blk_n[2 * blockIdx.x] = totc & 0xFFFFu;
-            Wk.blk_n[2 * blockIdx.x + 1] = totc >> 16;
+            Wk.blk_n[2 * bx] = totc & 0xFFFFu;
+            Wk.blk_n[2 * bx + 1] = totc >> 16;
         }
     }
     // The thread's SPT slots go to the global table in three batched stages, so their round trips
@@ -334,13 +342,41 @@ __global__ __launch_bounds__(CNT_THREADS) void k_count(const float* __restrict__
 }
 
 // ------------------------------------------------------------------------------------------------
+// k_sector_flags (sector sharding only): one wave per k_count block of RPB rays, 16 points per lane,
+// a wave vote; no LDS, so the pass runs at full occupancy and the walk kernels' blocks of other
+// sectors cost one byte load each instead of their point reads and LDS set-up.
+constexpr int FLG_THREADS = 256;
+__global__ __launch_bounds__(FLG_THREADS) void k_sector_flags(const float* __restrict__ xyz,
+                                                             BatchRef D, RayConst R, Work Wk,
+                                                             Globals* G, int parity) {
+    const uint32_t b = blockIdx.x * (FLG_THREADS / 64) + (threadIdx.x >> 6);
+    if (b >= D.n_blocks) return;  // wave-uniform
+    uint32_t t, r0, r1;
+    block_range(D, b, t, r0, r1);
+    const float ox = D.s[t].ox, oy = D.s[t].oy;
+    bool any = false;
+    for (uint32_t i = r0 + (threadIdx.x & 63); i < r1; i += 64)
+        any |= in_sector(R, xyz[3 * (size_t)i] - ox, xyz[3 * (size_t)i + 1] - oy);
+    const bool v = __any(any);
+    // the block joins the walk kernels' list (order is immaterial: blocks are independent)
+    if ((threadIdx.x & 63) == 0 && v) Wk.act[atomicAdd(&G->ctr[parity].n_act, 1u)] = b;
+}
+
+hipError_t launch_sector_flags(const float* d_xyz, const BatchRef& D, const RayConst& R,
+                               const Work& Wk, Globals* G, int parity, hipStream_t st) {
+    const uint32_t per = FLG_THREADS / 64;
+    k_sector_flags<<<(D.n_blocks + per - 1) / per, FLG_THREADS, 0, st>>>(d_xyz, D, R, Wk, G,
+                                                                        parity);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------------
 // k_compact: per active brick — record segment, new pool slot, per-scan cell prefix
 
 constexpr int CMP_THREADS = 256;
 constexpr int CMP_PER = CMP_CHUNK / CMP_THREADS;  // table entries per thread
-constexpr int CMP_GROUP = 16;  // lanes per touched brick: one uint4 of its cell row each (<= 64 scans)
+constexpr int CMP_GROUP = 16;  // lanes per touched brick: one uint4 of its cell row each per 64 scans
 constexpr int CMP_SCAN_THREADS = 1024;
-static_assert(MAX_BATCH <= 4 * CMP_GROUP, "a cell row is at most CMP_GROUP uint4");
 
 template <int NT>
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t* s_w, uint32_t* total) {
@@ -409,8 +445,10 @@ __global__ __launch_bounds__(CMP_THREADS) void k_compact_sum(uint32_t n_scans, T
     for (uint32_t k = grp; k < nh; k += CMP_THREADS / CMP_GROUP) {
         const uint32_t h = s_h[k];
         const uint4* cp = reinterpret_cast<const uint4*>(T.cell + (size_t)h * T.cell_stride);
-        const uint4 v = li < nq ? cp[li] : make_uint4(0u, 0u, 0u, 0u);
-        samples += v.x + v.y + v.z + v.w;
+        for (uint32_t q = li; q < nq; q += CMP_GROUP) {  // 64 scans per pass
+            const uint4 v = cp[q];
+            samples += v.x + v.y + v.z + v.w;
+        }
         if (li == 0 && T.slots[h] == UNASSIGNED) nnew++;
     }
     samples = wave_sum<uint32_t>(samples);
@@ -455,7 +493,7 @@ __global__ __launch_bounds__(CMP_SCAN_THREADS) void k_compact_scan(uint32_t nch,
         C->cursor = s_carry[1];
         C->n_new = s_carry[2] - G->pool_count;
         G->pool_count = s_carry[2];
-        if (s_carry[1] > Wk.max_smp) atomicOr(&C->ovf, OVF_PAIRS);
+        if (s_carry[1] > Wk.max_smp) atomicOr(&C->ovf, OVF_SMP);
         if (s_carry[0] > Wk.max_active) atomicOr(&C->ovf, OVF_ACTIVE);
     }
 }
@@ -473,8 +511,11 @@ __global__ __launch_bounds__(CMP_THREADS) void k_compact_write(uint32_t n_scans,
     const uint32_t grp = threadIdx.x / CMP_GROUP, li = threadIdx.x % CMP_GROUP;
     for (uint32_t k = grp; k < nh; k += CMP_THREADS / CMP_GROUP) {
         const uint4* cp = reinterpret_cast<const uint4*>(T.cell + (size_t)s_h[k] * T.cell_stride);
-        const uint4 v = li < nq ? cp[li] : make_uint4(0u, 0u, 0u, 0u);
-        uint32_t sum = v.x + v.y + v.z + v.w;
+        uint32_t sum = 0;
+        for (uint32_t q = li; q < nq; q += CMP_GROUP) {
+            const uint4 v = cp[q];
+            sum += v.x + v.y + v.z + v.w;
+        }
 #pragma unroll
         for (int d = CMP_GROUP / 2; d >= 1; d >>= 1) sum += __shfl_xor(sum, d, CMP_GROUP);
         if (li == 0) s_n[k] = sum;
@@ -522,17 +563,22 @@ __global__ __launch_bounds__(CMP_THREADS) void k_compact_write(uint32_t n_scans,
     // (k_place then finds a run's position with one gather)
     for (uint32_t k = grp; k < nh; k += CMP_THREADS / CMP_GROUP) {
         uint4* cp = reinterpret_cast<uint4*>(T.cell + (size_t)s_h[k] * T.cell_stride);
-        uint4 v = li < nq ? cp[li] : make_uint4(0u, 0u, 0u, 0u);
-        const uint32_t s4 = v.x + v.y + v.z + v.w;
-        static_assert(CMP_GROUP == 16, "a cell row is one 16-lane DPP row");
-        const uint32_t incl = row16_incl_scan(s4);
-        uint32_t p = s_n[k] + incl - s4;
-        const uint32_t x0 = v.x, x1 = v.y, x2 = v.z;
-        v.x = p; p += x0;
-        v.y = p; p += x1;
-        v.z = p; p += x2;
-        v.w = p;
-        if (li < nq) cp[li] = v;
+        uint32_t carry = s_n[k];
+        for (uint32_t q0 = 0; q0 < nq; q0 += CMP_GROUP) {  // 64 scans per pass, carried
+            const uint32_t q = q0 + li;
+            uint4 v = q < nq ? cp[q] : make_uint4(0u, 0u, 0u, 0u);
+            const uint32_t s4 = v.x + v.y + v.z + v.w;
+            static_assert(CMP_GROUP == 16, "a cell row pass is one 16-lane DPP row");
+            const uint32_t incl = row16_incl_scan(s4);
+            uint32_t p = carry + incl - s4;
+            const uint32_t x0 = v.x, x1 = v.y, x2 = v.z;
+            v.x = p; p += x0;
+            v.y = p; p += x1;
+            v.z = p; p += x2;
+            v.w = p;
+            if (q < nq) cp[q] = v;
+            carry += __shfl(incl, CMP_GROUP - 1, CMP_GROUP);  // the pass's row total
+        }
     }
 }
 
@@ -555,8 +601,9 @@ constexpr int PLC_THREADS = RPB / 2;  // one ray per lane, half a k_count workgr
 constexpr int PLC_STAGE = TSDF_PLC_STAGE;  // staged samples per workgroup (6 B each; 4 workgroups per CU)
 
 template <int SEM>
-__global__ __launch_bounds__(PLC_THREADS) void k_place(const float* __restrict__ xyz, BatchDesc D,
-                                                      RayConst R, Table T, Work Wk) {
+__global__ __launch_bounds__(PLC_THREADS) void k_place(const float* __restrict__ xyz, BatchRef D,
+                                                      RayConst R, Table T, Work Wk,
+                                                      const Globals* __restrict__ G, int parity) {
     constexpr int PLC_WORDS = (PLC_STAGE + 31) / 32;
     __shared__ uint32_t s_base[HCAP];      // run -> first sample of the run in the brick segment
     __shared__ uint16_t s_loff[HCAP];      // run -> offset in the workgroup's sample order
@@ -570,11 +617,17 @@ __global__ __launch_bounds__(PLC_THREADS) void k_place(const float* __restrict__
     unsigned long long pt[6];
     if (threadIdx.x == 0) pt[0] = clock64();
 #endif
-    // workgroup 2 b + hf takes half hf of k_count workgroup b's rays, and that half's run list
+    // workgroup 2 b + hf takes half hf of k_count block b's rays, and that half's run list
+    // (sector sharding: block b is the (w / 2)-th of k_sector_flags' list, the rest leave)
+    uint32_t wb = blockIdx.x;
+    if (R.sec_on) {
+        if ((blockIdx.x >> 1) >= G->ctr[parity].n_act) return;
+        wb = 2 * Wk.act[blockIdx.x >> 1] + (blockIdx.x & 1u);
+    }
     uint32_t t, r0, r1;
-    block_range(D, blockIdx.x >> 1, t, r0, r1);
-    r0 += (blockIdx.x & 1u) * PLC_THREADS;
-    const uint4* bt = Wk.blk + (size_t)blockIdx.x * HCAP;
+    block_range(D, wb >> 1, t, r0, r1);
+    r0 += (wb & 1u) * PLC_THREADS;
+    const uint4* bt = Wk.blk + (size_t)wb * HCAP;
     const uint32_t maxp = Wk.maxp;
     const uint32_t i = r0 + threadIdx.x;
     // Every independent global load is issued first, so the prologue waits two memory round trips
@@ -589,7 +642,7 @@ __global__ __launch_bounds__(PLC_THREADS) void k_place(const float* __restrict__
         pz = xyz[3 * (size_t)i + 2];
         if (maxp == 4) code4 = *reinterpret_cast<const uint4*>(pc);
     }
-    const uint32_t nruns = Wk.blk_n[blockIdx.x];
+    const uint32_t nruns = Wk.blk_n[wb];
     static_assert(PLC_THREADS <= HCAP, "a lane's first list entry lies inside the list");
     const uint4 e0 = bt[threadIdx.x];
     // a run's absolute sample position is its (brick, scan) cell (absolute after k_compact) + its
@@ -597,9 +650,11 @@ __global__ __launch_bounds__(PLC_THREADS) void k_place(const float* __restrict__
     const uint32_t base0 = (threadIdx.x < nruns && e0.x != NO_PAIR)
                                ? T.cell[(size_t)e0.x * T.cell_stride + t] + e0.y
                                : NO_PAIR;
-    const float ox = D.ox[t], oy = D.oy[t], oz = D.oz[t];
+    const float ox = D.s[t].ox, oy = D.s[t].oy, oz = D.s[t].oz;
     typename Walk<SEM>::State r;
     const bool ok = i < r1 && Walk<SEM>::init(R, D, t, px, py, pz, r);
+    // sector sharding: a half block without a ray of this GPU's sector has no samples to place
+    if (R.sec_on && !__syncthreads_or(ok)) return;
     for (int j = threadIdx.x; j < PLC_WORDS; j += PLC_THREADS) s_bits[j] = 0u;
     if (threadIdx.x == 0) s_nst = 0u;
     __syncthreads();
@@ -895,7 +950,7 @@ static int grid_for(uint64_t items, int per_block, int cap) {
 
 // One batch is k_count -> k_compact -> k_place -> k_integrate -> k_finish on one stream; the host
 // (tsdf_capi.cpp) interleaves the cross-batch waits between them.
-hipError_t launch_count(const float* d_xyz, const BatchDesc& D, const RayConst& R, const Table& T,
+hipError_t launch_count(const float* d_xyz, const BatchRef& D, const RayConst& R, const Table& T,
                         const Work& Wk, Globals* G, int parity, hipStream_t st) {
     if (R.sem == 1) k_count<1><<<D.n_blocks, CNT_THREADS, 0, st>>>(d_xyz, D, R, T, Wk, G, parity);
     else if (R.sem == 2) k_count<2><<<D.n_blocks, CNT_THREADS, 0, st>>>(d_xyz, D, R, T, Wk, G, parity);
@@ -903,7 +958,7 @@ hipError_t launch_count(const float* d_xyz, const BatchDesc& D, const RayConst& 
     return hipGetLastError();
 }
 
-hipError_t launch_compact(const BatchDesc& D, const Table& T, const Work& Wk, Globals* G,
+hipError_t launch_compact(const BatchRef& D, const Table& T, const Work& Wk, Globals* G,
                           int parity, hipStream_t st) {
     const uint32_t nch = (uint32_t)compact_chunks(T.mask + 1);
     k_compact_sum<<<nch, CMP_THREADS, 0, st>>>(D.n_scans, T, Wk);
@@ -912,11 +967,11 @@ hipError_t launch_compact(const BatchDesc& D, const Table& T, const Work& Wk, Gl
     return hipGetLastError();
 }
 
-hipError_t launch_place(const float* d_xyz, const BatchDesc& D, const RayConst& R, const Table& T,
-                        const Work& Wk, hipStream_t st) {
-    if (R.sem == 1) k_place<1><<<2 * D.n_blocks, PLC_THREADS, 0, st>>>(d_xyz, D, R, T, Wk);
-    else if (R.sem == 2) k_place<2><<<2 * D.n_blocks, PLC_THREADS, 0, st>>>(d_xyz, D, R, T, Wk);
-    else k_place<0><<<2 * D.n_blocks, PLC_THREADS, 0, st>>>(d_xyz, D, R, T, Wk);
+hipError_t launch_place(const float* d_xyz, const BatchRef& D, const RayConst& R, const Table& T,
+                        const Work& Wk, Globals* G, int parity, hipStream_t st) {
+    if (R.sem == 1) k_place<1><<<2 * D.n_blocks, PLC_THREADS, 0, st>>>(d_xyz, D, R, T, Wk, G, parity);
+    else if (R.sem == 2) k_place<2><<<2 * D.n_blocks, PLC_THREADS, 0, st>>>(d_xyz, D, R, T, Wk, G, parity);
+    else k_place<0><<<2 * D.n_blocks, PLC_THREADS, 0, st>>>(d_xyz, D, R, T, Wk, G, parity);
     return hipGetLastError();
 }
 

@@ -273,9 +273,9 @@ struct Walk;
 template <>
 struct Walk<0> {  // TSDF_SEM_VDBFUSION
     typedef RayState State;
-    __device__ static __forceinline__ bool init(const RayConst& R, const BatchDesc& D, uint32_t t,
+    __device__ static __forceinline__ bool init(const RayConst& R, const BatchRef& D, uint32_t t,
                                                 float px, float py, float pz, State& r) {
-        return ray_init(R, D.ox[t], D.oy[t], D.oz[t], px, py, pz, r);
+        return ray_init(R, D.s[t].ox, D.s[t].oy, D.s[t].oz, px, py, pz, r);
     }
     __device__ static __forceinline__ bool gate(const RayConst& R, float ox, float oy, float oz,
                                                 const State& r, bool check = true) {
@@ -301,9 +301,9 @@ struct Walk<0> {  // TSDF_SEM_VDBFUSION
 template <>
 struct Walk<1> {  // TSDF_SEM_VOXBLOX
     typedef VbState State;
-    __device__ static __forceinline__ bool init(const RayConst& R, const BatchDesc& D, uint32_t t,
+    __device__ static __forceinline__ bool init(const RayConst& R, const BatchRef& D, uint32_t t,
                                                 float px, float py, float pz, State& r) {
-        return vb_init(R, D.ox[t], D.oy[t], D.oz[t], px, py, pz, r);
+        return vb_init(R, D.s[t].ox, D.s[t].oy, D.s[t].oz, px, py, pz, r);
     }
     __device__ static __forceinline__ bool gate(const RayConst& R, float ox, float oy, float oz,
                                                 const State& r, bool check = true) {
@@ -355,12 +355,12 @@ __device__ __forceinline__ void vdb_axis(float di, float inv, float pos, float t
     }
 }
 
-__device__ __forceinline__ bool vdb_init(const RayConst& R, const BatchDesc& D, uint32_t t,
+__device__ __forceinline__ bool vdb_init(const RayConst& R, const BatchRef& D, uint32_t t,
                                          float px, float py, float pz, VdbState& r) {
-    if (!in_sector(R, px - D.ox[t], py - D.oy[t])) return false;  // another GPU's azimuth sector
-    r.oxd = D.odx[t];
-    r.oyd = D.ody[t];
-    r.ozd = D.odz[t];
+    if (!in_sector(R, px - D.s[t].ox, py - D.s[t].oy)) return false;  // another GPU's azimuth sector
+    r.oxd = D.s[t].odx;
+    r.oyd = D.s[t].ody;
+    r.ozd = D.s[t].odz;
     r.pxd = px;
     r.pyd = py;
     r.pzd = pz;
@@ -372,9 +372,9 @@ __device__ __forceinline__ bool vdb_init(const RayConst& R, const BatchDesc& D, 
     const float t0 = R.carving ? 0.0f : depth - R.tau;
     const float t1 = depth + R.tau;
     // Ray<float>(eye, dir, t0, t1).worldToIndex(grid)
-    const float ex = (float)((double)D.ox[t] * R.inv_s_d);
-    const float ey = (float)((double)D.oy[t] * R.inv_s_d);
-    const float ez = (float)((double)D.oz[t] * R.inv_s_d);
+    const float ex = (float)((double)D.s[t].ox * R.inv_s_d);
+    const float ey = (float)((double)D.s[t].oy * R.inv_s_d);
+    const float ez = (float)((double)D.s[t].oz * R.inv_s_d);
     const float jx = (float)((double)(float)(dx * il) * R.inv_s_d);
     const float jy = (float)((double)(float)(dy * il) * R.inv_s_d);
     const float jz = (float)((double)(float)(dz * il) * R.inv_s_d);
@@ -416,7 +416,7 @@ __device__ __forceinline__ bool vdb_inside(const VdbState& r) {
 template <>
 struct Walk<2> {  // TSDF_SEM_VDBFUSION_F64
     typedef VdbState State;
-    __device__ static __forceinline__ bool init(const RayConst& R, const BatchDesc& D, uint32_t t,
+    __device__ static __forceinline__ bool init(const RayConst& R, const BatchRef& D, uint32_t t,
                                                 float px, float py, float pz, State& r) {
         return vdb_init(R, D, t, px, py, pz, r);
     }

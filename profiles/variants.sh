@@ -3,6 +3,7 @@
 # the real build; one JSON line per variant into $OUT/<name>.json.
 OUT=${1:-gpurun_out/var}
 mkdir -p "$OUT"
+shopt -s nullglob
 for lib in "" noetic-slam_amd/lib/var/*.so; do
   n=real; [ -n "$lib" ] && n=$(basename "$lib" .so | sed 's/^libtsdf_hip_//')
   TSDF_HIP_LIB=$lib timeout -k 10 200 python3 bench.py --steps ${STEPS:-16} --warmup 2 --no-cpu > "$OUT/$n.json" 2> "$OUT/$n.err" || { echo "$n failed"; tail -3 "$OUT/$n.err"; exit 1; }

@@ -103,3 +103,48 @@ def test_import_grows(scan0):
     b.import_bricks(*a.export_bricks())
     for x, y in zip(a.export_bricks(), b.export_bricks()):
         assert np.array_equal(x, y)
+
+
+def test_large_batches_bitwise(sim):
+    """Batches of up to 512 scans (the sector-sharded multi-GPU step is one batch): a 130-scan
+    device batch is one launch, bit-exact to the oracle."""
+    import torch
+    scans = [(decimate(p, 16), o) for p, o in (sim.scan(k) for k in range(130))]
+    allp = np.concatenate([p for p, _ in scans])
+    offs = np.cumsum([0] + [p.shape[0] for p, _ in scans]).astype(np.uint64)
+    org = np.stack([o for _, o in scans])
+    d = torch.from_numpy(allp).to("cuda:0")
+    torch.cuda.synchronize()
+    g = hip(max_batch=512)
+    g.integrate_batch_device(d.data_ptr(), offs, org)
+    g.sync()
+    assert g.stats()["n_batches"] == 1
+    o = ora()
+    for p, q in scans:
+        o.integrate(p, q)
+    assert bitwise(g, o)
+
+
+def test_sector_sample_list_grows(sim):
+    """A sharded context sizes its sample list for 1 / n_sectors of the rays; scans whose points
+    all lie in its sector overflow it, and it grows (OVF_SMP) without losing an update."""
+    import torch
+    from tsdf_map import sector_ids
+    scans = []
+    for k in range(6):
+        p, o = sim.scan(k)
+        p = p[sector_ids(p, o, 8, 0.0) == 0]
+        scans.append((np.ascontiguousarray(p), o))
+    allp = np.concatenate([p for p, _ in scans])
+    offs = np.cumsum([0] + [p.shape[0] for p, _ in scans]).astype(np.uint64)
+    org = np.stack([o for _, o in scans])
+    d = torch.from_numpy(allp).to("cuda:0")
+    torch.cuda.synchronize()
+    g = hip(max_batch=8, n_sectors=8, sector=0, max_points=1 << 15)  # 819 k sample slots
+    g.integrate_batch_device(d.data_ptr(), offs, org)
+    g.sync()
+    assert g.stats()["n_grows"] >= 1
+    o = ora(n_sectors=8, sector=0)
+    for p, q in scans:
+        o.integrate(p, q)
+    assert bitwise(g, o)
