@@ -7,10 +7,16 @@ import oracle
 from conftest import GOLDEN
 
 
-def test_oracle_reproduces_golden():
+def _make_golden():
     import sys
-    sys.path.insert(0, GOLDEN)
-    from make_golden import digest
+    if GOLDEN not in sys.path:
+        sys.path.insert(0, GOLDEN)
+    import make_golden
+    return make_golden
+
+
+def test_oracle_reproduces_golden():
+    digest = _make_golden().digest
     z = np.load(os.path.join(GOLDEN, "golden_c1_decimated.npz"), allow_pickle=False)
     v = oracle.OracleTSDFVolume(float(z["voxel_size"]), float(z["sdf_trunc"]))
     offs = z["scan_offsets"]
@@ -26,7 +32,7 @@ def test_oracle_reproduces_golden():
 
 def test_golden_inputs_follow_the_generator():
     """The stored inputs are the generator's (regression of the Ouster LUT / scene code)."""
-    import make_golden
+    make_golden = _make_golden()
     from tsdf_map.scan_gen import OusterSim
     z = np.load(os.path.join(GOLDEN, "golden_c1_decimated.npz"), allow_pickle=False)
     p, o = OusterSim().scan(make_golden.SCANS[0])
