@@ -62,6 +62,9 @@ def parse():
                          "scans per step): its time per step is one rank's; value = N x batch "
                          "scans / step time, the N-GPU throughput if every rank took as long "
                          "(rehearsal of the scaling runs on a one-GPU box)")
+    ap.add_argument("--walk", default="two", choices=("two", "single"),
+                    help="front end (tsdf_params.walk): two = k_count + k_place (default); single = "
+                         "every ray walked once (k_walk + k_spans) when the band allows it")
     ap.add_argument("--no-profile", action="store_true",
                     help="do not record per-kernel HIP events in the timed region")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_r01.json"),
@@ -123,7 +126,8 @@ def main():
                         max_bricks=args.max_bricks, device_id=local,
                         max_batch=min(scans_per_step, 512),  # one launch per step (all shards)
                         pipeline=args.pipeline, semantics=args.semantics,
-                        n_sectors=n_shards, sector=rank)  # this rank's azimuth sector of every scan
+                        n_sectors=n_shards, sector=rank,  # this rank's azimuth sector of every scan
+                        walk=args.walk)
 
     def run_step(i):
         x, offs, org = steps[i]
@@ -173,7 +177,9 @@ def main():
     dedup_bytes_per_launch = (12.0 * st["n_rays_total"] + 16.0 * st["n_dirty_total"]) / n_batches
     kms = st["kernel_ms"]
     roofline = None
-    kernel_ms_per_launch = {k: (kms[k] / max(1, st["kernel_launches"][k])) for k in kms}
+    kernel_ms_per_launch = {k: (kms[k] / st["kernel_launches"][k]) for k in kms
+                            if st["kernel_launches"][k] > 0}
+    kms = {k: kms[k] for k in kernel_ms_per_launch}
     if not args.no_profile and sum(kms.values()) > 0:
         dom = max(kms, key=lambda k: kms[k])
         t_launch = kernel_ms_per_launch[dom] * 1e-3
@@ -192,6 +198,10 @@ def main():
                     "dedup_bytes_per_launch": round(dedup_bytes_per_launch),
                     "scans_per_launch": round(scans_per_launch, 2),
                     "avg_launch_ms": round(kernel_ms_per_launch[dom], 5)}
+        # the whole path: the same algorithmic bytes over the sum of the batch's kernel times
+        path_ms = sum(kernel_ms_per_launch.values())
+        roofline["path_achieved"] = round(bytes_per_launch / (path_ms * 1e-3) / 1e9, 2)
+        roofline["path_frac"] = round(bytes_per_launch / (path_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 5)
     path_ms_per_scan = sum(kernel_ms_per_launch.values()) * n_batches / n_scans_rank
 
     # ---- read-out merge of border bricks (not in the timed region) ----------------------------
@@ -271,7 +281,9 @@ def main():
                        "parallelism": ("azimuth-sector x%d" % world if world > 1 else
                                        "rank-0 rehearsal of azimuth-sector x%d" % n_shards
                                        if n_shards > 1 else "single"),
-                       "sector_split": "in-kernel (timed)" if n_shards > 1 else None},
+                       "sector_split": "in-kernel (timed)" if n_shards > 1 else None,
+                       "front_end": ("single walk (k_walk + k_spans)" if "walk" in kernel_ms_per_launch
+                                     else "two walks (k_count + k_place)")},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "path_ms_per_scan": round(path_ms_per_scan, 5),

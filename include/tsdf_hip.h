@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define TSDF_ABI_VERSION 4
+#define TSDF_ABI_VERSION 5
 #define TSDF_MAX_BATCH 512 /* scans per GPU batch (see tsdf_params.max_batch) */
 #define TSDF_BRICK_SIDE 8 /* voxels per brick edge: a brick is 8^3 = 512 voxels */
 
@@ -106,7 +106,18 @@ typedef struct tsdf_params {
      * capacity: an overflow then drops the updates that do not fit and tsdf_sync reports
      * TSDF_ENOMEM. */
     uint64_t max_bricks_hard;
+    /* ABI v5: front end of the batch pipeline.  TSDF_WALK_TWO (default): every ray
+     * is walked twice (k_count counts, k_place writes each brick's samples contiguously).
+     * TSDF_WALK_SINGLE: every ray is walked ONCE (k_walk keeps its samples in registers, stages
+     * them per workgroup and writes them linearly; k_spans lists each brick's samples as spans)
+     * whenever the band's walk has a proven bound of at most 32 voxels and 4 bricks per ray (no
+     * space carving, no Voxblox clearing rays), else twice.  The field is bit for bit the same
+     * either way; the single walk measures slower on MI355X. */
+    int32_t walk;
 } tsdf_params;
+
+#define TSDF_WALK_TWO 0
+#define TSDF_WALK_SINGLE 1
 
 /* Batching.  Scans are integrated in call order and the field after any sequence of calls is
  * bitwise the one scan-at-a-time integration gives; the GPU merely processes up to max_batch
@@ -139,6 +150,8 @@ typedef struct tsdf_stats {
 #define TSDF_K_COMPACT 1   /* k_compact: per-brick sample segments, pool slots, per-scan prefix */
 #define TSDF_K_PLACE 2     /* k_place: second walk, samples staged in LDS, written per brick run */
 #define TSDF_K_INTEGRATE 3 /* k_integrate: per-brick live-cell accumulate + scan-ordered fuse */
+#define TSDF_K_WALK 4      /* k_walk: the single walk (samples staged per workgroup, linear write) */
+#define TSDF_K_SPANS 5     /* k_spans: per-brick span lists of the single walk's samples */
 
 typedef struct tsdf_ctx tsdf_ctx;
 

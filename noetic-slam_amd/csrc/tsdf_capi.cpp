@@ -149,6 +149,10 @@ struct tsdf_ctx {
     uint64_t batch_points = 0;  // pair-slot capacity / maxp: points one batch may hold
     uint32_t max_blocks = 0;    // k_count / k_place workgroups one batch may need
     uint64_t slots = 0;         // pair slots of one batch
+    // single walk: k_walk + k_spans instead of k_count + k_place, when asked for
+    // (tsdf_params.walk) and the band's walk fits nstep register slots per ray
+    bool fused = false;
+    int nstep = 0;
     // host-pointer path: pinned double buffer per scan; the pending batch's points are staged in
     // stage2[batch parity]
     float* h_stage[2] = {nullptr, nullptr};
@@ -160,7 +164,7 @@ struct tsdf_ctx {
     // (the table's `touched` words), k_integrate(b+1) after k_finish(b) (per-brick fuse order).
     hipStream_t bst[2] = {nullptr, nullptr};
     Work W2[2]{};
-    uint32_t* cell2[2] = {nullptr, nullptr};
+    uint32_t* cell2[2] = {nullptr, nullptr};  // u64 cells with the single walk
     float* stage2[2] = {nullptr, nullptr};
     hipEvent_t ev_main = nullptr;
     hipEvent_t ev_compact[2] = {nullptr, nullptr}, ev_integ[2] = {nullptr, nullptr};
@@ -289,13 +293,16 @@ static int launch(tsdf_ctx* c, const float* d_xyz, BatchDesc& D) {
     HIPCHK(c, hipMemcpyAsync(ds, hs, (D.n_scans + 1) * sizeof(ScanRec), hipMemcpyHostToDevice, st));
     HIPCHK(c, hipEventRecord(c->ring_ev[slot], st));
     const BatchRef B{D.n_scans, D.n_blocks, ds};
+    const int k_front = c->fused ? KIND_WALK : KIND_COUNT;
+    const int k_back = c->fused ? KIND_SPANS : KIND_PLACE;
     if (D.n_blocks) {
-        if (tm) tm->begin(KIND_COUNT, st);
+        if (tm) tm->begin(k_front, st);
         if (c->R.sec_on) HIPCHK(c, launch_sector_flags(d_xyz, B, c->R, W, c->G, par, st));
-        HIPCHK(c, launch_count(d_xyz, B, c->R, T, W, c->G, par, st));
-        if (tm) tm->end(KIND_COUNT, st);
+        if (c->fused) HIPCHK(c, launch_walk(d_xyz, B, c->R, T, W, c->G, par, c->nstep, st));
+        else HIPCHK(c, launch_count(d_xyz, B, c->R, T, W, c->G, par, st));
+        if (tm) tm->end(k_front, st);
         if (tm) tm->begin(KIND_COMPACT, st);
-        HIPCHK(c, launch_compact(B, T, W, c->G, par, st));
+        HIPCHK(c, launch_compact(B, T, W, c->G, par, c->fused, st));
 #ifndef TSDF_NO_ORDER
         HIPCHK(c, launch_order(W, c->G, par, st));
 #endif
@@ -303,9 +310,10 @@ static int launch(tsdf_ctx* c, const float* d_xyz, BatchDesc& D) {
     }
     HIPCHK(c, hipEventRecord(c->ev_compact[par], st));
     if (D.n_blocks) {
-        if (tm) tm->begin(KIND_PLACE, st);
-        HIPCHK(c, launch_place(d_xyz, B, c->R, T, W, c->G, par, st));
-        if (tm) tm->end(KIND_PLACE, st);
+        if (tm) tm->begin(k_back, st);
+        if (c->fused) HIPCHK(c, launch_spans(B, c->R, T, W, c->G, par, c->nstep, st));
+        else HIPCHK(c, launch_place(d_xyz, B, c->R, T, W, c->G, par, st));
+        if (tm) tm->end(k_back, st);
     }
     if (c->batch_id > 0 && cross) HIPCHK(c, hipStreamWaitEvent(st, c->ev_integ[par ^ 1], 0));
     if (D.n_blocks) {
@@ -313,9 +321,9 @@ static int launch(tsdf_ctx* c, const float* d_xyz, BatchDesc& D) {
 #ifndef TSDF_NO_ORDER
         Work Wi = W;
         Wi.active = W.active_ord;  // largest bricks first (k_order)
-        HIPCHK(c, launch_integrate(B, c->R, T, Wi, c->Pl, c->G, par, st));
+        HIPCHK(c, launch_integrate(B, c->R, T, Wi, c->Pl, c->G, par, c->fused, c->max_batch > 64, st));
 #else
-        HIPCHK(c, launch_integrate(B, c->R, T, W, c->Pl, c->G, par, st));
+        HIPCHK(c, launch_integrate(B, c->R, T, W, c->Pl, c->G, par, c->fused, c->max_batch > 64, st));
 #endif
         if (tm) tm->end(KIND_INTEGRATE, st);
     }
@@ -387,7 +395,7 @@ static int alloc_capacity(tsdf_ctx* c, uint64_t max_bricks, Capacity& K) {
     K.max_bricks = max_bricks;
     K.cap = next_pow2(2 * max_bricks);
     K.max_active = (uint32_t)std::min<uint64_t>(K.cap, c->slots);
-    const size_t cells = K.cap * c->T.cell_stride * sizeof(uint32_t);
+    const size_t cells = K.cap * c->T.cell_stride * (c->fused ? sizeof(uint64_t) : sizeof(uint32_t));
     hipError_t e = hipMalloc(&K.keys, K.cap * sizeof(uint64_t));
     if (e == hipSuccess) e = hipMalloc(&K.slots, K.cap * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc(&K.touched, K.cap * sizeof(uint32_t));
@@ -527,9 +535,11 @@ static int drain_all(tsdf_ctx* c) {
 // batches from it (their inputs are still valid), until a round succeeds.  Without growth (hard
 // limit, or a non-growable overflow) the batches are re-run committing what fits, and tsdf_sync
 // reports the overflow.
-// Double both parities' sample lists (OVF_SMP), up to the 32-bit sample index.
+// Double both parities' sample lists (OVF_SMP), up to the 32-bit sample index (single walk: the
+// workgroup regions, up to the span record's 30-bit sample position).
+static uint64_t smp_limit(const tsdf_ctx* c) { return c->fused ? (1ull << 30) : 0xFFFFFFF0ull; }
 static int grow_smp(tsdf_ctx* c) {
-    const uint64_t ns = std::min<uint64_t>(2ull * c->Wk.max_smp, 0xFFFFFFF0ull);
+    const uint64_t ns = std::min<uint64_t>(2ull * c->Wk.max_smp, smp_limit(c));
     if (ns <= c->Wk.max_smp) return fail(c, TSDF_ENOMEM, "sample list at its limit");
     uint2* f[2] = {nullptr, nullptr};
     hipError_t e = hipMalloc(&f[0], ns * sizeof(uint2));
@@ -545,6 +555,28 @@ static int grow_smp(tsdf_ctx* c) {
         c->W2[q].max_smp = (uint32_t)ns;
     }
     c->Wk.max_smp = (uint32_t)ns;
+    c->n_grows++;
+    return TSDF_OK;
+}
+
+// Double both parities' span lists (OVF_SPN, single walk).
+static int grow_spn(tsdf_ctx* c) {
+    const uint64_t ns = std::min<uint64_t>(2ull * c->Wk.max_spn, 0xFFFFFFF0ull);
+    if (ns <= c->Wk.max_spn) return fail(c, TSDF_ENOMEM, "span list at its limit");
+    uint32_t* f[2] = {nullptr, nullptr};
+    hipError_t e = hipMalloc(&f[0], ns * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc(&f[1], ns * sizeof(uint32_t));
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        for (auto q : f) if (q) (void)hipFree(q);
+        return fail(c, TSDF_ENOMEM, "span list allocation failed");
+    }
+    for (int q = 0; q < 2; q++) {
+        (void)hipFree(c->W2[q].spn);
+        c->W2[q].spn = f[q];
+        c->W2[q].max_spn = (uint32_t)ns;
+    }
+    c->Wk.max_spn = (uint32_t)ns;
     c->n_grows++;
     return TSDF_OK;
 }
@@ -570,6 +602,7 @@ static int check_and_replay(tsdf_ctx* c) {
                 rc = grow_capacity(c, std::max<uint64_t>(g.pool_count, c->T.max_bricks + 1));
             if (rc == TSDF_OK && (g.overflow & OVF_FB)) rc = grow_fb(c);
             if (rc == TSDF_OK && (g.overflow & OVF_SMP)) rc = grow_smp(c);
+            if (rc == TSDF_OK && (g.overflow & OVF_SPN)) rc = grow_spn(c);
             if (rc == TSDF_EHIP) return rc;
         }
         // the replay: from the first failed batch on, in order
@@ -639,11 +672,19 @@ static int emit_metrics(tsdf_ctx* c) {
             if (ti < bm.size() && bm[ti].first == b) ms = &bm[ti].second;
         }
         if (ms) {
-            const double path = (*ms)[0] + (*ms)[1] + (*ms)[2] + (*ms)[3];
-            fprintf(c->metrics,
-                    ", \"kernel_ms\": {\"count\": %.5f, \"compact\": %.5f, \"place\": %.5f, "
-                    "\"integrate\": %.5f}, \"path_ms\": %.5f, \"gbs\": %.2f",
-                    (*ms)[0], (*ms)[1], (*ms)[2], (*ms)[3], path,
+            double path = 0;
+            for (int k = 0; k < KIND_N; k++) path += (*ms)[k];
+            if (c->fused)
+                fprintf(c->metrics,
+                        ", \"kernel_ms\": {\"walk\": %.5f, \"compact\": %.5f, \"spans\": %.5f, "
+                        "\"integrate\": %.5f}",
+                        (*ms)[KIND_WALK], (*ms)[KIND_COMPACT], (*ms)[KIND_SPANS], (*ms)[KIND_INTEGRATE]);
+            else
+                fprintf(c->metrics,
+                        ", \"kernel_ms\": {\"count\": %.5f, \"compact\": %.5f, \"place\": %.5f, "
+                        "\"integrate\": %.5f}",
+                        (*ms)[KIND_COUNT], (*ms)[KIND_COMPACT], (*ms)[KIND_PLACE], (*ms)[KIND_INTEGRATE]);
+            fprintf(c->metrics, ", \"path_ms\": %.5f, \"gbs\": %.2f", path,
                     path > 0 ? bytes / (path * 1e-3) / 1e9 : 0.0);
         }
         fprintf(c->metrics, "}\n");
@@ -786,7 +827,8 @@ void tsdf_destroy(tsdf_ctx* c) {
                    c->W2[0].smp,     c->W2[0].active,  c->W2[0].active_ord, c->W2[1].active_ord,
                    c->W2[0].ord_hist, c->W2[1].ord_hist,    c->W2[1].pair,    c->W2[1].blk,
                    c->W2[1].blk_n, c->W2[1].fb,        c->W2[1].smp,     c->W2[1].active,
-                   c->W2[0].cagg,    c->W2[1].cagg,      c->W2[0].act,     c->W2[1].act};
+                   c->W2[0].cagg,    c->W2[1].cagg,      c->W2[0].act,     c->W2[1].act,
+                   c->W2[0].spn,     c->W2[1].spn};
     for (void* d : dev)
         if (d) (void)hipFree(d);
     for (int i = 0; i < 2; i++) {
@@ -865,29 +907,67 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
                     "max_points %llu exceeds what one batch can hold (%llu: %u pair and %u sample "
                     "slots per ray)", (unsigned long long)p->max_points, (unsigned long long)bp,
                     maxp, spr);
+    // Single walk: k_walk keeps a ray's samples in one register slot per DDA step, so
+    // the band's walk must have a proven bound: a segment of L voxels crosses at most floor(L |u_a|)
+    // + 1 boundaries per axis, i.e. visits <= sqrt(3) L + 4 voxels.  Carving and Voxblox clearing
+    // rays (length up to max_range) keep the two-walk path, the default (tsdf_params.walk).
+    {
+        const double band = 2.0 * p->sdf_trunc / p->voxel_size;
+        const double steps = std::floor(std::sqrt(3.0) * band * (1.0 + 1e-4)) + 5.0;
+        const bool clearing = p->semantics == TSDF_SEM_VOXBLOX && p->allow_clear &&
+                              std::isfinite(p->max_range);
+        c->fused = p->walk == TSDF_WALK_SINGLE && !p->space_carving && !clearing && maxp <= 4 &&
+                   steps <= 32.0;
+        c->nstep = steps <= 16.0 ? 16 : 32;
+    }
+    const uint64_t stg = (uint64_t)WLK_THREADS * (uint64_t)c->nstep;  // samples per k_walk region
+    if (c->fused) {
+        // the span record addresses 2^30 samples: at most 2^30 / stg k_walk workgroups per batch
+        const uint64_t lim = ((1ull << 30) / (2 * stg) - MAX_BATCH - 1) * RPB;
+        bp = std::min<uint64_t>(bp, lim);
+        if (bp < p->max_points)
+            return fail(c, TSDF_EINVAL, "max_points %llu exceeds a single-walk batch (%llu)",
+                        (unsigned long long)p->max_points, (unsigned long long)bp);
+    }
     c->max_points = p->max_points;
     c->batch_points = bp;
     const uint64_t slots = bp * maxp;
     c->slots = slots;
-    c->T.cell_stride = (c->max_batch + 3u) & ~3u;
-    c->Wk.maxp = maxp;
-    c->Wk.max_smp = (uint32_t)std::min<uint64_t>(
-        std::min<uint64_t>(bp * spr / std::max<uint32_t>(1u, p->n_sectors), smp_budget),
-        0xFFFFFFF0ull);
-    // fallback pairs (a workgroup's LDS brick hash is full): rare without carving, the rule with it
-    // (the fallback index has 26 bits; past it pairs are dropped and OVF_FB reported)
-    c->Wk.max_fb = (uint32_t)std::min<uint64_t>(
-        p->space_carving ? slots : std::max<uint64_t>(slots / 16, 1u << 20), 1u << 26);
     c->max_blocks = (uint32_t)(c->batch_points / RPB + MAX_BATCH + 1);
+    const uint32_t nsec = std::max<uint32_t>(1u, p->n_sectors);
+    if (c->fused) {
+        // 64-bit cells and a totals cell after the last scan; the pair and fallback lists are not
+        // used; one region of stg samples per k_walk workgroup (sharded: this GPU's share of the
+        // blocks, grown on OVF_SMP); span records ~ samples / SPAN + one partial span per run
+        c->T.cell_stride = (c->max_batch + 2u) & ~1u;
+        c->Wk.maxp = maxp;
+        const uint64_t reg_blocks = nsec > 1 ? std::min<uint64_t>(
+            c->max_blocks, c->max_blocks * 5ull / (4ull * nsec) + 2ull * c->max_batch + 64) : c->max_blocks;
+        c->Wk.max_smp = (uint32_t)std::min<uint64_t>(2 * reg_blocks * stg, 1ull << 30);
+        c->Wk.max_spn = (uint32_t)std::min<uint64_t>(
+            bp * spr / SPAN / nsec + 2 * reg_blocks * 256, 0xFFFFFFF0ull);
+        c->Wk.max_fb = 4;
+    } else {
+        c->T.cell_stride = (c->max_batch + 3u) & ~3u;
+        c->Wk.maxp = maxp;
+        c->Wk.max_smp = (uint32_t)std::min<uint64_t>(
+            std::min<uint64_t>(bp * spr / nsec, smp_budget), 0xFFFFFFF0ull);
+        // fallback pairs (a workgroup's LDS brick hash is full): rare without carving, the rule with
+        // it (the fallback index has 26 bits; past it pairs are dropped and OVF_FB reported)
+        c->Wk.max_fb = (uint32_t)std::min<uint64_t>(
+            p->space_carving ? slots : std::max<uint64_t>(slots / 16, 1u << 20), 1u << 26);
+        c->Wk.max_spn = 4;
+    }
 
     for (int q = 0; q < 2; q++) {  // one set per batch parity (capacity-independent part)
         Work& W = c->W2[q];
         W = c->Wk;
-        HIPCHK(c, hipMalloc(&W.pair, slots * sizeof(uint32_t)));
+        HIPCHK(c, hipMalloc(&W.pair, (c->fused ? 4 : slots) * sizeof(uint32_t)));
         HIPCHK(c, hipMalloc(&W.blk, (size_t)c->max_blocks * 2 * HCAP * sizeof(uint4)));
         HIPCHK(c, hipMalloc(&W.blk_n, (size_t)c->max_blocks * 2 * sizeof(uint32_t)));
         HIPCHK(c, hipMalloc(&W.fb, (size_t)W.max_fb * sizeof(uint4)));
         HIPCHK(c, hipMalloc(&W.smp, (size_t)W.max_smp * sizeof(uint2)));
+        HIPCHK(c, hipMalloc(&W.spn, (size_t)W.max_spn * sizeof(uint32_t)));
         HIPCHK(c, hipMalloc(&W.ord_hist, 64 * 32 * sizeof(uint32_t)));
         HIPCHK(c, hipMalloc(&W.act, (size_t)c->max_blocks * sizeof(uint32_t)));
         HIPCHK(c, hipMalloc(&c->stage2[q], c->batch_points * 3 * sizeof(float)));

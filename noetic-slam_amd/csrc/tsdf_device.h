@@ -11,7 +11,9 @@
 //           slots[cap] u32  brick-pool slot (UNASSIGNED until the batch's compaction pass)
 //           touched[cap] u32  1 if the batch touches the brick (k_count sets, k_compact clears)
 //           cell[cap * cell_stride] u32  per (brick, scan) SAMPLE counts (k_count), then the
-//                                        absolute position of those samples (k_compact)
+//                                        absolute position of those samples (k_compact);
+//                                        single walk: u64 (samples | spans << 32), then (relative
+//                                        sample prefix | absolute span position << 32)
 //   Pool    sdf[max_bricks][512] f32, weight[max_bricks][512] f32 — voxel l = z*64 + y*8 + x;
 //           brick_keys[max_bricks] u64 (slot -> key, for export)
 //   Work    pair[max_batch_points * maxp] u32    per-ray pair codes (see PAIR_*)
@@ -47,6 +49,10 @@ constexpr int RPB = TSDF_RPB;          // rays per k_count / k_place block (one 
 constexpr int HCAP = TSDF_HCAP;        // LDS brick-hash slots per k_count block (~300-800 used)
 constexpr int LDS_PROBES = 64;         // probe limit before a pair takes the global fallback
 constexpr int MAX_IN_BRICK = 22;       // a line visits at most 8+8+8-2 voxels of an 8^3 brick
+// single-walk front end (tsdf_walk.hip): rays per k_walk workgroup (one per lane; half an RPB
+// block) and samples per span record
+constexpr int WLK_THREADS = RPB / 2;
+constexpr int SPAN = 4;
 
 // pair codes (one u32 per (ray, k-th brick) slot); count = the pair's in-brick samples
 //   local:    bit 31 = 0 | count << 26 | lid << 15 | local sample offset  (lid < HCAP,
@@ -64,7 +70,9 @@ static_assert(HCAP <= (1 << (PAIR_CNT_SHIFT - PAIR_LID_SHIFT)), "lid overflows")
 
 // overflow bits (sticky until tsdf_sync reads them)
 constexpr uint32_t OVF_TABLE = 1u, OVF_POOL = 2u, OVF_PAIRS = 4u, OVF_ACTIVE = 8u, OVF_FB = 16u,
-                   OVF_SMP = 32u;  // the batch's samples exceed the sample list
+                   OVF_SMP = 32u,  // the batch's samples exceed the sample list (single walk:
+                                   // the workgroup regions)
+                   OVF_SPN = 64u;  // single walk: the batch's spans exceed the span list
 // a border tile whose brick this context lacks (tsdf_border_merge_device; sticky like OVF_*)
 constexpr uint32_t ERR_MERGE_KEY = 1u << 8;
 
@@ -141,7 +149,8 @@ struct Table {
     uint64_t* brick_keys;  // pool slot -> key
     uint64_t mask;
     uint32_t max_bricks;
-    uint32_t cell_stride;  // >= max_batch, multiple of 4
+    uint32_t cell_stride;  // cells per row: u32 >= max_batch, multiple of 4 (two walks); u64 >=
+                           // max_batch + 1, even (single walk: a totals cell after the last scan)
 };
 
 struct Pool {
@@ -162,10 +171,13 @@ struct Work {
     uint32_t* ord_hist; // k_order: per (slice, size class) counts, then first positions
     uint4* cagg;    // k_compact: per table chunk (touched bricks, samples, new bricks), then bases
     uint32_t* act;  // sector sharding: the k_count blocks holding a ray of this GPU's sector (n_act)
+    uint32_t* spn;  // single walk: span records (sample position | (samples - 1) << 30), per brick
+                    // contiguous and scan-ordered (k_spans)
     uint32_t maxp;        // pair slots per ray
     uint32_t max_active;  // capacity of `active`
     uint32_t max_fb;      // capacity of `fb`
     uint32_t max_smp;     // capacity of smp
+    uint32_t max_spn;     // capacity of spn
 };
 
 // per-batch counters, double-buffered by batch parity (zeroed by k_finish at the end of a batch)
@@ -212,7 +224,11 @@ struct Globals {
     BatchRecord ring[METRIC_RING];  // per-batch records (k_finish), drained by the host's metrics log
 };
 
-enum KernelKind { KIND_COUNT = 0, KIND_COMPACT = 1, KIND_PLACE = 2, KIND_INTEGRATE = 3, KIND_N = 4 };
+enum KernelKind {
+    KIND_COUNT = 0, KIND_COMPACT = 1, KIND_PLACE = 2, KIND_INTEGRATE = 3,
+    KIND_WALK = 4, KIND_SPANS = 5,  // the single-walk front end
+    KIND_N = 6
+};
 
 // Optional per-kernel HIP-event timing (profiling mode); implemented in tsdf_capi.cpp.
 struct KernelTimer {
@@ -230,8 +246,15 @@ inline uint64_t compact_chunks(uint64_t cap) { return (cap + CMP_CHUNK - 1) / CM
 // kernels' other workgroups leave after one load.
 hipError_t launch_sector_flags(const float* d_xyz, const BatchRef& D, const RayConst& R,
                                const Work& Wk, Globals* G, int parity, hipStream_t st);
+// fused: the single-walk path's 64-bit cells (samples | spans << 32; after k_compact_write the
+// relative sample prefix | absolute span position, with the totals at scan n_scans)
 hipError_t launch_compact(const BatchRef& D, const Table& T, const Work& Wk, Globals* G,
-                          int parity, hipStream_t st);
+                          int parity, bool fused, hipStream_t st);
+// single-walk front end (tsdf_walk.hip); nstep = 16 or 32 register slots per ray
+hipError_t launch_walk(const float* d_xyz, const BatchRef& D, const RayConst& R, const Table& T,
+                       const Work& Wk, Globals* G, int parity, int nstep, hipStream_t st);
+hipError_t launch_spans(const BatchRef& D, const RayConst& R, const Table& T, const Work& Wk,
+                        Globals* G, int parity, int nstep, hipStream_t st);
 hipError_t launch_place(const float* d_xyz, const BatchRef& D, const RayConst& R, const Table& T,
                         const Work& Wk, Globals* G, int parity, hipStream_t st);
 hipError_t launch_finish(Globals* G, int parity, uint32_t batch_id, hipStream_t st);
@@ -239,8 +262,10 @@ hipError_t launch_finish(Globals* G, int parity, uint32_t batch_id, hipStream_t 
 hipError_t launch_rehash(const Table& T, uint32_t n, Globals* G, hipStream_t st);
 // Orders the batch's active bricks by size class, largest first (k_integrate's load balance).
 hipError_t launch_order(const Work& Wk, Globals* G, int parity, hipStream_t st);
+// fused: samples through the span list (single walk); big: batches of more than 64 scans
 hipError_t launch_integrate(const BatchRef& D, const RayConst& R, const Table& T, const Work& Wk,
-                            const Pool& Pl, Globals* G, int parity, hipStream_t st);
+                            const Pool& Pl, Globals* G, int parity, bool fused, bool big,
+                            hipStream_t st);
 hipError_t launch_query_dense(const Table& T, const Pool& Pl, const int lo[3], const int dims[3],
                               float bg, float* d_sdf, float* d_w, hipStream_t st);
 hipError_t launch_import(const Table& T, const Pool& Pl, const int32_t* d_coords, uint32_t n,

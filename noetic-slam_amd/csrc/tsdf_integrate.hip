@@ -45,6 +45,14 @@ typedef uint32_t MaskT;
 #define MASK_POPC(m) __popc(m)
 #endif
 constexpr uint32_t INT_MAX_WIN = TSDF_INT_WIN;       // scans per window (mask bits)
+// single walk (FUSED): the register cache holds INT_SPT span records' samples per thread, so a
+// chunk is INT_SCH spans; a window also keeps its spans <= INT_SCH (one chunk per window)
+#ifndef TSDF_INT_SPT
+#define TSDF_INT_SPT 2
+#endif
+constexpr int INT_SPT = TSDF_INT_SPT;
+constexpr uint32_t INT_SCH = INT_SPT * INT_THREADS;
+constexpr uint32_t NO_SPAN = 0xFFFFFFFFu;
 
 #ifdef TSDF_ABLATE_PHASE  // `make ablate ABLATE=PHASE`
 #define TSDF_PHASE_TIMING
@@ -71,9 +79,13 @@ constexpr uint32_t INT_MAX_WIN = TSDF_INT_WIN;       // scans per window (mask b
 // clamps the distance to +-tau and the weight to max_weight.
 // MAXS: the most scans a batch of this instantiation holds (64: the LDS of the single-GPU batches;
 // 512: the sector-sharded multi-GPU batches, one batch per step).
-template <int SEM, int MAXS>
+// FUSED (single walk, tsdf_walk.hip): a brick's samples are read through its span records (active
+// record = (table index, slot, first span, spans); 64-bit cells = relative sample prefix | absolute
+// span position, the totals at scan n_scans).  Otherwise they are one contiguous segment (k_place).
+template <int SEM, int MAXS, bool FUSED>
 __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchRef D, Table T, Work Wk, Pool Pl,
                                                           Globals* G, int parity, RayConst R) {
+    constexpr int NSLOT = FUSED ? INT_SPT * SPAN : INT_PER;  // register-cached samples per thread
     typedef typename std::conditional<SEM == 1, unsigned long long, uint32_t>::type CellB;
     __shared__ unsigned long long cA[INT_CAP];  // live cell: sum of trunc(s w * 2^32)
     __shared__ CellB cB[INT_CAP];               // live cell: sample count / sum of trunc(w 2^32)
@@ -85,6 +97,7 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchRef D, Table T, 
     // brick's per-scan sample prefix, double-buffered by brick parity: a wave may still read the
     // previous brick's prefix while another writes the next one
     __shared__ uint32_t s_csb[2][MAXS + 1];
+    __shared__ uint32_t s_psb[FUSED ? 2 : 1][FUSED ? MAXS + 1 : 1];  // FUSED: per-scan span positions
     static_assert(MAXS <= 2 * INT_THREADS, "two cells per thread");
     __shared__ uint32_t s_red[INT_THREADS / 64];
     __shared__ uint32_t s_nlive, s_ncell;
@@ -107,27 +120,54 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchRef D, Table T, 
     // Software pipeline over the workgroup's bricks: while brick a is processed, brick a + G's
     // cell row, (S, W) and first INT_CAP samples are in flight to registers (BrickRegs), and
     // brick a + 2G's active record is loading.  A brick then starts with its data at hand.
+    typedef typename std::conditional<FUSED, unsigned long long, uint32_t>::type CellT;
+    const CellT* cells = reinterpret_cast<const CellT*>(T.cell);
     struct BrickRegs {
-        uint2 c[INT_PER];
+        uint2 c[NSLOT];
         float s0, s1, w0, w1;
-        uint32_t cell, cell2;
+        CellT cell, cell2;
     };
+    // FUSED: span records [p, min(p + INT_SCH, pend)) -> sp; their samples -> c (a span of cnt
+    // samples fills slots j * SPAN .. j * SPAN + cnt - 1; empty slots hold scan ~0: never in a window)
+    auto load_spans = [&](uint32_t p, uint32_t pend, uint32_t (&sp)[INT_SPT]) {
+#pragma unroll
+        for (int j = 0; j < INT_SPT; j++) {
+            const uint32_t q = p + tid + j * INT_THREADS;
+            sp[j] = (q < pend && q < Wk.max_spn) ? Wk.spn[q] : NO_SPAN;
+        }
+    };
+    auto load_span_samples = [&](const uint32_t (&sp)[INT_SPT], uint2 (&c)[NSLOT]) {
+#pragma unroll
+        for (int j = 0; j < INT_SPT; j++) {
+            const uint32_t e = sp[j];
+            const uint32_t src = e & 0x3FFFFFFFu, cnt = e == NO_SPAN ? 0u : (e >> 30) + 1u;
+#pragma unroll
+            for (int k = 0; k < SPAN; k++)
+                c[j * SPAN + k] = ((uint32_t)k < cnt && src + k < Wk.max_smp) ? Wk.smp[src + k]
+                                                                           : make_uint2(0u, ~0u);
+        }
+    };
+    uint32_t SP[INT_SPT];  // FUSED: span records of the next brick to load
     auto load_brick = [&](const uint4& r, BrickRegs& B) {
         const uint32_t n = r.w, base = r.z;
         const bool has = r.y < T.max_bricks;
+        if constexpr (FUSED) {
+            load_span_samples(SP, B.c);
+        } else {
 #pragma unroll
-        for (int j = 0; j < INT_PER; j++) {
-            const uint32_t i = tid + j * INT_THREADS;
-            // base + i >= max_smp: capacity overflow (reported by k_compact)
-            B.c[j] = (i < n && base + i < Wk.max_smp) ? Wk.smp[base + i] : make_uint2(0u, ~0u);
+            for (int j = 0; j < INT_PER; j++) {
+                const uint32_t i = tid + j * INT_THREADS;
+                // base + i >= max_smp: capacity overflow (reported by k_compact)
+                B.c[j] = (i < n && base + i < Wk.max_smp) ? Wk.smp[base + i] : make_uint2(0u, ~0u);
+            }
         }
-        // absolute position of the brick's scan-tid samples -> relative to its segment
+        // two walks: absolute position of the brick's scan-tid samples -> relative to its segment
         // (made relative to the segment where it is consumed: a use here, or a load inside a
-        // branch, would make the compiler wait for this prefetch at once)
-        B.cell = T.cell[(size_t)r.x * T.cell_stride + min((uint32_t)tid, T.cell_stride - 1u)];
+        // branch, would make the compiler wait for this prefetch at once); FUSED: the cell as is
+        B.cell = cells[(size_t)r.x * T.cell_stride + min((uint32_t)tid, T.cell_stride - 1u)];
         if (MAXS > INT_THREADS)
-            B.cell2 = T.cell[(size_t)r.x * T.cell_stride +
-                             min((uint32_t)tid + INT_THREADS, T.cell_stride - 1u)];
+            B.cell2 = cells[(size_t)r.x * T.cell_stride +
+                            min((uint32_t)tid + INT_THREADS, T.cell_stride - 1u)];
         const float* Sg = Pl.sdf + (size_t)(has ? r.y : 0) * BRICK_VOX;
         const float* Wg = Pl.weight + (size_t)(has ? r.y : 0) * BRICK_VOX;
         B.s0 = has ? Sg[tid] : R.bg;
@@ -136,34 +176,73 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchRef D, Table T, 
         B.w1 = has ? Wg[tid + 256] : 0.0f;
     };
     const uint32_t G0 = gridDim.x;
-    uint4 rec_next = blockIdx.x + G0 < n_active ? Wk.active[blockIdx.x + G0] : make_uint4(0u, 0u, 0u, 0u);
+    const uint4 zero4 = make_uint4(0u, 0u, 0u, 0u);
+    auto rec_at = [&](uint32_t a) { return a < n_active ? Wk.active[a] : zero4; };
     BrickRegs P;
-    if (blockIdx.x < n_active) load_brick(Wk.active[blockIdx.x], P);
-    uint4 rec = blockIdx.x < n_active ? Wk.active[blockIdx.x] : make_uint4(0u, 0u, 0u, 0u);
+    uint4 rec = rec_at(blockIdx.x);
+    uint4 rec_next = rec_at(blockIdx.x + G0);
+    uint4 rec_next2 = FUSED ? rec_at(blockIdx.x + 2 * G0) : zero4;
+    if constexpr (FUSED) {
+        // three-stage pipeline: records three bricks ahead, span records two, samples one
+        if (blockIdx.x < n_active) {
+            load_spans(rec.z, rec.z + rec.w, SP);
+            load_brick(rec, P);
+        }
+        if (blockIdx.x + G0 < n_active) load_spans(rec_next.z, rec_next.z + rec_next.w, SP);
+    } else {
+        if (blockIdx.x < n_active) load_brick(rec, P);
+    }
     for (uint32_t a = blockIdx.x; a < n_active; a += G0, par ^= 1u) {
         uint32_t* s_cs = s_csb[par];
-        const uint4 cur = rec;  // (h, slot, toff, n)
+        uint32_t* s_ps = s_psb[FUSED ? par : 0];
+        const uint4 cur = rec;  // (h, slot, toff, n); FUSED: (h, slot, first span, spans)
         const BrickRegs B = P;
         rec = rec_next;
-        if (a + G0 < n_active) load_brick(rec, P);                     // brick a + G
-        if (a + 2 * G0 < n_active) rec_next = Wk.active[a + 2 * G0];  // record of a + 2G
+        if (a + G0 < n_active) load_brick(rec, P);  // brick a + G
+        if constexpr (FUSED) {
+            rec_next = rec_next2;
+            if (a + 2 * G0 < n_active) load_spans(rec_next.z, rec_next.z + rec_next.w, SP);  // a + 2G
+            if (a + 3 * G0 < n_active) rec_next2 = Wk.active[a + 3 * G0];                  // a + 3G
+        } else {
+            if (a + 2 * G0 < n_active) rec_next = Wk.active[a + 2 * G0];  // record of a + 2G
+        }
         const uint32_t h = cur.x, n = cur.w, base = cur.z;
-        uint2 c[INT_PER];
+        uint2 c[NSLOT];
 #pragma unroll
-        for (int j = 0; j < INT_PER; j++) c[j] = B.c[j];
-        uint32_t cq = 0;  // samples [cq, cq + INT_CAP) are in c[] (uniform)
+        for (int j = 0; j < NSLOT; j++) c[j] = B.c[j];
+        // samples [cq, cq + INT_CAP) (FUSED: spans [cq, cq + INT_SCH)) are in c[] (uniform)
+        uint32_t cq = FUSED ? base : 0u;
+        const uint32_t pend = FUSED ? base + n : 0u;  // FUSED: the brick's span end
         auto load_chunk = [&](uint32_t q) {
             cq = q;
+            if constexpr (FUSED) {
+                uint32_t sp[INT_SPT];
+                load_spans(q, pend, sp);
+                load_span_samples(sp, c);
+            } else {
 #pragma unroll
-            for (int j = 0; j < INT_PER; j++) {
-                const uint32_t i = q + tid + j * INT_THREADS;
-                c[j] = (i < n && base + i < Wk.max_smp) ? Wk.smp[base + i] : make_uint2(0u, ~0u);
+                for (int j = 0; j < INT_PER; j++) {
+                    const uint32_t i = q + tid + j * INT_THREADS;
+                    c[j] = (i < n && base + i < Wk.max_smp) ? Wk.smp[base + i] : make_uint2(0u, ~0u);
+                }
             }
         };
         const bool has_slot = cur.y < T.max_bricks;
-        if ((uint32_t)tid < ns) s_cs[tid] = B.cell - base;
-        if (MAXS > INT_THREADS && (uint32_t)tid + INT_THREADS < ns) s_cs[tid + INT_THREADS] = B.cell2 - base;
-        if (tid == 0) s_cs[ns] = n;
+        if constexpr (FUSED) {
+            // per scan: relative sample prefix, absolute span position (scan ns: the totals)
+            if ((uint32_t)tid <= ns) {
+                s_cs[tid] = (uint32_t)B.cell;
+                s_ps[tid] = (uint32_t)(B.cell >> 32);
+            }
+            if (MAXS > INT_THREADS && (uint32_t)tid + INT_THREADS <= ns) {
+                s_cs[tid + INT_THREADS] = (uint32_t)B.cell2;
+                s_ps[tid + INT_THREADS] = (uint32_t)(B.cell2 >> 32);
+            }
+        } else {
+            if ((uint32_t)tid < ns) s_cs[tid] = B.cell - base;
+            if (MAXS > INT_THREADS && (uint32_t)tid + INT_THREADS < ns) s_cs[tid + INT_THREADS] = B.cell2 - base;
+            if (tid == 0) s_cs[ns] = n;
+        }
         float* Sg = Pl.sdf + (size_t)(has_slot ? cur.y : 0) * BRICK_VOX;
         float* Wg = Pl.weight + (size_t)(has_slot ? cur.y : 0) * BRICK_VOX;
         // sS / sW of voxels tid, tid + 256: the previous brick's last readers are past a barrier
@@ -179,10 +258,16 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchRef D, Table T, 
             // window [t0, t1): as many scans as keep its samples <= INT_CAP (at least one)
             // (the extension test is monotone in the scan: one lane per candidate, one ballot)
             const uint32_t q0 = s_cs[t0];
+            const uint32_t p0 = FUSED ? s_ps[t0] : 0u;
             const uint32_t tt = t0 + 1 + lane;
-            const bool ext = tt < ns && tt - t0 < INT_MAX_WIN && s_cs[min(tt + 1, ns)] - q0 <= INT_CAP;
+            const bool ext = tt < ns && tt - t0 < INT_MAX_WIN && s_cs[min(tt + 1, ns)] - q0 <= INT_CAP &&
+                             (!FUSED || s_ps[min(tt + 1, ns)] - p0 <= INT_SCH);
             const uint32_t t1 = t0 + 1 + (uint32_t)__popcll(__ballot(ext));
             const uint32_t q1 = s_cs[t1], nw = t1 - t0;
+            const uint32_t p1 = FUSED ? s_ps[t1] : 0u;
+            // the window's chunks: samples [q0, q1) in INT_CAP steps, FUSED spans [p0, p1) in INT_SCH
+            const uint32_t ck0 = FUSED ? p0 : q0, ck1 = FUSED ? p1 : q1;
+            constexpr uint32_t CK = FUSED ? INT_SCH : INT_CAP;
             if (q0 == q1) {  // uniform: no sample of this brick in the window
                 t0 = t1;
                 continue;
@@ -191,13 +276,13 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchRef D, Table T, 
             nwin++;
 #endif
             // P1: scan masks (a one-scan window may exceed INT_CAP samples: chunked)
-            for (uint32_t qc = q0; qc < q1; qc += INT_CAP) {
+            for (uint32_t qc = ck0; qc < ck1; qc += CK) {
                 if (cq != qc) {
                     load_chunk(qc);
                     PHASE(2);
                 }
 #pragma unroll
-                for (int j = 0; j < INT_PER; j++) {
+                for (int j = 0; j < NSLOT; j++) {
                     const uint32_t w = (c[j].y >> 9) - t0;
 #ifdef TSDF_ABLATE_INT_NOP1
                     if (w < nw && c[j].x == 0x7FFFFFFFu)
@@ -255,12 +340,12 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchRef D, Table T, 
             __syncthreads();
             PHASE(4);
             // P3: accumulate into the live cells
-            for (uint32_t qc = q0; qc < q1; qc += INT_CAP) {
+            for (uint32_t qc = ck0; qc < ck1; qc += CK) {
                 if (cq != qc) {
                     load_chunk(qc);
                 }
 #pragma unroll
-                for (int j = 0; j < INT_PER; j++) {
+                for (int j = 0; j < NSLOT; j++) {
                     const uint32_t w = (c[j].y >> 9) - t0;
                     if (w < nw) {
                         const uint32_t l = c[j].y & 511u;
@@ -286,7 +371,7 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchRef D, Table T, 
                 }
             }
             // the next window starts at q1: its samples load while this one converts and fuses
-            if (q1 < n) load_chunk(q1);
+            if (FUSED ? p1 < pend : q1 < n) load_chunk(ck1);
             __syncthreads();
             PHASE(5);
 #ifndef TSDF_FUSE_P4A
@@ -419,7 +504,8 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchRef D, Table T, 
         }
         ndirty += __popc(dirty);
         // zero every cell of the brick (k_compact prefixes whole uint4 groups) for the next batch
-        for (uint32_t q = tid; q < T.cell_stride; q += INT_THREADS) T.cell[(size_t)h * T.cell_stride + q] = 0u;
+        for (uint32_t q = tid; q < T.cell_stride; q += INT_THREADS)
+            const_cast<CellT*>(cells)[(size_t)h * T.cell_stride + q] = 0u;
 #ifdef TSDF_PHASE_TIMING
         nb++;
 #endif
@@ -450,14 +536,14 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchRef D, Table T, 
 // Grid = exactly the workgroups the device holds at once (CUs x resident workgroups per CU, from
 // the occupancy API: VGPRs or LDS, whichever binds): every workgroup of the grid-stride loop starts
 // at once, none waits for a second dispatch round.
-template <int SEM, int MAXS>
+template <int SEM, int MAXS, bool FUSED>
 static int integrate_grid() {
     static int grid = 0;
     if (grid == 0) {
         int dev = 0, cus = 0, per_cu = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_integrate<SEM, MAXS>,
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_integrate<SEM, MAXS, FUSED>,
                                                          INT_THREADS, 0) != hipSuccess ||
             cus <= 0 || per_cu <= 0) {
             cus = 256;
@@ -468,24 +554,31 @@ static int integrate_grid() {
     return grid;
 }
 
-template <int SEM, int MAXS>
+template <int SEM, int MAXS, bool FUSED>
 static void integrate_sem(const BatchRef& D, const RayConst& R, const Table& T, const Work& Wk,
                           const Pool& Pl, Globals* G, int parity, hipStream_t st) {
-    k_integrate<SEM, MAXS><<<integrate_grid<SEM, MAXS>(), INT_THREADS, 0, st>>>(D, T, Wk, Pl, G,
-                                                                                parity, R);
+    k_integrate<SEM, MAXS, FUSED><<<integrate_grid<SEM, MAXS, FUSED>(), INT_THREADS, 0, st>>>(
+        D, T, Wk, Pl, G, parity, R);
+}
+
+template <bool FUSED>
+static void integrate_mode(const BatchRef& D, const RayConst& R, const Table& T, const Work& Wk,
+                           const Pool& Pl, Globals* G, int parity, bool big, hipStream_t st) {
+    // SEM 2 (VDBFusion at double precision) fuses like SEM 0
+    if (R.sem == 1) {
+        if (big) integrate_sem<1, MAX_BATCH, FUSED>(D, R, T, Wk, Pl, G, parity, st);
+        else integrate_sem<1, 64, FUSED>(D, R, T, Wk, Pl, G, parity, st);
+    } else {
+        if (big) integrate_sem<0, MAX_BATCH, FUSED>(D, R, T, Wk, Pl, G, parity, st);
+        else integrate_sem<0, 64, FUSED>(D, R, T, Wk, Pl, G, parity, st);
+    }
 }
 
 hipError_t launch_integrate(const BatchRef& D, const RayConst& R, const Table& T, const Work& Wk,
-                            const Pool& Pl, Globals* G, int parity, hipStream_t st) {
-    // SEM 2 (VDBFusion at double precision) fuses like SEM 0
-    const bool big = T.cell_stride > 64;
-    if (R.sem == 1) {
-        if (big) integrate_sem<1, MAX_BATCH>(D, R, T, Wk, Pl, G, parity, st);
-        else integrate_sem<1, 64>(D, R, T, Wk, Pl, G, parity, st);
-    } else {
-        if (big) integrate_sem<0, MAX_BATCH>(D, R, T, Wk, Pl, G, parity, st);
-        else integrate_sem<0, 64>(D, R, T, Wk, Pl, G, parity, st);
-    }
+                            const Pool& Pl, Globals* G, int parity, bool fused, bool big,
+                            hipStream_t st) {
+    if (fused) integrate_mode<true>(D, R, T, Wk, Pl, G, parity, big, st);
+    else integrate_mode<false>(D, R, T, Wk, Pl, G, parity, big, st);
     return hipGetLastError();
 }
 

@@ -430,6 +430,24 @@ __device__ __forceinline__ uint32_t compact_list(const Table& T, uint32_t chunk,
     return nh;
 }
 
+// A brick's cell row as uint4 groups, and the group's count (fused: u64 cells, two per group, the
+// span counts in the high words; the row runs to the totals cell at n_scans).
+template <bool FUSED>
+__device__ __forceinline__ uint32_t row_groups(uint32_t n_scans) {
+    return FUSED ? (n_scans + 2) / 2 : (n_scans + 3) / 4;
+}
+template <bool FUSED>
+__device__ __forceinline__ uint32_t group_count(const uint4& v) {
+    return FUSED ? v.y + v.w : v.x + v.y + v.z + v.w;
+}
+template <bool FUSED>
+__device__ __forceinline__ const uint4* cell_row(const Table& T, uint32_t h) {
+    return FUSED ? reinterpret_cast<const uint4*>(reinterpret_cast<const uint64_t*>(T.cell) +
+                                                  (size_t)h * T.cell_stride)
+                 : reinterpret_cast<const uint4*>(T.cell + (size_t)h * T.cell_stride);
+}
+
+template <bool FUSED>
 __global__ __launch_bounds__(CMP_THREADS) void k_compact_sum(uint32_t n_scans, Table T, Work Wk) {
     __shared__ uint32_t s_w[CMP_THREADS / 64];
     __shared__ uint32_t s_h[CMP_CHUNK];
@@ -439,16 +457,13 @@ __global__ __launch_bounds__(CMP_THREADS) void k_compact_sum(uint32_t n_scans, T
         s_acc[1] = 0u;
     }
     const uint32_t nh = compact_list(T, blockIdx.x * CMP_CHUNK, s_h, s_w, false);
-    const uint32_t nq = (n_scans + 3) / 4;  // cell_stride is a multiple of 4
+    const uint32_t nq = row_groups<FUSED>(n_scans);  // whole uint4 groups (see cell_stride)
     const uint32_t grp = threadIdx.x / CMP_GROUP, li = threadIdx.x % CMP_GROUP;
-    uint32_t samples = 0, nnew = 0;
+    uint32_t samples = 0, nnew = 0;  // fused: spans
     for (uint32_t k = grp; k < nh; k += CMP_THREADS / CMP_GROUP) {
         const uint32_t h = s_h[k];
-        const uint4* cp = reinterpret_cast<const uint4*>(T.cell + (size_t)h * T.cell_stride);
-        for (uint32_t q = li; q < nq; q += CMP_GROUP) {  // 64 scans per pass
-            const uint4 v = cp[q];
-            samples += v.x + v.y + v.z + v.w;
-        }
+        const uint4* cp = cell_row<FUSED>(T, h);
+        for (uint32_t q = li; q < nq; q += CMP_GROUP) samples += group_count<FUSED>(cp[q]);
         if (li == 0 && T.slots[h] == UNASSIGNED) nnew++;
     }
     samples = wave_sum<uint32_t>(samples);
@@ -462,7 +477,8 @@ __global__ __launch_bounds__(CMP_THREADS) void k_compact_sum(uint32_t n_scans, T
 }
 
 __global__ __launch_bounds__(CMP_SCAN_THREADS) void k_compact_scan(uint32_t nch, Work Wk,
-                                                                   Globals* G, int parity) {
+                                                                   Globals* G, int parity,
+                                                                   int fused) {
     __shared__ uint32_t s_w[3][CMP_SCAN_THREADS / 64];
     __shared__ uint32_t s_carry[3];
     Counters* C = &G->ctr[parity];
@@ -493,11 +509,13 @@ __global__ __launch_bounds__(CMP_SCAN_THREADS) void k_compact_scan(uint32_t nch,
         C->cursor = s_carry[1];
         C->n_new = s_carry[2] - G->pool_count;
         G->pool_count = s_carry[2];
-        if (s_carry[1] > Wk.max_smp) atomicOr(&C->ovf, OVF_SMP);
+        if (fused ? s_carry[1] > Wk.max_spn : s_carry[1] > Wk.max_smp)
+            atomicOr(&C->ovf, fused ? OVF_SPN : OVF_SMP);
         if (s_carry[0] > Wk.max_active) atomicOr(&C->ovf, OVF_ACTIVE);
     }
 }
 
+template <bool FUSED>
 __global__ __launch_bounds__(CMP_THREADS) void k_compact_write(uint32_t n_scans, uint32_t nch,
                                                                Table T, Work Wk, Globals* G,
                                                                int parity) {
@@ -507,15 +525,12 @@ __global__ __launch_bounds__(CMP_THREADS) void k_compact_write(uint32_t n_scans,
     const uint32_t chunk = blockIdx.x * CMP_CHUNK;
     const uint32_t nh = compact_list(T, chunk, s_h, s_w, true);
     if (nh == 0) return;  // uniform
-    const uint32_t nq = (n_scans + 3) / 4;
+    const uint32_t nq = row_groups<FUSED>(n_scans);
     const uint32_t grp = threadIdx.x / CMP_GROUP, li = threadIdx.x % CMP_GROUP;
     for (uint32_t k = grp; k < nh; k += CMP_THREADS / CMP_GROUP) {
-        const uint4* cp = reinterpret_cast<const uint4*>(T.cell + (size_t)s_h[k] * T.cell_stride);
-        uint32_t sum = 0;
-        for (uint32_t q = li; q < nq; q += CMP_GROUP) {
-            const uint4 v = cp[q];
-            sum += v.x + v.y + v.z + v.w;
-        }
+        const uint4* cp = cell_row<FUSED>(T, s_h[k]);
+        uint32_t sum = 0;  // fused: spans
+        for (uint32_t q = li; q < nq; q += CMP_GROUP) sum += group_count<FUSED>(cp[q]);
 #pragma unroll
         for (int d = CMP_GROUP / 2; d >= 1; d >>= 1) sum += __shfl_xor(sum, d, CMP_GROUP);
         if (li == 0) s_n[k] = sum;
@@ -559,6 +574,28 @@ __global__ __launch_bounds__(CMP_THREADS) void k_compact_write(uint32_t n_scans,
         en += isnew[j];
     }
     __syncthreads();
+    if constexpr (FUSED) {
+        // the per-scan cells become (sample prefix relative to the brick | absolute span position):
+        // the totals cell at n_scans (zero until now) receives (samples | span end), and k_spans
+        // finds a run's span position with one gather
+        for (uint32_t k = grp; k < nh; k += CMP_THREADS / CMP_GROUP) {
+            uint4* cp = const_cast<uint4*>(cell_row<true>(T, s_h[k]));
+            uint32_t cs = 0, cp_ = s_n[k];
+            for (uint32_t q0 = 0; q0 < nq; q0 += CMP_GROUP) {
+                const uint32_t q = q0 + li;
+                uint4 v = q < nq ? cp[q] : make_uint4(0u, 0u, 0u, 0u);
+                const uint32_t s2 = v.x + v.z, p2 = v.y + v.w;
+                static_assert(CMP_GROUP == 16, "a cell row pass is one 16-lane DPP row");
+                const uint32_t is = row16_incl_scan(s2), ip = row16_incl_scan(p2);
+                const uint32_t ps = cs + is - s2, pp = cp_ + ip - p2;
+                v = make_uint4(ps, pp, ps + v.x, pp + v.y);
+                if (q < nq) cp[q] = v;
+                cs += __shfl(is, CMP_GROUP - 1, CMP_GROUP);
+                cp_ += __shfl(ip, CMP_GROUP - 1, CMP_GROUP);
+            }
+        }
+        return;
+    }
     // the per-scan cells become absolute sample positions: segment start + exclusive prefix
     // (k_place then finds a run's position with one gather)
     for (uint32_t k = grp; k < nh; k += CMP_THREADS / CMP_GROUP) {
@@ -959,11 +996,13 @@ hipError_t launch_count(const float* d_xyz, const BatchRef& D, const RayConst& R
 }
 
 hipError_t launch_compact(const BatchRef& D, const Table& T, const Work& Wk, Globals* G,
-                          int parity, hipStream_t st) {
+                          int parity, bool fused, hipStream_t st) {
     const uint32_t nch = (uint32_t)compact_chunks(T.mask + 1);
-    k_compact_sum<<<nch, CMP_THREADS, 0, st>>>(D.n_scans, T, Wk);
-    k_compact_scan<<<1, CMP_SCAN_THREADS, 0, st>>>(nch, Wk, G, parity);
-    k_compact_write<<<nch, CMP_THREADS, 0, st>>>(D.n_scans, nch, T, Wk, G, parity);
+    if (fused) k_compact_sum<true><<<nch, CMP_THREADS, 0, st>>>(D.n_scans, T, Wk);
+    else k_compact_sum<false><<<nch, CMP_THREADS, 0, st>>>(D.n_scans, T, Wk);
+    k_compact_scan<<<1, CMP_SCAN_THREADS, 0, st>>>(nch, Wk, G, parity, fused ? 1 : 0);
+    if (fused) k_compact_write<true><<<nch, CMP_THREADS, 0, st>>>(D.n_scans, nch, T, Wk, G, parity);
+    else k_compact_write<false><<<nch, CMP_THREADS, 0, st>>>(D.n_scans, nch, T, Wk, G, parity);
     return hipGetLastError();
 }
 

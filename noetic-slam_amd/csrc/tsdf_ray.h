@@ -146,6 +146,23 @@ __device__ __forceinline__ bool ray_step(RayState& r) {
     return true;
 }
 
+// ray_step without the early return: the state advances only when the step is taken, with selects
+// (for the single walk's unrolled loop, where every branch would split the wave's exec mask)
+__device__ __forceinline__ bool ray_step_sel(RayState& r) {
+    const bool mx = (r.tnx < r.tny) && (r.tnx < r.tnz);
+    const bool my = !mx && (r.tny < r.tnz);
+    const bool mz = !mx && !my;
+    const float t = mx ? r.tnx : (my ? r.tny : r.tnz);
+    const bool adv = t <= r.t1i;
+    r.tnx = (mx && adv) ? r.tnx + r.tdx : r.tnx;
+    r.tny = (my && adv) ? r.tny + r.tdy : r.tny;
+    r.tnz = (mz && adv) ? r.tnz + r.tdz : r.tnz;
+    r.vx += (mx && adv) ? r.sx : 0;
+    r.vy += (my && adv) ? r.sy : 0;
+    r.vz += (mz && adv) ? r.sz : 0;
+    return adv;
+}
+
 // ------------------------------------------------------------------------------------------------
 // Voxblox ray model (TSDF_SEM_VOXBLOX; the bit-exact twin of oracle/tsdf_oracle.c walk_ray_vb,
 // which restates voxblox SimpleTsdfIntegrator / RayCaster / updateTsdfVoxel — DESIGN.md §2b)
@@ -266,6 +283,24 @@ __device__ __forceinline__ bool vb_step(VbState& r) {
     return true;
 }
 
+// vb_step with selects (see ray_step_sel)
+__device__ __forceinline__ bool vb_step_sel(VbState& r) {
+    const bool adv = r.rem > 0;
+    r.rem -= adv ? 1 : 0;
+    const bool y0 = r.tny < r.tnx;
+    const float m01 = y0 ? r.tny : r.tnx;
+    const bool mz = (r.tnz < m01) && adv;
+    const bool my = y0 && !(r.tnz < m01) && adv;
+    const bool mx = !y0 && !(r.tnz < m01) && adv;
+    r.tnx = mx ? r.tnx + r.tdx : r.tnx;
+    r.tny = my ? r.tny + r.tdy : r.tny;
+    r.tnz = mz ? r.tnz + r.tdz : r.tnz;
+    r.vx += mx ? r.sx : 0;
+    r.vy += my ? r.sy : 0;
+    r.vz += mz ? r.sz : 0;
+    return adv;
+}
+
 // The ray model of each semantics, as one interface for the walk kernels (k_count / k_place).
 template <int SEM>
 struct Walk;
@@ -296,6 +331,7 @@ struct Walk<0> {  // TSDF_SEM_VDBFUSION
         return m < VOX_LIMIT - R.band_vox;
     }
     __device__ static __forceinline__ bool step(State& r) { return ray_step(r); }
+    __device__ static __forceinline__ bool step_sel(State& r) { return ray_step_sel(r); }
 };
 
 template <>
@@ -324,6 +360,7 @@ struct Walk<1> {  // TSDF_SEM_VOXBLOX
         return m < VOX_LIMIT - R.band_vox;
     }
     __device__ static __forceinline__ bool step(State& r) { return vb_step(r); }
+    __device__ static __forceinline__ bool step_sel(State& r) { return vb_step_sel(r); }
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -457,6 +494,7 @@ struct Walk<2> {  // TSDF_SEM_VDBFUSION_F64
         return m < VOX_LIMIT - R.band_vox;
     }
     __device__ static __forceinline__ bool step(State& r) { return ray_step(r); }
+    __device__ static __forceinline__ bool step_sel(State& r) { return ray_step_sel(r); }
 };
 
 __device__ __forceinline__ uint64_t pack_brick(int bx, int by, int bz) {

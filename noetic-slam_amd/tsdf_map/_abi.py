@@ -16,7 +16,7 @@ STATUS_NAMES = {
     TSDF_EHIP: "TSDF_EHIP", TSDF_ENODEV: "TSDF_ENODEV", TSDF_EOVERFLOW: "TSDF_EOVERFLOW",
 }
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 TILE_WORDS = 1028  # TSDF_TILE_WORDS: u32 words of one border-brick tile
 MAX_WORLD = 64
 SEM_VDBFUSION = 0
@@ -25,7 +25,10 @@ SEM_VDBFUSION_F64 = 2
 SEMANTICS = {"vdbfusion": SEM_VDBFUSION, "voxblox": SEM_VOXBLOX,
              "vdbfusion_f64": SEM_VDBFUSION_F64}
 
-KERNEL_KINDS = ("count", "compact", "place", "integrate")  # k_<kind>, KernelKind order
+# k_<kind>, KernelKind order: the two-walk front end (count, place) or the single walk (walk, spans)
+KERNEL_KINDS = ("count", "compact", "place", "integrate", "walk", "spans")
+WALK_TWO = 0     # tsdf_params.walk: k_count + k_place (default)
+WALK_SINGLE = 1  # k_walk + k_spans when the band allows it
 
 
 class TsdfParams(C.Structure):
@@ -53,6 +56,8 @@ class TsdfParams(C.Structure):
         ("sector", C.c_uint32),
         ("sector_yaw0", C.c_double),
         ("max_bricks_hard", C.c_uint64),
+        # ABI v5
+        ("walk", C.c_int32),
     ]
 
 
@@ -163,6 +168,7 @@ def default_params(lib=None, **kw):
         p.device_id, p.brick_side, p.max_batch = 0, BRICK_SIDE, 32
         p.semantics, p.allow_clear, p.use_weight_dropoff, p.max_weight = SEM_VDBFUSION, 1, 1, 1e4
         p.n_sectors, p.sector, p.sector_yaw0, p.max_bricks_hard = 0, 0, 0.0, 0
+        p.walk = WALK_TWO
     for k, v in kw.items():
         if not hasattr(p, k):
             raise TypeError("unknown tsdf_params field %r" % k)

@@ -55,7 +55,7 @@ class TSDFVolume:
                  max_range=math.inf, max_bricks=1 << 20, max_points=1 << 18, device_id=0,
                  max_batch=32, pipeline=False, semantics="vdbfusion", allow_clear=True,
                  use_weight_dropoff=True, max_weight=10000.0, n_sectors=0, sector=0,
-                 sector_yaw0=0.0, max_bricks_hard=0):
+                 sector_yaw0=0.0, max_bricks_hard=0, walk="two"):
         self._lib = lib
         if semantics not in _abi.SEMANTICS:
             raise ValueError("semantics must be one of %s" % sorted(_abi.SEMANTICS))
@@ -79,6 +79,9 @@ class TSDFVolume:
         p.sector = int(sector)
         p.sector_yaw0 = float(sector_yaw0)
         p.max_bricks_hard = int(max_bricks_hard)
+        # "two": k_count + k_place (default); "single": rays walked once (k_walk + k_spans) when the
+        # band allows it
+        p.walk = {"two": _abi.WALK_TWO, "single": _abi.WALK_SINGLE}[walk]
         self.params = p
         self.semantics = semantics
         rc = lib.tsdf_create(C.byref(p), C.byref(self._ctx))

@@ -125,13 +125,19 @@ def test_large_batches_bitwise(sim):
     assert bitwise(g, o)
 
 
-def test_sector_sample_list_grows(sim):
-    """A sharded context sizes its sample list for 1 / n_sectors of the rays; scans whose points
-    all lie in its sector overflow it, and it grows (OVF_SMP) without losing an update."""
+@pytest.mark.parametrize("walk", ["two", "single"])
+def test_sector_sample_list_grows(sim, walk):
+    """A sharded context sizes its sample list (single walk: its k_walk regions) for 1 / n_sectors
+    of the rays; scans whose points all lie in its sector overflow it, and it grows (OVF_SMP)
+    without losing an update."""
     import torch
     from tsdf_map import sector_ids
+    # two walks: 819 k sample slots for 8 x 2^15 points; single walk: 1184 regions of 512 rays for
+    # 64 x 2^15 points, while the 64 scans' sector-0 points fill ~2200 of them
+    n, kw = (6, dict(max_batch=8, max_points=1 << 15)) if walk == "two" else \
+        (64, dict(max_batch=64, max_points=1 << 15))
     scans = []
-    for k in range(6):
+    for k in range(n):
         p, o = sim.scan(k)
         p = p[sector_ids(p, o, 8, 0.0) == 0]
         scans.append((np.ascontiguousarray(p), o))
@@ -140,7 +146,7 @@ def test_sector_sample_list_grows(sim):
     org = np.stack([o for _, o in scans])
     d = torch.from_numpy(allp).to("cuda:0")
     torch.cuda.synchronize()
-    g = hip(max_batch=8, n_sectors=8, sector=0, max_points=1 << 15)  # 819 k sample slots
+    g = hip(n_sectors=8, sector=0, walk=walk, **kw)
     g.integrate_batch_device(d.data_ptr(), offs, org)
     g.sync()
     assert g.stats()["n_grows"] >= 1
