@@ -147,6 +147,43 @@ __global__ __launch_bounds__(CNT_THREADS) void k_count(const float* __restrict__
 #else
             if (ok) {
 #endif
+#ifndef TSDF_CNT_BRANCHY
+                // Branch-free walk (lanes are at different steps of different rays): the gate and
+                // the pair bookkeeping are selects on 32-bit brick codes; the 64-bit keys are built
+                // from the codes after the walk (code_key: a ray's bricks lie within one brick of
+                // its first one per axis).
+                const int bx0 = r.vx >> 3, by0 = r.vy >> 3, bz0 = r.vz >> 3;
+                uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0, curc = ~0u, ccount = 0;
+                auto walk = [&](auto chk) {
+                    for (int it = 0; it < MAX_DDA_STEPS; it++) {
+                        const bool g = Walk<SEM>::gate_sel(R, ox, oy, oz, r, decltype(chk)::value);
+                        const uint32_t bc = brick_code_of(r.vx, r.vy, r.vz);
+                        const bool nb = g && bc != curc;
+                        const bool cl = nb && curc != ~0u;  // the previous pair closes
+                        c0 = (cl && np == 0) ? curc : c0; n0 = (cl && np == 0) ? ccount : n0;
+                        c1 = (cl && np == 1) ? curc : c1; n1 = (cl && np == 1) ? ccount : n1;
+                        c2 = (cl && np == 2) ? curc : c2; n2 = (cl && np == 2) ? ccount : n2;
+                        c3 = (cl && np == 3) ? curc : c3; n3 = (cl && np == 3) ? ccount : n3;
+                        np += cl ? 1u : 0u;
+                        curc = nb ? bc : curc;
+                        ccount = (nb ? 0u : ccount) + (g ? 1u : 0u);
+                        if (!Walk<SEM>::step(r)) break;
+                    }
+                };
+                if (__all(Walk<SEM>::inside(R, r))) walk(std::false_type{});
+                else walk(std::true_type{});
+                if (curc != ~0u) {
+                    c0 = np == 0 ? curc : c0; n0 = np == 0 ? ccount : n0;
+                    c1 = np == 1 ? curc : c1; n1 = np == 1 ? ccount : n1;
+                    c2 = np == 2 ? curc : c2; n2 = np == 2 ? ccount : n2;
+                    c3 = np == 3 ? curc : c3; n3 = np == 3 ? ccount : n3;
+                    np++;
+                }
+                if (np > 0) q0 = code_key(c0, bx0, by0, bz0);
+                if (np > 1) q1 = code_key(c1, bx0, by0, bz0);
+                if (np > 2) q2 = code_key(c2, bx0, by0, bz0);
+                if (np > 3) q3 = code_key(c3, bx0, by0, bz0);
+#else
                 uint64_t cur = EMPTY_KEY;
                 uint32_t curc = ~0u, ccount = 0;
                 // a pair boundary is a brick-code change (32-bit); the full key is built per pair
@@ -181,6 +218,7 @@ __global__ __launch_bounds__(CNT_THREADS) void k_count(const float* __restrict__
                     q3 = np == 3 ? cur : q3; n3 = np == 3 ? ccount : n3;
                     np++;
                 }
+#endif
             }
             if (np > maxp) atomicOr(&C->ovf, OVF_PAIRS);  // beyond the geometric bound
             k = min(np, maxp);

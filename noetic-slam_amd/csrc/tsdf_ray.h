@@ -128,6 +128,26 @@ __device__ __forceinline__ bool voxel_gate(const RayConst& R, float ox, float oy
     return __builtin_sqrtf(d2) < R.tau;  // -dist > -tau
 }
 
+// voxel_gate without early exits (same verdict, bit for bit): the squared distance is always formed
+// and only the rare near-tau case (|d2 - tau^2| within 2^-20) takes the sqrt, in a branch the wave
+// skips when none of its lanes needs it.
+__device__ __forceinline__ bool voxel_gate_sel(const RayConst& R, float ox, float oy, float oz,
+                                               const RayState& r, bool check = true) {
+    const bool inl = !check || (r.vx > -VOX_LIMIT && r.vx < VOX_LIMIT && r.vy > -VOX_LIMIT &&
+                                r.vy < VOX_LIMIT && r.vz > -VOX_LIMIT && r.vz < VOX_LIMIT);
+    const float cx = ((float)r.vx + 0.5f) * R.vs;
+    const float cy = ((float)r.vy + 0.5f) * R.vs;
+    const float cz = ((float)r.vz + 0.5f) * R.vs;
+    const float ax = cx - ox, ay = cy - oy, az = cz - oz;
+    const float bx = r.px - cx, by = r.py - cy, bz = r.pz - cz;
+    const float proj = ax * bx + ay * by + az * bz;
+    const float d2 = bx * bx + by * by + bz * bz;
+    bool behind = d2 < R.tau2_lo;  // dist < tau, so -dist > -tau
+    const bool near = !behind && d2 <= R.tau2_hi;
+    if (near) behind = __builtin_sqrtf(d2) < R.tau;
+    return inl && (proj > 0.0f || (proj < 0.0f && behind));
+}
+
 // One DDA step (math::MinIndex tie-break: equal entries resolve to the higher axis).
 // Returns false when the next entry time is past the band end.
 // Written with selects only: an axis index would make hipcc spill the state to scratch.
@@ -316,6 +336,10 @@ struct Walk<0> {  // TSDF_SEM_VDBFUSION
                                                 const State& r, bool check = true) {
         return voxel_gate(R, ox, oy, oz, r, check);
     }
+    __device__ static __forceinline__ bool gate_sel(const RayConst& R, float ox, float oy, float oz,
+                                                    const State& r, bool check = true) {
+        return voxel_gate_sel(R, ox, oy, oz, r, check);
+    }
     __device__ static __forceinline__ bool sample(const RayConst& R, float ox, float oy, float oz,
                                                   const State& r, float& s, bool check = true) {
         return voxel_sample(R, ox, oy, oz, r, s, check);
@@ -343,6 +367,11 @@ struct Walk<1> {  // TSDF_SEM_VOXBLOX
     }
     __device__ static __forceinline__ bool gate(const RayConst& R, float ox, float oy, float oz,
                                                 const State& r, bool check = true) {
+        float s;
+        return vb_sample(R, ox, oy, oz, r, s, check);
+    }
+    __device__ static __forceinline__ bool gate_sel(const RayConst& R, float ox, float oy, float oz,
+                                                    const State& r, bool check = true) {
         float s;
         return vb_sample(R, ox, oy, oz, r, s, check);
     }
@@ -466,6 +495,13 @@ struct Walk<2> {  // TSDF_SEM_VDBFUSION_F64
         if (!(proj < 0.0)) return false;
         return d2 < R.gate_d2;  // (float)sqrt(d2) < tau, i.e. -dist > -tau
     }
+    __device__ static __forceinline__ bool gate_sel(const RayConst& R, float, float, float,
+                                                    const State& r, bool check = true) {
+        const bool inl = !check || vdb_inside(r);
+        double proj, d2;
+        vdb_geom(R, r, proj, d2);
+        return inl && (proj > 0.0 || (proj < 0.0 && d2 < R.gate_d2));
+    }
     __device__ static __forceinline__ bool sample(const RayConst& R, float, float, float,
                                                   const State& r, float& s, bool check = true) {
         if (check && !vdb_inside(r)) return false;
@@ -512,6 +548,18 @@ __device__ __forceinline__ uint64_t brick_key_of(int vx, int vy, int vz) {
 __device__ __forceinline__ uint32_t brick_code_of(int vx, int vy, int vz) {
     return ((uint32_t)(vx >> 3) & 1023u) | (((uint32_t)(vy >> 3) & 1023u) << 10) |
            (((uint32_t)(vz >> 3) & 1023u) << 20);
+}
+
+// The full key of a pair from its brick code and the ray's first brick: a ray's bricks lie within
+// 511 bricks of each other per axis (in practice within one), so the truncated difference is exact.
+__device__ __forceinline__ int code_axis(uint32_t c, int b0) {
+    const int d = (int)((c - (uint32_t)b0) & 1023u);
+    return b0 + ((d << 22) >> 22);
+}
+
+__device__ __forceinline__ uint64_t code_key(uint32_t code, int bx0, int by0, int bz0) {
+    return pack_brick(code_axis(code & 1023u, bx0), code_axis((code >> 10) & 1023u, by0),
+                      code_axis((code >> 20) & 1023u, bz0));
 }
 
 __device__ __forceinline__ uint64_t mix64(uint64_t k) {

@@ -62,18 +62,6 @@ __device__ __forceinline__ int lds_insert_full(unsigned long long* s_key, uint64
     }
 }
 
-// Brick of a pair from its 10-bit-per-axis code and the ray's first brick (a ray's bricks lie
-// within one brick of each other per axis, so the truncated difference is exact).
-__device__ __forceinline__ int code_axis(uint32_t c, int b0) {
-    const int d = (int)((c - (uint32_t)b0) & 1023u);
-    return b0 + ((d << 22) >> 22);
-}
-
-__device__ __forceinline__ uint64_t pair_key(uint32_t code, int bx0, int by0, int bz0) {
-    return pack_brick(code_axis(code & 1023u, bx0), code_axis((code >> 10) & 1023u, by0),
-                      code_axis((code >> 20) & 1023u, bz0));
-}
-
 static_assert(WLK_THREADS * 4 <= HCAP, "a workgroup's pairs must fit its LDS brick hash");
 
 template <int SEM, int NSTEP>
@@ -175,7 +163,7 @@ __global__ __launch_bounds__(WLK_THREADS) void k_walk(const float* __restrict__ 
     // pairs -> LDS hash: all lanes emit pair j together (convergent); e = slot | rank << 16
     uint32_t e0 = 0, e1 = 0, e2 = 0, e3 = 0;
     auto emit = [&](uint32_t code, uint32_t cnt) -> uint32_t {
-        const int lid = lds_insert_full(s_key, pair_key(code, bx0, by0, bz0));
+        const int lid = lds_insert_full(s_key, code_key(code, bx0, by0, bz0));
         const uint32_t lr = atomicAdd(&s_cnt[lid], cnt);
         return (uint32_t)lid | (lr << 16);
     };

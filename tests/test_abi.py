@@ -62,6 +62,18 @@ def test_default_params_roundtrip():
     p = _abi.default_params(lib)
     assert p.voxel_size == 0.05 and p.sdf_trunc == 0.15 and p.brick_side == 8
     assert p.space_carving == 0 and np.isinf(p.max_range)
+    assert p.walk == _abi.WALK_TWO == 0  # ABI v5: two walks unless the single walk is asked for
+    # the ctypes mirror ends where the C struct ends (ABI v5 appended `walk`)
+    assert _abi.TsdfParams._fields_[-1][0] == "walk"
+
+
+def test_header_kernel_kinds_match_the_binding():
+    """TSDF_K_* of the header name the binding's KERNEL_KINDS (k_<kind>) in order."""
+    import re
+    from tsdf_map import _abi
+    hdr = open(os.path.join(REPO, "include", "tsdf_hip.h")).read()
+    kinds = {int(v): k.lower() for k, v in re.findall(r"#define TSDF_K_(\w+) (\d+)", hdr)}
+    assert [kinds[i] for i in range(len(kinds))] == list(_abi.KERNEL_KINDS)
 
 
 @pytest.mark.skipif(os.path.exists("/dev/kfd") and os.access("/dev/kfd", os.R_OK),

@@ -62,7 +62,8 @@ def test_decimated_scan_bitwise(scan0):
 
 
 def test_full_c1_scan_bitwise(scan0):
-    """C1: one full 128x1024 synthetic Ouster scan, identity pose, 5 cm / 15 cm."""
+    """C1: one full 128x1024 synthetic Ouster scan (the trajectory's first pose: origin (8, 0, 0),
+    yaw pi/2), 5 cm / 15 cm."""
     g, o = run_both([scan0])
     n = assert_bitwise(g, o)
     st = g.stats()
@@ -178,12 +179,15 @@ def test_repeatability_bitwise(scan0):
 
 
 def test_c4_dense_2048_2cm():
-    """C4 geometry: OS-1-128 2048-column beams, 2 cm voxels, 6 cm truncation."""
+    """C4 as configured: full OS-1-128 2048-column scans (262,144 points each), 2 cm voxels, 6 cm
+    truncation, 20 Hz trajectory, two consecutive scans."""
     from tsdf_map.scan_gen import OusterSim
     sim4 = OusterSim("os1_128_2048", hz=20.0)
-    pts, org = sim4.scan(0)
-    g, o = run_both([(decimate(pts, 2), org)], voxel_size=0.02, sdf_trunc=0.06)
-    assert_bitwise(g, o)
+    scans = [sim4.scan(0), sim4.scan(1)]
+    assert scans[0][0].shape[0] == 128 * 2048
+    g, o = run_both(scans, voxel_size=0.02, sdf_trunc=0.06, max_points=1 << 19,
+                    max_bricks=1 << 21)
+    assert assert_bitwise(g, o) > 2_000_000
 
 
 def test_long_runs_unpacked_cells(scan0):
