@@ -692,6 +692,14 @@ __global__ __launch_bounds__(PLC_THREADS) void k_place(const float* __restrict__
     unsigned long long pt[6];
     if (threadIdx.x == 0) pt[0] = clock64();
 #endif
+#ifdef TSDF_ABLATE_PL_EMPTY  // diagnostic build: the workgroups' dispatch and LDS allocation only
+    if (threadIdx.x < 2 && D.n_scans == 0xFFFFFFFFu) {
+        s_base[threadIdx.x] = 0u; s_loff[threadIdx.x] = 0; s_ord[threadIdx.x] = 0;
+        s_bits[threadIdx.x] = 0u; s_wpre[threadIdx.x] = 0; st_s[threadIdx.x] = 0.0f;
+        st_l[threadIdx.x] = 0; s_nst = 0u;
+    }
+    return;
+#endif
     // workgroup 2 b + hf takes half hf of k_count block b's rays, and that half's run list
     // (sector sharding: block b is the (w / 2)-th of k_sector_flags' list, the rest leave)
     uint32_t wb = blockIdx.x;
@@ -758,6 +766,9 @@ __global__ __launch_bounds__(PLC_THREADS) void k_place(const float* __restrict__
     __syncthreads();
 #ifdef TSDF_PLC_PHASE
     if (threadIdx.x == 0) pt[2] = clock64();
+#endif
+#ifdef TSDF_ABLATE_PL_PROLOGUE  // diagnostic build: the prologue (loads, run tables) only
+    if (D.n_scans != 0xFFFFFFFFu) return;
 #endif
     if (threadIdx.x < 64) {  // exclusive prefix of run starts per bitmap word (one wave)
         constexpr int WPL = (PLC_WORDS + 63) / 64;
