@@ -14,9 +14,14 @@
 #include <cstdarg>
 #include <cstddef>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/tsdf_hip.h"
@@ -86,6 +91,61 @@ struct EventTimer final : KernelTimer {
     ~EventTimer() override {
         for (auto& r : pending) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
         for (auto e : free_ev) (void)hipEventDestroy(e);
+    }
+};
+
+// Host staging of tsdf_integrate's PointCloud2 records (the node's per-scan call): the record ->
+// packed-xyz loop of a large scan is split over a few persistent threads (the caller's thread takes
+// the first chunk).  One context is used by one thread at a time, so one pool per context.
+struct PackPool {
+    std::vector<std::thread> th;
+    std::mutex m;
+    std::condition_variable go, done;
+    std::function<void(int)> job;
+    uint64_t gen = 0;
+    int busy = 0;
+    bool stop = false;
+
+    explicit PackPool(int workers) {
+        for (int w = 0; w < workers; w++)
+            th.emplace_back([this, w] {
+                uint64_t seen = 0;
+                for (;;) {
+                    std::function<void(int)> f;
+                    {
+                        std::unique_lock<std::mutex> l(m);
+                        go.wait(l, [&] { return stop || gen != seen; });
+                        if (stop) return;
+                        seen = gen;
+                        f = job;
+                    }
+                    f(w + 1);
+                    std::lock_guard<std::mutex> l(m);
+                    if (--busy == 0) done.notify_one();
+                }
+            });
+    }
+    int parts() const { return (int)th.size() + 1; }
+    // f(part) for part = 0 .. parts() - 1, part 0 on the calling thread
+    void run(const std::function<void(int)>& f) {
+        {
+            std::lock_guard<std::mutex> l(m);
+            job = f;
+            busy = (int)th.size();
+            gen++;
+        }
+        go.notify_all();
+        f(0);
+        std::unique_lock<std::mutex> l(m);
+        done.wait(l, [&] { return busy == 0; });
+    }
+    ~PackPool() {
+        {
+            std::lock_guard<std::mutex> l(m);
+            stop = true;
+        }
+        go.notify_all();
+        for (auto& t : th) t.join();
     }
 };
 
@@ -192,6 +252,7 @@ struct tsdf_ctx {
     uint64_t metrics_next = 0;  // the next batch id to report
     struct BatchInfo { uint64_t id; uint32_t scans; uint64_t points; };
     std::vector<BatchInfo> metrics_info;  // host-side facts of the batches not yet reported
+    PackPool* pack = nullptr;  // host staging threads (tsdf_integrate of strided records)
     uint64_t n_grows = 0, n_replayed = 0;
 };
 
@@ -819,6 +880,7 @@ void tsdf_destroy(tsdf_ctx* c) {
     }
     if (c->metrics) fclose(c->metrics);
     delete c->timer;
+    delete c->pack;
     void* dev[] = {c->T.keys,        c->T.slots,
                    c->T.touched,
                    c->T.brick_keys,  c->Pl.sdf,          c->Pl.weight,     c->G,
@@ -973,6 +1035,19 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
         HIPCHK(c, hipMalloc(&c->stage2[q], c->batch_points * 3 * sizeof(float)));
     }
     HIPCHK(c, hipMalloc(&c->G, sizeof(Globals)));
+    {
+        // host staging threads: 3 workers + the caller (TSDF_PACK_THREADS overrides; 1 = none)
+        int nt = 4;
+        if (const char* e = std::getenv("TSDF_PACK_THREADS")) nt = std::max(1, std::atoi(e));
+        nt = std::min<int>(nt, (int)std::max(1u, std::thread::hardware_concurrency()));
+        if (nt > 1) {
+            try {
+                c->pack = new PackPool(nt - 1);
+            } catch (...) {  // no threads: the caller's thread stages alone
+                c->pack = nullptr;
+            }
+        }
+    }
     HIPCHK(c, hipHostMalloc(&c->h_ring, tsdf_ctx::RING * (MAX_BATCH + 1) * sizeof(ScanRec),
                             hipHostMallocDefault));
     HIPCHK(c, hipMalloc(&c->d_ring, tsdf_ctx::RING * (MAX_BATCH + 1) * sizeof(ScanRec)));
@@ -1062,17 +1137,25 @@ int tsdf_integrate(tsdf_ctx* c, const void* pts, uint64_t n, uint32_t point_step
     if (!xyz_is_f64 && point_step == 12 && xyz_offset == 0) {
         std::memcpy(h, base, n * 12);
     } else {
-        for (uint64_t i = 0; i < n; i++) {
-            const char* q = base + i * point_step + xyz_offset;
-            if (xyz_is_f64) {
-                double d[3];
-                std::memcpy(d, q, sizeof d);
-                h[3 * i] = (float)d[0];
-                h[3 * i + 1] = (float)d[1];
-                h[3 * i + 2] = (float)d[2];
-            } else {
-                std::memcpy(h + 3 * i, q, 12);
+        auto pack = [&](uint64_t i0, uint64_t i1) {
+            for (uint64_t i = i0; i < i1; i++) {
+                const char* q = base + i * point_step + xyz_offset;
+                if (xyz_is_f64) {
+                    double d[3];
+                    std::memcpy(d, q, sizeof d);
+                    h[3 * i] = (float)d[0];
+                    h[3 * i + 1] = (float)d[1];
+                    h[3 * i + 2] = (float)d[2];
+                } else {
+                    std::memcpy(h + 3 * i, q, 12);
+                }
             }
+        };
+        if (c->pack && n >= (1u << 15)) {
+            const uint64_t parts = (uint64_t)c->pack->parts();
+            c->pack->run([&](int k) { pack(n * k / parts, n * (k + 1) / parts); });
+        } else {
+            pack(0, n);
         }
     }
     BatchDesc& D = c->pend;
