@@ -45,6 +45,10 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="threads of the multi-threaded oracle leg (capped by the CPU affinity set; "
                          "16 = one GPU's CPU share on the box)")
+    ap.add_argument("--cpu-threads-full", type=int, default=0,
+                    help="also time the oracle on this many threads (0: off; the box's rules size "
+                         "worker pools to one GPU's 16-core share, so the whole host is projected, "
+                         "not run)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--pipeline", action="store_true",
                     help="overlap consecutive batches on two HIP streams (tsdf_params.pipeline); "
@@ -55,8 +59,11 @@ def parse():
     ap.add_argument("--hz", type=float, default=10.0)
     ap.add_argument("--max-bricks", type=int, default=1 << 20,
                     help="brick pool capacity (4 KiB per brick)")
-    ap.add_argument("--semantics", default="vdbfusion", choices=("vdbfusion", "voxblox", "vdbfusion_f64"),
-                    help="fusion rule (tsdf_params.semantics); the headline metric is vdbfusion")
+    ap.add_argument("--semantics", default="vdbfusion_f64",
+                    choices=("vdbfusion", "voxblox", "vdbfusion_f64"),
+                    help="fusion rule (tsdf_params.semantics); the headline is vdbfusion_f64, "
+                         "VDBFusion at upstream's own precisions (the mode that meets SURVEY §8c's "
+                         "per-voxel bar against literal VDBFusion, DESIGN.md §2c)")
     ap.add_argument("--rank-rehearsal", type=int, default=0, metavar="N",
                     help="one process plays rank 0 of an N-GPU run (sector 0 of N, N x batch full "
                          "scans per step): its time per step is one rank's; value = N x batch "
@@ -72,16 +79,57 @@ def parse():
     return ap.parse_args()
 
 
+def launch_ranks(n, script=None, argv=None):
+    """`bench.py --gpus N` without a launcher (no WORLD_SIZE in the environment): start N rank
+    processes of this script, one per GPU, before this process touches any GPU, and exit with
+    their status.  Rank 0 prints the JSON line.  If a rank fails, the others are stopped (by their
+    PIDs) so no rank waits forever at a barrier."""
+    import signal
+    import socket
+    import subprocess
+
+    with socket.socket() as sk:  # a free rendezvous port on the loopback interface
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        cmd = [sys.executable, script or os.path.abspath(__file__)]
+        procs.append(subprocess.Popen(cmd + list(sys.argv[1:] if argv is None else argv), env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                for q in live:
+                    q.send_signal(signal.SIGTERM)
+        time.sleep(0.05)
+    return rc
+
+
+def check_world(n_gpus, world):
+    """The printed line's n_gpus must be the ranks that actually ran."""
+    if n_gpus != world:
+        raise SystemExit("refusing to report n_gpus=%d from a world of %d rank(s)" % (n_gpus, world))
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and world > 1:
-        raise SystemExit("--gpus %d but WORLD_SIZE %d" % (args.gpus, world))
+    check_world(args.gpus, world)
     # TSDF_BENCH_SHARED_GPU=1 (rehearsal only, never the driver's runs): every rank on device
     # local % device_count, collectives over gloo on host tensors -- exercises the N-rank path
     # (sector sharding, max-over-ranks timing, read-out merge) on a one-GPU box
@@ -154,10 +202,15 @@ def main():
     elapsed = time.perf_counter() - t0
     st = vol.stats()
 
+    # every rank's time (reported), the step time is the slowest rank's
     el = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
     if world > 1:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    elapsed = float(el.item())
+        all_el = [torch.zeros_like(el) for _ in range(world)]
+        dist.all_gather(all_el, el)
+        rank_elapsed = [float(t.item()) for t in all_el]
+    else:
+        rank_elapsed = [elapsed]
+    elapsed = max(rank_elapsed)
     total_scans = args.steps * scans_per_step
     value = total_scans / elapsed
 
@@ -244,16 +297,29 @@ def main():
         threads = max(1, min(args.cpu_threads, share or 1))
         n_mt, t_mt = oracle_leg(threads)
         n_1, t_1 = oracle_leg(1)
+        host = os.cpu_count() or 1
         cpu = {"value": round(n_mt / t_mt, 4), "unit": "scans/s", "cores": threads, "kind": "port",
-               "host_nproc": os.cpu_count(), "affinity_cpus": share,
+               "host_nproc": host, "affinity_cpus": share,
                "sample": "the first %d scans of the timed steps (%.1f s), C oracle in its partitioned "
-                         "multi-threaded scan-fused mode (%d threads), same inputs"
-                         % (n_mt, t_mt, threads),
+                         "multi-threaded scan-fused mode (%d threads: one GPU's CPU share of the "
+                         "box), same inputs, same semantics" % (n_mt, t_mt, threads),
                "serial": {"value": round(n_1 / t_1, 4), "cores": 1,
-                          "sample": "the first %d scans (%.1f s), serial scan-fused oracle"
-                                    % (n_1, t_1)}}
+                          "sample": "the first %d scans (%.1f s), serial scan-fused oracle "
+                                    "(VDBFusion's serial Integrate loop)" % (n_1, t_1)},
+               # the whole host at the measured per-thread rate of the share leg (linear scaling:
+               # an upper bound for the CPU); not run, the box's rules size worker pools to 16
+               "full_host_projection": {"value": round(n_mt / t_mt * host / threads, 2),
+                                        "cores": host,
+                                        "note": "share-leg rate x host_nproc / cores (perfect "
+                                                "scaling assumed: an upper bound, not a run)"}}
+        if args.cpu_threads_full > 0:
+            tf = min(args.cpu_threads_full, share or 1)
+            n_f, t_f = oracle_leg(tf)
+            cpu["full"] = {"value": round(n_f / t_f, 4), "cores": tf,
+                           "sample": "the first %d scans (%.1f s), %d threads" % (n_f, t_f, tf)}
 
     if rank == 0:
+        check_world(args.gpus, world)
         out = {
             "metric": "scans/sec TSDF integration (128x1024 pts, 5 cm voxel)",
             "value": round(value, 2),
@@ -262,10 +328,12 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "rank_ms_per_step": [round(e / args.steps * 1e3, 4) for e in rank_elapsed],
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": {"vdbfusion": "f32", "voxblox": "f32",
+                      "vdbfusion_f64": "f64+f32"}[args.semantics],  # f64 SDF, f32 DDA (upstream's)
             "data": "synthetic (OS-1-128 1024x10 beam angles from the reference's metadata "
                     "fixture; analytic scene; resident in HBM)",
             "config": {"workload": ("C1/M1 ouster_os1_128_1024x10_synthetic_5cm"

@@ -76,7 +76,15 @@ __device__ __forceinline__ int lds_insert(unsigned long long* s_key, uint64_t ke
 constexpr int CNT_THREADS = TSDF_CNT_THREADS;
 
 template <int SEM>
-__global__ __launch_bounds__(CNT_THREADS) void k_count(const float* __restrict__ xyz, BatchRef D,
+// TSDF_SEM_VDBFUSION_F64: the fp32 filter's rare double branch would lift k_count to 93 VGPRs (5
+// waves per SIMD); the bound keeps the LDS-limited 6, spilling only inside that branch
+#ifndef TSDF_F64_COUNT_WAVES
+#define TSDF_F64_COUNT_WAVES 6
+#endif
+#ifndef TSDF_F64_PLACE_WAVES
+#define TSDF_F64_PLACE_WAVES 1
+#endif
+__global__ __launch_bounds__(CNT_THREADS, SEM == 2 ? TSDF_F64_COUNT_WAVES : 1) void k_count(const float* __restrict__ xyz, BatchRef D,
                                                       RayConst R, Table T, Work Wk, Globals* G,
                                                       int parity) {
     __shared__ unsigned long long s_key[HCAP];
@@ -676,7 +684,7 @@ constexpr int PLC_THREADS = RPB / 2;  // one ray per lane, half a k_count workgr
 constexpr int PLC_STAGE = TSDF_PLC_STAGE;  // staged samples per workgroup (6 B each; 4 workgroups per CU)
 
 template <int SEM>
-__global__ __launch_bounds__(PLC_THREADS) void k_place(const float* __restrict__ xyz, BatchRef D,
+__global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) void k_place(const float* __restrict__ xyz, BatchRef D,
                                                       RayConst R, Table T, Work Wk,
                                                       const Globals* __restrict__ G, int parity) {
     constexpr int PLC_WORDS = (PLC_STAGE + 31) / 32;

@@ -399,9 +399,42 @@ struct Walk<1> {  // TSDF_SEM_VOXBLOX
 // GetVoxelCenter / ComputeSDF in double (Eigen's x + (y + z) reductions).  No contraction; double
 // division and sqrt are IEEE (LLVM's correctly rounded f64 expansions).
 
+// A wave-uniform double, declared so (its halves through readfirstlane): the compiler then keeps it
+// in an SGPR pair instead of a VGPR pair.
+__device__ __forceinline__ double uniform_f64(double v) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
+// (float)sqrt(x) of a double x >= 0 (ComputeSDF's (float)dist, VDBFusion's depth): LLVM's correctly
+// rounded f64 sqrt sequence (v_rsq_f64 and two Newton-Raphson corrections; the hardware v_sqrt_f64
+// is only ~2^-25 accurate, profiles/tools/sqrt_check) without its input scaling, which acts only
+// below 2^-767: a nonzero squared distance is at least 2^-298 (p and the centre lie on the float
+// grid, |b| >= 2^-149), a nonzero depth^2 far above it.  x = 0 gives 0, as the sequence's class
+// check does.  RN_f of the correctly rounded double equals RN_f(sqrt(x)) (double rounding is
+// innocuous for sqrt at 53 >= 2 * 24 + 2 bits).
+__device__ __forceinline__ float vdb_sqrt_f(double x) {
+    const double r = __builtin_amdgcn_rsq(x);
+    double g = x * r, h = r * 0.5;
+    const double e = __builtin_fma(-h, g, 0.5);
+    g = __builtin_fma(g, e, g);
+    h = __builtin_fma(h, e, h);
+    double d = __builtin_fma(-g, g, x);
+    g = __builtin_fma(d, h, g);
+    d = __builtin_fma(-g, g, x);
+    g = __builtin_fma(d, h, g);
+    return x == 0.0 ? 0.0f : (float)g;
+}
+
 struct VdbState : RayState {
-    double pxd, pyd, pzd;  // the point
-    double oxd, oyd, ozd;  // the origin as given
+    double oxd, oyd, ozd;  // the origin as given (uniform over a k_count / k_place workgroup)
+    const ScanRec* sr;     // its scan record (k_count's filter re-reads the origin from it)
+    // k_count's fp32 filter of the double gate (vdb_gate_filtered): |proj_f - proj| <= ep and
+    // |d2_f - d2| <= e2 hold for every voxel with d2_f <= bchk (so |p - c| <= bn); glo / ghi are
+    // gate_d2 -/+ 2 e2
+    float ep, glo, ghi, bchk;
 };
 
 __device__ __forceinline__ void vdb_axis(float di, float inv, float pos, float t0i, int v,
@@ -424,13 +457,11 @@ __device__ __forceinline__ void vdb_axis(float di, float inv, float pos, float t
 __device__ __forceinline__ bool vdb_init(const RayConst& R, const BatchRef& D, uint32_t t,
                                          float px, float py, float pz, VdbState& r) {
     if (!in_sector(R, px - D.s[t].ox, py - D.s[t].oy)) return false;  // another GPU's azimuth sector
-    r.oxd = D.s[t].odx;
-    r.oyd = D.s[t].ody;
-    r.ozd = D.s[t].odz;
-    r.pxd = px;
-    r.pyd = py;
-    r.pzd = pz;
-    const double dx = r.pxd - r.oxd, dy = r.pyd - r.oyd, dz = r.pzd - r.ozd;
+    r.oxd = uniform_f64(D.s[t].odx);  // the workgroup's scan: keep the origin in SGPRs
+    r.oyd = uniform_f64(D.s[t].ody);
+    r.ozd = uniform_f64(D.s[t].odz);
+    r.sr = D.s + t;
+    const double dx = (double)px - r.oxd, dy = (double)py - r.oyd, dz = (double)pz - r.ozd;
     const float depth = (float)__builtin_sqrt(dx * dx + (dy * dy + dz * dz));  // direction.norm()
     if (!(depth > 0.0f)) return false;
     if (!(depth >= R.min_range) || !(depth <= R.max_range)) return false;
@@ -459,19 +490,99 @@ __device__ __forceinline__ bool vdb_init(const RayConst& R, const BatchRef& D, u
     r.px = px;
     r.py = py;
     r.pz = pz;
+    // Bounds of k_count's fp32 filter (u = 2^-24; every factor (1 + 2^-20) and the final 1.01
+    // absorb the rounding of this bound arithmetic itself).  bn is any radius; a voxel whose fp32
+    // squared distance d2_f <= bchk has |b_f| <= bn - sqrt3 db, hence for the exact b* = p - c*:
+    //   |c*_i| <= (|p_i| + |b_f|)(1 + 3u) <= cmax           (c_f = fl(c*), b_f = fl(p - c_f))
+    //   |b_f,i - b*_i| <= u (cmax + bn) = db,  |b*| <= bn,   |a*| <= |p - o| + bn <= amax
+    //   |a_f,i - a*_i| <= u (cmax + omax + amax) = da         (a_f = fl(fl(c*) - fl(o)))
+    //   |proj_f - proj_d| <= 3.0001u |a_f||b_f| + sqrt3 (amax db + bn da) + 3 da db + 2^-50 amax bn
+    //   |d2_f - d2_d|     <= 3.0001u |b_f|^2 + 2 sqrt3 bn db + 3 db^2 + 2^-50 bn^2
+    // (Cauchy-Schwarz for the sums of products; 2^-50 covers the double evaluation's own error).
+    {
+        constexpr float u = 5.9604645e-8f, s3 = 1.7320509f, g = 1.00000095f;  // 2^-24, sqrt 3, 1 + 2^-20
+        const float bn = fmaxf(depth - t0, R.tau) + 2.0f * R.vs;
+        const float pmax = fmaxf(fmaxf(fabsf(px), fabsf(py)), fabsf(pz));
+        const float omax = fmaxf(fmaxf(fabsf(D.s[t].ox), fabsf(D.s[t].oy)), fabsf(D.s[t].oz)) * g;
+        const float cmax = (pmax + bn) * g;
+        const float amax = depth * g + bn;
+        const float db = u * (cmax + bn) * g;
+        const float da = u * (cmax + omax + amax) * g;
+        const float am = amax + s3 * da, bm = bn + s3 * db;
+        r.ep = 1.01f * (3.0001f * u * am * bm + s3 * (amax * db + bn * da) + 3.0f * da * db +
+                        8.9e-16f * amax * bn);
+        const float e2 = 1.01f * (3.0001f * u * bm * bm + 2.0f * s3 * bn * db + 3.0f * db * db +
+                                  8.9e-16f * bn * bn);
+        const float gf = (float)R.gate_d2;
+        r.glo = gf - 2.0f * e2;
+        r.ghi = gf + 2.0f * e2;
+        const float bc = bn - s3 * db;
+        r.bchk = bc * bc * (1.0f - 8.0f * u);
+    }
     return true;
 }
 
-// GetVoxelCenter + ComputeSDF in double at the current voxel: proj and the squared distance
+// GetVoxelCenter + ComputeSDF in double at the current voxel: proj and the squared distance.
+// GetVoxelCenter's v vs + vs / 2 is exact in double ((2v + 1) < 2^25 times the 24-bit float vs),
+// so it is formed as (2v + 1) (vs / 2): one conversion and one product per axis.  The axes are
+// taken z, y, then x (Eigen's x + (y + z) reductions), so few double temporaries are live.
+__device__ __forceinline__ void vdb_geom_at(double hv, double ox, double oy, double oz, float px,
+                                            float py, float pz, int vx, int vy, int vz,
+                                            double& proj, double& d2) {
+    double c = (double)(int)(2u * (uint32_t)vz + 1u) * hv;
+    double b = (double)pz - c;
+    proj = (c - oz) * b;
+    d2 = b * b;
+    c = (double)(int)(2u * (uint32_t)vy + 1u) * hv;
+    b = (double)py - c;
+    proj = (c - oy) * b + proj;
+    d2 = b * b + d2;
+    c = (double)(int)(2u * (uint32_t)vx + 1u) * hv;
+    b = (double)px - c;
+    proj = (c - ox) * b + proj;
+    d2 = b * b + d2;
+}
+
 __device__ __forceinline__ void vdb_geom(const RayConst& R, const VdbState& r, double& proj,
                                          double& d2) {
-    const double cx = (double)r.vx * R.vs_d + R.vs_d / 2.0;
-    const double cy = (double)r.vy * R.vs_d + R.vs_d / 2.0;
-    const double cz = (double)r.vz * R.vs_d + R.vs_d / 2.0;
-    const double ax = cx - r.oxd, ay = cy - r.oyd, az = cz - r.ozd;
-    const double bx = r.pxd - cx, by = r.pyd - cy, bz = r.pzd - cz;
-    proj = ax * bx + (ay * by + az * bz);
-    d2 = bx * bx + (by * by + bz * bz);
+    // the point's double conversions stay per voxel (hoisted they would hold 6 VGPRs)
+    float px = r.px, py = r.py, pz = r.pz;
+    asm volatile("" : "+v"(px), "+v"(py), "+v"(pz));
+    vdb_geom_at(uniform_f64(R.vs_d * 0.5), r.oxd, r.oyd, r.ozd, px, py, pz, r.vx, r.vy, r.vz, proj,
+                d2);
+}
+
+// The double gate's verdict (proj > 0, or proj < 0 and d2 < gate_d2) from fp32 arithmetic: the
+// fp32 centre, offsets, projection and squared distance with the per-ray error bounds of vdb_init;
+// a voxel whose verdict the bounds leave open (|proj_f| <= ep, d2_f within 2 e2 of gate_d2, d2_f
+// beyond bchk, NaN) takes the double evaluation, in a branch the wave skips when none of its lanes
+// needs it.  Bit-identical verdict to the double gate by construction.
+__device__ __forceinline__ bool vdb_gate_filtered(const RayConst& R, float ox, float oy, float oz,
+                                                  const VdbState& r) {
+    const float cx = ((float)r.vx + 0.5f) * R.vs;
+    const float cy = ((float)r.vy + 0.5f) * R.vs;
+    const float cz = ((float)r.vz + 0.5f) * R.vs;
+    const float ax = cx - ox, ay = cy - oy, az = cz - oz;
+    const float bx = r.px - cx, by = r.py - cy, bz = r.pz - cz;
+    const float proj = ax * bx + ay * by + az * bz;
+    const float d2 = bx * bx + by * by + bz * bz;
+    const bool pos = proj > r.ep, neg = proj < -r.ep;
+    const bool in = d2 < r.glo, out = d2 >= r.ghi;
+    bool g = pos || (neg && in);
+    const bool open = !(d2 <= r.bchk) || !(pos || neg) || (neg && !(in || out));
+    if (__builtin_expect(__any(open), 0)) {
+        if (open) {
+            // the origin, vs / 2 and the point re-read or re-converted here (opaque to hoisting),
+            // so that the rare branch keeps no double live across the walk loop
+            const ScanRec* q = r.sr;
+            float px = r.px, py = r.py, pz = r.pz, vs = R.vs;
+            asm volatile("" : "+v"(q), "+v"(px), "+v"(py), "+v"(pz), "+v"(vs));
+            double pd, dd;
+            vdb_geom_at((double)vs * 0.5, q->odx, q->ody, q->odz, px, py, pz, r.vx, r.vy, r.vz, pd, dd);
+            g = pd > 0.0 || (pd < 0.0 && dd < R.gate_d2);
+        }
+    }
+    return g;
 }
 
 __device__ __forceinline__ bool vdb_inside(const VdbState& r) {
@@ -486,21 +597,16 @@ struct Walk<2> {  // TSDF_SEM_VDBFUSION_F64
                                                 float px, float py, float pz, State& r) {
         return vdb_init(R, D, t, px, py, pz, r);
     }
-    __device__ static __forceinline__ bool gate(const RayConst& R, float, float, float,
+    // k_count: the verdict alone ((float)sqrt(d2) < tau, i.e. -dist > -tau, is d2 < gate_d2)
+    __device__ static __forceinline__ bool gate(const RayConst& R, float ox, float oy, float oz,
                                                 const State& r, bool check = true) {
         if (check && !vdb_inside(r)) return false;
-        double proj, d2;
-        vdb_geom(R, r, proj, d2);
-        if (proj > 0.0) return true;
-        if (!(proj < 0.0)) return false;
-        return d2 < R.gate_d2;  // (float)sqrt(d2) < tau, i.e. -dist > -tau
+        return vdb_gate_filtered(R, ox, oy, oz, r);
     }
-    __device__ static __forceinline__ bool gate_sel(const RayConst& R, float, float, float,
+    __device__ static __forceinline__ bool gate_sel(const RayConst& R, float ox, float oy, float oz,
                                                     const State& r, bool check = true) {
         const bool inl = !check || vdb_inside(r);
-        double proj, d2;
-        vdb_geom(R, r, proj, d2);
-        return inl && (proj > 0.0 || (proj < 0.0 && d2 < R.gate_d2));
+        return inl && vdb_gate_filtered(R, ox, oy, oz, r);
     }
     __device__ static __forceinline__ bool sample(const RayConst& R, float, float, float,
                                                   const State& r, float& s, bool check = true) {
@@ -508,7 +614,7 @@ struct Walk<2> {  // TSDF_SEM_VDBFUSION_F64
         double proj, d2;
         vdb_geom(R, r, proj, d2);
         if (!(proj > 0.0 || proj < 0.0)) return false;
-        const float dist = (float)__builtin_sqrt(d2);
+        const float dist = vdb_sqrt_f(d2);
         const float sdf = proj > 0.0 ? dist : -dist;
         if (!(sdf > -R.tau)) return false;
         s = sdf < R.tau ? sdf : R.tau;
@@ -520,7 +626,7 @@ struct Walk<2> {  // TSDF_SEM_VDBFUSION_F64
         const bool inl = !check || vdb_inside(r);
         double proj, d2;
         vdb_geom(R, r, proj, d2);
-        const float dist = (float)__builtin_sqrt(d2);
+        const float dist = vdb_sqrt_f(d2);
         const float sdf = proj > 0.0 ? dist : -dist;
         s = sdf < R.tau ? sdf : R.tau;
         return inl && (proj > 0.0 || proj < 0.0) && sdf > -R.tau;

@@ -1,0 +1,65 @@
+"""bench.py's own multi-rank launcher (`python3 bench.py --gpus N` with no torchrun): N rank
+processes with the torch.distributed environment, the status of the first failing rank, and the
+refusal to print a line whose n_gpus is not the world that ran."""
+import os
+import subprocess
+import sys
+import textwrap
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+import bench  # noqa: E402
+
+
+def test_check_world_refuses_mismatch():
+    bench.check_world(2, 2)
+    with pytest.raises(SystemExit):
+        bench.check_world(8, 1)
+
+
+def test_launch_ranks_env(tmp_path):
+    out = tmp_path / "ranks"
+    out.mkdir()
+    child = tmp_path / "child.py"
+    child.write_text(textwrap.dedent("""
+        import os, sys
+        keys = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")
+        with open(os.path.join(sys.argv[1], os.environ["RANK"]), "w") as f:
+            f.write(" ".join(os.environ[k] for k in keys))
+    """))
+    assert bench.launch_ranks(3, script=str(child), argv=[str(out)]) == 0
+    got = sorted(os.listdir(out))
+    assert got == ["0", "1", "2"]
+    rows = [open(out / r).read().split() for r in got]
+    assert [r[0] for r in rows] == ["0", "1", "2"] and all(r[1] == r[0] for r in rows)
+    assert all(r[2] == "3" and r[3] == "127.0.0.1" for r in rows)
+    assert len({r[4] for r in rows}) == 1  # one rendezvous port
+
+
+def test_launch_ranks_failure_stops_the_others(tmp_path):
+    child = tmp_path / "child.py"
+    child.write_text(textwrap.dedent("""
+        import os, sys, time
+        if os.environ["RANK"] == "1":
+            sys.exit(3)
+        time.sleep(60)  # would wait at a barrier for the failed rank
+    """))
+    import time
+    t = time.time()
+    assert bench.launch_ranks(2, script=str(child), argv=[]) == 3
+    assert time.time() - t < 30
+
+
+def test_bench_gpus2_without_launcher_sets_world(tmp_path):
+    """The real script with --gpus 2 and no WORLD_SIZE spawns two ranks (they fail here at the
+    first GPU call: no device on the CPU runner), never one rank reporting n_gpus 1."""
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env["CUDA_VISIBLE_DEVICES"] = ""
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "1",
+                        "--warmup", "0", "--no-cpu"], env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode != 0
+    assert '"n_gpus"' not in r.stdout

@@ -101,6 +101,51 @@ def test_gpu_f64_semantics(case):
     assert r["max_abs_dsdf"] <= 1e-5
 
 
+def _filter_stress_scans():
+    """Inputs aimed at k_count's fp32 filter of the double gate: voxel centres
+    exactly on the plane through p normal to the ray (proj == 0 in double: skipped), points whose
+    behind-the-hit distances straddle tau, far-from-origin coordinates (large fp32 rounding of the
+    centres), a coarse grid of random rays, and a carving band."""
+    rng = np.random.default_rng(7)
+    scans = []
+    # axis rays: p_x on a voxel centre -> proj exactly 0 at that voxel; p_y, p_z on centres too
+    o = np.array([0.025, 0.025, 0.025])
+    xs = (np.arange(100, 140) + 0.5) * np.float64(np.float32(0.05))
+    p = np.stack([xs, np.full_like(xs, 0.025), np.full_like(xs, 0.025)], 1).astype(np.float32)
+    scans.append((p, o))
+    # far from the world origin: o ~ 1e3..1e4 m, a synthetic scan translated there
+    sim = OusterSim()
+    q, o0 = sim.scan(3)
+    off = np.array([4321.123456789, -1234.987654321, 77.7])
+    scans.append(((q.astype(np.float64) + off).astype(np.float32), o0 + off))
+    # random rays whose hits sit near voxel corners / centres at tau distances
+    o = np.array([0.3, -0.2, 0.1])
+    d = rng.normal(size=(20000, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    r = rng.uniform(1.0, 20.0, size=(20000, 1))
+    hit = o + d * r
+    hit = np.round(hit / 0.025) * 0.025 + rng.choice([0.0, 1e-7, -1e-7], size=hit.shape)
+    scans.append((hit.astype(np.float32), o))
+    return scans
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("carving", [False, True])
+def test_gpu_f64_filter_stress(carving):
+    """The fp32-filtered gate and the sample path of TSDF_SEM_VDBFUSION_F64 equal the oracle's
+    double arithmetic bit for bit on inputs that sit on the filter's edges."""
+    from tsdf_map import HipTSDFVolume
+    kw = dict(space_carving=carving, max_range=60.0) if carving else {}
+    scans = _filter_stress_scans()
+    g = fill(HipTSDFVolume(0.05, 0.15, semantics="vdbfusion_f64", **kw), scans)
+    g.sync()
+    o = fill(oracle.OracleTSDFVolume(0.05, 0.15, semantics="vdbfusion_f64", **kw), scans)
+    r = compare(g.export_voxels(), o.export_voxels())
+    print("f64 filter stress (carving=%s):" % carving, r)
+    assert r["only_a"] == r["only_b"] == r["weight_mismatch"] == 0
+    assert r["bitwise_equal"] == r["voxels_a"] > 0, r
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", ["C1", "C4"])
 def test_gpu_fp32_distance_from_literal(case):
