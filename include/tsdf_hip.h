@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define TSDF_ABI_VERSION 5
+#define TSDF_ABI_VERSION 6
 #define TSDF_MAX_BATCH 512 /* scans per GPU batch (see tsdf_params.max_batch) */
 #define TSDF_BRICK_SIDE 8 /* voxels per brick edge: a brick is 8^3 = 512 voxels */
 
@@ -122,9 +122,10 @@ typedef struct tsdf_params {
 /* Batching.  Scans are integrated in call order and the field after any sequence of calls is
  * bitwise the one scan-at-a-time integration gives; the GPU merely processes up to max_batch
  * consecutive scans per launch sequence (rays of all of them walk together; each brick applies
- * its per-scan fuses in scan order).  Host-pointer scans are copied to device staging at once and
- * queued until max_batch are pending; any other call (sync, query, export, import, stats, a
- * device-pointer integrate) flushes the queue first. */
+ * its per-scan fuses in scan order).  Host-pointer scans (tsdf_integrate) and single device scans
+ * (tsdf_integrate_device) are copied to device staging at once and queued until max_batch are
+ * pending; any other call (sync, query, export, import, stats, tsdf_integrate_batch_device)
+ * flushes the queue first. */
 
 typedef struct tsdf_stats {
     uint64_t n_scans;          /* scans integrated (queued scans are flushed first) */
@@ -171,8 +172,11 @@ const char* tsdf_last_error(const tsdf_ctx* ctx);
 int tsdf_integrate(tsdf_ctx* ctx, const void* pts, uint64_t n, uint32_t point_step,
                    uint32_t xyz_offset, int32_t xyz_is_f64, const double origin[3]);
 
-/* One scan already in device memory: d_xyz = n packed float32 triplets (12 B per point).
- * Launched at once as a batch of one (after flushing the pending host scans). */
+/* One scan already in device memory: d_xyz = n packed float32 triplets (12 B per point).  The
+ * points are copied (device to device) into the pending batch's staging before the call returns,
+ * so d_xyz may be reused or freed at once; the scan joins the pending batch like a host scan (see
+ * Batching).  (ABI v6; before, the scan launched at once and d_xyz had to stay valid until the next
+ * tsdf_sync.) */
 int tsdf_integrate_device(tsdf_ctx* ctx, const float* d_xyz, uint64_t n, const double origin[3]);
 
 /* n_scans scans in device memory, integrated in order, max_batch scans per GPU batch.  Scan s is
@@ -205,7 +209,9 @@ int tsdf_export_bricks(tsdf_ctx* ctx, int32_t* coords, float* sdf, float* weight
 /* Merge n unique bricks into the field: for every voxel with weight w_in > 0,
  * sdf <- (sdf*W + sdf_in*w_in) / (W + w_in), W <- W + w_in, or a plain copy where W == 0
  * (weighted-mean merge of partial fields; used for multi-GPU border bricks and for resuming
- * from an export). */
+ * from an export).  With TSDF_SEM_VOXBLOX the merged weight is capped at max_weight, as Voxblox
+ * caps every weight (its clamped update is order dependent, so a merge of Voxblox partial fields
+ * is an approximation). */
 int tsdf_import_bricks(tsdf_ctx* ctx, const int32_t* coords, const float* sdf, const float* weight,
                        uint64_t n);
 

@@ -89,7 +89,7 @@ __global__ __launch_bounds__(BRD_THREADS) void k_border_pack(Table T, Pool Pl, f
 
 __global__ __launch_bounds__(BRD_THREADS) void k_border_merge(Table T, Pool Pl,
                                                               const uint32_t* __restrict__ recv,
-                                                              Globals* G) {
+                                                              Globals* G, float max_w) {
     const uint32_t* tile = recv + (size_t)blockIdx.x * TILE_WORDS;
     const uint64_t key = (uint64_t)tile[2 * BRICK_VOX] | ((uint64_t)tile[2 * BRICK_VOX + 1] << 32);
     const int64_t h = table_find(T, key);  // every lane finds the same entry (no LDS broadcast)
@@ -113,7 +113,7 @@ __global__ __launch_bounds__(BRD_THREADS) void k_border_merge(Table T, Pool Pl,
         }
         const float nw = w0 + wi;
         *S = (*S * w0 + s_in[l] * wi) / nw;
-        *W = nw;
+        *W = nw > max_w ? max_w : nw;  // Voxblox: capped at max_weight (else +inf)
     }
 }
 
@@ -151,10 +151,11 @@ hipError_t launch_border_pack(const Table& T, const Pool& Pl, float bg, uint32_t
 }
 
 hipError_t launch_border_merge(const Table& T, const Pool& Pl, const uint32_t* d_recv,
-                               uint64_t n_rows, Globals* G, hipStream_t st) {
+                               uint64_t n_rows, Globals* G, float max_w, hipStream_t st) {
     for (uint64_t r0 = 0; r0 < n_rows; r0 += (1u << 30)) {
         const uint64_t nr = std::min<uint64_t>(n_rows - r0, 1u << 30);
-        k_border_merge<<<(uint32_t)nr, BRD_THREADS, 0, st>>>(T, Pl, d_recv + r0 * TILE_WORDS, G);
+        k_border_merge<<<(uint32_t)nr, BRD_THREADS, 0, st>>>(T, Pl, d_recv + r0 * TILE_WORDS, G,
+                                                             max_w);
     }
     return hipGetLastError();
 }

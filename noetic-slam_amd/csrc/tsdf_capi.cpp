@@ -228,7 +228,13 @@ struct tsdf_ctx {
     float* stage2[2] = {nullptr, nullptr};
     hipEvent_t ev_main = nullptr;
     hipEvent_t ev_compact[2] = {nullptr, nullptr}, ev_integ[2] = {nullptr, nullptr};
-    BatchDesc pend{};  // pending host scans (points in stage2[batch_id & 1])
+    BatchDesc pend{};  // pending host scans (points in stage2[pend_stage])
+    // Device staging ownership (independent of batch parity, which replays can shift): the pending
+    // batch's buffer, and per buffer the last batch that read it (its id and completion event).
+    int pend_stage = 0;
+    int last_stage = 1;  // the buffer of the most recently launched host batch
+    uint64_t stage_reader[2] = {~0ull, ~0ull};
+    hipEvent_t stage_ev[2] = {nullptr, nullptr};
     // batch records for the kernels: a pinned host ring and its device twin (launch() copies a
     // batch's n_scans + 1 records into the next slot on the batch's stream)
     static constexpr int RING = 16;
@@ -255,6 +261,11 @@ struct tsdf_ctx {
     PackPool* pack = nullptr;  // host staging threads (tsdf_integrate of strided records)
     uint64_t n_grows = 0, n_replayed = 0;
 };
+
+// Weight cap of the weighted-mean merges (import, border reduce): Voxblox's max_weight, else none
+static float merge_cap(const tsdf_ctx* c) {
+    return c->p.semantics == TSDF_SEM_VOXBLOX ? c->p.max_weight : INFINITY;
+}
 
 static int fail(tsdf_ctx* c, int code, const char* fmt, ...) {
     if (c) {
@@ -391,6 +402,11 @@ static int launch(tsdf_ctx* c, const float* d_xyz, BatchDesc& D) {
     HIPCHK(c, launch_finish(c->G, par, (uint32_t)c->batch_id, st));
     HIPCHK(c, hipEventRecord(c->ev_integ[par], st));
     if (c->can_grow) c->log.push_back({c->batch_id, d_xyz, D});
+    for (int k = 0; k < 2; k++)  // a host batch: its staging buffer's last reader
+        if (d_xyz == c->stage2[k]) {
+            c->stage_reader[k] = c->batch_id;
+            HIPCHK(c, hipEventRecord(c->stage_ev[k], st));
+        }
     c->batch_id++;
     c->n_batches++;
     c->n_scans += D.n_scans;
@@ -412,7 +428,10 @@ static int join(tsdf_ctx* c) {
 // Launch the queued host scans (integrate paths: no join, so batches keep overlapping).
 static int flush(tsdf_ctx* c) {
     if (c->pend.n_scans == 0) return TSDF_OK;
-    const int rc = launch(c, c->stage2[c->batch_id & 1], c->pend);
+    // the buffer the pending scans were staged into; a replay that runs inside launch() (metrics
+    // drain, log bound) re-reads only logged batches, none of which uses this buffer any more
+    const int rc = launch(c, c->stage2[c->pend_stage], c->pend);
+    c->last_stage = c->pend_stage;
     c->pend.n_scans = 0;
     c->pend.s[0].off = 0;
     return rc;
@@ -901,6 +920,7 @@ void tsdf_destroy(tsdf_ctx* c) {
         if (c->bst[q]) (void)hipStreamDestroy(c->bst[q]);
         if (c->ev_compact[q]) (void)hipEventDestroy(c->ev_compact[q]);
         if (c->ev_integ[q]) (void)hipEventDestroy(c->ev_integ[q]);
+        if (c->stage_ev[q]) (void)hipEventDestroy(c->stage_ev[q]);
     }
     if (c->ev_main) (void)hipEventDestroy(c->ev_main);
     for (int k = 0; k < tsdf_ctx::RING; k++)
@@ -925,6 +945,7 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
         HIPCHK(c, hipStreamCreateWithFlags(&c->bst[q], hipStreamNonBlocking));
         HIPCHK(c, hipEventCreateWithFlags(&c->ev_compact[q], hipEventDisableTiming));
         HIPCHK(c, hipEventCreateWithFlags(&c->ev_integ[q], hipEventDisableTiming));
+        HIPCHK(c, hipEventCreateWithFlags(&c->stage_ev[q], hipEventDisableTiming));
     }
     HIPCHK(c, hipEventCreateWithFlags(&c->ev_main, hipEventDisableTiming));
 
@@ -1114,6 +1135,54 @@ static void set_origin(BatchDesc& D, uint32_t s, const double o[3]) {
     D.s[s].odz = o[2];
 }
 
+// The pending batch's device staging buffer (host and single device scans are queued there).  A
+// new pending batch takes the buffer the last launched host batch did not use; that buffer's
+// previous reader must be complete and, with growth possible, committed: an overflowed batch is
+// re-run from its logged input, so that input stays until then.
+static int pend_stage_buffer(tsdf_ctx* c) {
+    if (c->pend.n_scans != 0) return TSDF_OK;
+    const int k = c->last_stage ^ 1;
+    if (c->stage_reader[k] != ~0ull) {
+        if (c->can_grow) {
+            HIPCHK(c, hipEventSynchronize(c->stage_ev[k]));
+            uint32_t failed = 0;
+            HIPCHK(c, hipMemcpy(&failed, &c->G->failed, 4, hipMemcpyDeviceToHost));
+            if (failed) {  // replays re-read stage2[k]: it is written only after them
+                int rc = drain_all(c);
+                if (!rc) rc = check_and_replay(c);
+                if (rc) return rc;
+            } else {  // every batch up to stage2[k]'s reader committed
+                const uint64_t done = c->stage_reader[k];
+                size_t j = 0;
+                while (j < c->log.size() && c->log[j].id <= done) j++;
+                c->log.erase(c->log.begin(), c->log.begin() + j);
+            }
+        }
+        HIPCHK(c, hipStreamWaitEvent(c->stream, c->stage_ev[k], 0));
+    }
+    c->pend_stage = k;
+    return TSDF_OK;
+}
+
+// Append a staged scan of n points seen from origin to the pending batch; launch it when full.
+static int pend_push(tsdf_ctx* c, uint64_t n, const double origin[3]) {
+    BatchDesc& D = c->pend;
+    const uint32_t s = D.n_scans;
+    set_origin(D, s, origin);
+    D.s[s + 1].off = D.s[s].off + (uint32_t)n;
+    D.n_scans = s + 1;
+    c->n_points_in += n;
+    if (D.n_scans == c->max_batch) return flush(c);
+    return TSDF_OK;
+}
+
+// Room for a scan of n points in the pending batch (flushing it first if needed).
+static int pend_room(tsdf_ctx* c, uint64_t n) {
+    if (c->pend.n_scans == c->max_batch || c->pend.s[c->pend.n_scans].off + n > c->batch_points)
+        return flush(c);
+    return TSDF_OK;
+}
+
 int tsdf_integrate(tsdf_ctx* c, const void* pts, uint64_t n, uint32_t point_step,
                    uint32_t xyz_offset, int32_t xyz_is_f64, const double origin[3]) {
     if (!c) return TSDF_EINVAL;
@@ -1125,8 +1194,8 @@ int tsdf_integrate(tsdf_ctx* c, const void* pts, uint64_t n, uint32_t point_step
         return fail(c, TSDF_EINVAL, "scan of %llu points exceeds max_points %llu",
                     (unsigned long long)n, (unsigned long long)c->max_points);
     HIPCHK(c, hipSetDevice(c->device));
-    if (c->pend.n_scans == c->max_batch || c->pend.s[c->pend.n_scans].off + n > c->batch_points) {
-        const int rc = flush(c);
+    {
+        const int rc = pend_room(c, n);
         if (rc) return rc;
     }
     const int b = c->stage_cur;
@@ -1158,41 +1227,14 @@ int tsdf_integrate(tsdf_ctx* c, const void* pts, uint64_t n, uint32_t point_step
             pack(0, n);
         }
     }
-    BatchDesc& D = c->pend;
-    const uint32_t s = D.n_scans;
-    if (s == 0 && c->batch_id >= 2) {  // stage2[batch_id & 1] was last read by batch batch_id - 2
-        const int sp = (int)(c->batch_id & 1);
-        if (c->can_grow) {
-            // checkpoint: batch batch_id - 2 must have committed before its staged input goes
-            // (an overflowed batch is re-run from it after growing)
-            HIPCHK(c, hipEventSynchronize(c->ev_integ[sp]));
-            uint32_t failed = 0;
-            HIPCHK(c, hipMemcpy(&failed, &c->G->failed, 4, hipMemcpyDeviceToHost));
-            if (failed) {
-                int rc = drain_all(c);
-                if (!rc) rc = check_and_replay(c);
-                if (rc) return rc;
-            } else {
-                const uint64_t done = c->batch_id - 2;
-                size_t k = 0;
-                while (k < c->log.size() && c->log[k].id <= done) k++;
-                c->log.erase(c->log.begin(), c->log.begin() + k);
-            }
-        }
-        HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_integ[c->batch_id & 1], 0));
-    }
-    const int sp = (int)(c->batch_id & 1);  // the pending batch's parity (after any replay)
+    int rc = pend_stage_buffer(c);
+    if (rc) return rc;
     if (n) {
-        HIPCHK(c, hipMemcpyAsync(c->stage2[sp] + 3 * (uint64_t)D.s[s].off, h, n * 12,
-                                 hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->stage2[c->pend_stage] + 3 * (uint64_t)c->pend.s[c->pend.n_scans].off,
+                                 h, n * 12, hipMemcpyHostToDevice, c->stream));
     }
     HIPCHK(c, hipEventRecord(c->stage_done[b], c->stream));
-    set_origin(D, s, origin);
-    D.s[s + 1].off = D.s[s].off + (uint32_t)n;
-    D.n_scans = s + 1;
-    c->n_points_in += n;
-    if (D.n_scans == c->max_batch) return flush(c);
-    return TSDF_OK;
+    return pend_push(c, n, origin);
 }
 
 int tsdf_integrate_batch_device(tsdf_ctx* c, const float* d_xyz, const uint64_t* offs,
@@ -1229,11 +1271,25 @@ int tsdf_integrate_batch_device(tsdf_ctx* c, const float* d_xyz, const uint64_t*
     return TSDF_OK;
 }
 
+// A single device scan joins the pending batch like a host scan: its points are copied into the
+// pending batch's device staging before the call returns, so the caller's buffer is free at once
+// (and a capacity replay re-reads the library's copy, not the caller's memory).
 int tsdf_integrate_device(tsdf_ctx* c, const float* d_xyz, uint64_t n, const double origin[3]) {
     if (!c) return TSDF_EINVAL;
     if ((!d_xyz && n) || !origin) return fail(c, TSDF_EINVAL, "null argument");
-    const uint64_t offs[2] = {0, n};
-    return tsdf_integrate_batch_device(c, d_xyz, offs, 1, origin);
+    if (n > c->max_points)
+        return fail(c, TSDF_EINVAL, "scan of %llu points exceeds max_points %llu",
+                    (unsigned long long)n, (unsigned long long)c->max_points);
+    HIPCHK(c, hipSetDevice(c->device));
+    int rc = pend_room(c, n);
+    if (!rc) rc = pend_stage_buffer(c);
+    if (rc) return rc;
+    if (n) {
+        HIPCHK(c, hipMemcpyAsync(c->stage2[c->pend_stage] + 3 * (uint64_t)c->pend.s[c->pend.n_scans].off,
+                                 d_xyz, n * 12, hipMemcpyDeviceToDevice, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    return pend_push(c, n, origin);
 }
 
 int tsdf_sync(tsdf_ctx* c) {
@@ -1253,12 +1309,14 @@ int tsdf_sync(tsdf_ctx* c) {
         HIPCHK(c, hipMemset(&c->G->overflow, 0, sizeof ovf));
         if (ovf & ERR_MERGE_KEY)
             return fail(c, TSDF_EINVAL, "border merge: a tile's brick is not held by this context");
-        return fail(c, TSDF_ENOMEM, "capacity overflow (%s%s%s%s%s): updates were dropped",
+        return fail(c, TSDF_ENOMEM, "capacity overflow (%s%s%s%s%s%s%s): updates were dropped",
                     (ovf & OVF_TABLE) ? "hash table full; " : "",
                     (ovf & OVF_POOL) ? "brick pool exhausted; " : "",
                     (ovf & OVF_PAIRS) ? "ray brick-pair slots exceeded; " : "",
                     (ovf & OVF_ACTIVE) ? "active-brick list full; " : "",
-                    (ovf & OVF_SMP) ? "sample list full" : "");
+                    (ovf & OVF_SMP) ? "sample list full; " : "",
+                    (ovf & OVF_FB) ? "fallback pair list full; " : "",
+                    (ovf & OVF_SPN) ? "span list full; " : "");
     }
     return TSDF_OK;
 }
@@ -1548,7 +1606,8 @@ int tsdf_import_bricks(tsdf_ctx* c, const int32_t* coords, const float* sdf, con
         e = hipMemcpyAsync(ds, sdf, n * BRICK_VOX * 4, hipMemcpyHostToDevice, c->stream);
     if (e == hipSuccess)
         e = hipMemcpyAsync(dw, weight, n * BRICK_VOX * 4, hipMemcpyHostToDevice, c->stream);
-    if (e == hipSuccess) e = launch_import(c->T, c->Pl, dc, (uint32_t)n, ds, dw, dt, c->G, c->stream);
+    if (e == hipSuccess) e = launch_import(c->T, c->Pl, dc, (uint32_t)n, ds, dw, dt, c->G, merge_cap(c),
+                                           c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     (void)hipFree(dc);
     (void)hipFree(ds);
@@ -1756,7 +1815,7 @@ int tsdf_border_merge_device(tsdf_ctx* c, const uint32_t* d_recv, const uint64_t
     for (uint32_t r = 0; r < world; r++) {  // sources in ascending rank order
         if (recv_counts[r])
             HIPCHK(c, launch_border_merge(c->T, c->Pl, d_recv + row * TSDF_TILE_WORDS,
-                                          recv_counts[r], c->G, c->stream));
+                                          recv_counts[r], c->G, merge_cap(c), c->stream));
         row += recv_counts[r];
     }
     HIPCHK(c, hipStreamSynchronize(c->stream));

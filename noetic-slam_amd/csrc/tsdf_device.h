@@ -270,7 +270,7 @@ hipError_t launch_query_dense(const Table& T, const Pool& Pl, const int lo[3], c
                               float bg, float* d_sdf, float* d_w, hipStream_t st);
 hipError_t launch_import(const Table& T, const Pool& Pl, const int32_t* d_coords, uint32_t n,
                          const float* d_sdf, const float* d_w, uint32_t* d_tidx, Globals* G,
-                         hipStream_t st);
+                         float max_w, hipStream_t st);
 hipError_t launch_fill(float* p, float v, uint64_t n, hipStream_t st);
 // border-brick reduce (tsdf_border.hip)
 constexpr int TILE_WORDS = 1028;  // include/tsdf_hip.h TSDF_TILE_WORDS
@@ -285,8 +285,9 @@ hipError_t launch_border_owner(const Table& T, uint32_t n_bricks, const uint64_t
 hipError_t launch_border_pack(const Table& T, const Pool& Pl, float bg, uint32_t n_bricks,
                               uint32_t rank, const uint32_t* d_owner, uint32_t* d_cursor,
                               uint32_t* d_rows, uint32_t n_rows, uint32_t* d_send, hipStream_t st);
+// max_w: the merged weight's cap (Voxblox max_weight; +inf for VDBFusion)
 hipError_t launch_border_merge(const Table& T, const Pool& Pl, const uint32_t* d_recv,
-                               uint64_t n_rows, Globals* G, hipStream_t st);
+                               uint64_t n_rows, Globals* G, float max_w, hipStream_t st);
 // Ouster packets (tsdf_ouster.hip)
 struct OsField {
     uint32_t nbytes;  // little-endian source bytes (0: the profile has no such field)

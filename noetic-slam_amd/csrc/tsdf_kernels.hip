@@ -1002,7 +1002,8 @@ __global__ void k_import_insert(Table T, const int32_t* __restrict__ coords, uin
 }
 
 __global__ void k_import_merge(Table T, Pool Pl, const uint32_t* __restrict__ tidx, uint32_t n,
-                               const float* __restrict__ sdf_in, const float* __restrict__ w_in) {
+                               const float* __restrict__ sdf_in, const float* __restrict__ w_in,
+                               float max_w) {
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < (uint64_t)n * BRICK_VOX;
          i += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t b = (uint32_t)(i / BRICK_VOX);
@@ -1023,7 +1024,7 @@ __global__ void k_import_merge(Table T, Pool Pl, const uint32_t* __restrict__ ti
         }
         const float nw = w0 + wi;
         *S = (*S * w0 + sdf_in[i] * wi) / nw;
-        *W = nw;
+        *W = nw > max_w ? max_w : nw;  // Voxblox: capped at max_weight (else +inf)
     }
 }
 
@@ -1239,10 +1240,10 @@ hipError_t launch_query_dense(const Table& T, const Pool& Pl, const int lo[3], c
 
 hipError_t launch_import(const Table& T, const Pool& Pl, const int32_t* d_coords, uint32_t n,
                          const float* d_sdf, const float* d_w, uint32_t* d_tidx, Globals* G,
-                         hipStream_t st) {
+                         float max_w, hipStream_t st) {
     k_import_insert<<<grid_for(n, 256, 4096), 256, 0, st>>>(T, d_coords, n, d_tidx, G);
     k_import_merge<<<grid_for((uint64_t)n * BRICK_VOX, 256, 8192), 256, 0, st>>>(T, Pl, d_tidx, n,
-                                                                                 d_sdf, d_w);
+                                                                                 d_sdf, d_w, max_w);
     return hipGetLastError();
 }
 

@@ -954,7 +954,10 @@ int tsdf_import_bricks(tsdf_ctx* c, const int32_t* coords, const float* sdf, con
             }
             const float nw = v->W + wi;
             v->S = (v->S * v->W + sdf[512 * i + l] * wi) / nw;
-            v->W = nw;
+            /* Voxblox semantics never lets a weight pass max_weight (updateTsdfVoxel's cap): the
+             * merged replica weight is capped the same way (an approximation of Voxblox's
+             * order-dependent update) */
+            v->W = (c->sem == TSDF_SEM_VOXBLOX && nw > c->p.max_weight) ? c->p.max_weight : nw;
         }
     return TSDF_OK;
 }
