@@ -114,6 +114,12 @@ typedef struct tsdf_params {
      * space carving, no Voxblox clearing rays), else twice.  The field is bit for bit the same
      * either way; the single walk measures slower on MI355X. */
     int32_t walk;
+    /* ABI v6: Voxblox's sample weight (TSDF_SEM_VOXBLOX only).  1 (tsdf_default_params; voxblox
+     * TsdfIntegratorBase::Config use_const_weight = false, upstream's default): w = 1 / z^2, z the
+     * point's depth along the sensor's z axis (|z| <= 1e-6: w = 0), the axis taken from the scan's
+     * pose (tsdf_integrate_pose; the plain integrate calls use the world z axis, an identity
+     * rotation); then the dropoff.  0: w = 1 (use_const_weight = true). */
+    int32_t depth_weight;
 } tsdf_params;
 
 #define TSDF_WALK_TWO 0
@@ -172,6 +178,14 @@ const char* tsdf_last_error(const tsdf_ctx* ctx);
 int tsdf_integrate(tsdf_ctx* ctx, const void* pts, uint64_t n, uint32_t point_step,
                    uint32_t xyz_offset, int32_t xyz_is_f64, const double origin[3]);
 
+/* ABI v6: tsdf_integrate with the sensor's full pose: pose = (x, y, z, qx, qy, qz, qw), the
+ * position (the ray origin) and orientation of the sensor in the world frame, in
+ * geometry_msgs/Pose order (DLIO's /robot/dlio/odom_node/pose, odom.cc:315-356).  The orientation
+ * gives the sensor z axis of Voxblox's 1/z^2 weight (tsdf_params.depth_weight); VDBFusion ignores
+ * it.  The quaternion need not be normalised. */
+int tsdf_integrate_pose(tsdf_ctx* ctx, const void* pts, uint64_t n, uint32_t point_step,
+                        uint32_t xyz_offset, int32_t xyz_is_f64, const double pose[7]);
+
 /* One scan already in device memory: d_xyz = n packed float32 triplets (12 B per point).  The
  * points are copied (device to device) into the pending batch's staging before the call returns,
  * so d_xyz may be reused or freed at once; the scan joins the pending batch like a host scan (see
@@ -186,6 +200,10 @@ int tsdf_integrate_device(tsdf_ctx* ctx, const float* d_xyz, uint64_t n, const d
  * re-run from it after growing (tsdf_params.max_bricks_hard). */
 int tsdf_integrate_batch_device(tsdf_ctx* ctx, const float* d_xyz, const uint64_t* scan_offsets,
                                 uint32_t n_scans, const double* origins);
+/* ABI v6: the same with one pose (x, y, z, qx, qy, qz, qw) per scan (poses: host, 7 x n_scans). */
+int tsdf_integrate_batch_device_pose(tsdf_ctx* ctx, const float* d_xyz,
+                                     const uint64_t* scan_offsets, uint32_t n_scans,
+                                     const double* poses);
 
 /* Block until all queued work finished (growing capacity and re-running overflowed batches first,
  * see tsdf_params.max_bricks_hard); reports an overflow that could not be grown away as
@@ -238,6 +256,17 @@ int tsdf_extract_mesh(tsdf_ctx* ctx, float min_weight, float* tri, uint64_t cap,
 /* The generated marching-cubes case table (256 x 32 bytes: [case][0] = triangles, then 3 edge ids
  * per triangle; corner c = (c & 1, c >> 1 & 1, c >> 2 & 1); edges axis-major). */
 int tsdf_mc_table(uint8_t* out);
+
+/* ABI v6: marching-cubes case tables.  TSDF_MC_GENERATED: the table above (ambiguous faces paired
+ * around their inside corners, so neighbouring cubes agree).  TSDF_MC_LORENSEN: the classic
+ * Lorensen / Bourke table that VDBFusion's extract_triangle_mesh uses (the same triangles for
+ * unambiguous cases; ambiguous faces are split the classic way, which can leave cracks). */
+#define TSDF_MC_GENERATED 0
+#define TSDF_MC_LORENSEN 1
+int tsdf_extract_mesh_table(tsdf_ctx* ctx, float min_weight, int32_t table, float* tri,
+                            uint64_t cap, uint64_t* n_tri);
+/* The case table `table` in tsdf_mc_table's layout (edges in this library's numbering). */
+int tsdf_mc_table_of(int32_t table, uint8_t* out);
 
 /* ---- Ouster sensor input ------------------------------------------------------
  * The reference's sensor path is the Ouster SDK (src/ouster/ouster-sdk/ouster_client): UDP lidar

@@ -622,16 +622,21 @@ static int grow_smp(tsdf_ctx* c) {
     const uint64_t ns = std::min<uint64_t>(2ull * c->Wk.max_smp, smp_limit(c));
     if (ns <= c->Wk.max_smp) return fail(c, TSDF_ENOMEM, "sample list at its limit");
     uint2* f[2] = {nullptr, nullptr};
+    float* fw[2] = {nullptr, nullptr};  // sem 3: the samples' weights
     hipError_t e = hipMalloc(&f[0], ns * sizeof(uint2));
     if (e == hipSuccess) e = hipMalloc(&f[1], ns * sizeof(uint2));
+    for (int q = 0; q < 2 && e == hipSuccess && c->R.depth_w; q++) e = hipMalloc(&fw[q], ns * sizeof(float));
     if (e != hipSuccess) {
         (void)hipGetLastError();
         for (auto q : f) if (q) (void)hipFree(q);
+        for (auto q : fw) if (q) (void)hipFree(q);
         return fail(c, TSDF_ENOMEM, "sample list allocation failed");
     }
     for (int q = 0; q < 2; q++) {
         (void)hipFree(c->W2[q].smp);
+        if (c->W2[q].smw) (void)hipFree(c->W2[q].smw);
         c->W2[q].smp = f[q];
+        c->W2[q].smw = fw[q];
         c->W2[q].max_smp = (uint32_t)ns;
     }
     c->Wk.max_smp = (uint32_t)ns;
@@ -786,7 +791,11 @@ struct McTable {
     uint8_t edge[12][2];   // edge -> (a, b), b = a | axis bit
 };
 
-static McTable build_mc_table() {
+// lorensen: the classic table's ambiguity rule instead (Lorensen & Cline's complement symmetry,
+// the table VDBFusion's extract_triangle_mesh transcribes): an ambiguous face pairs its crossings
+// around the inside corners when at most 4 corners of the cube are inside, around the outside
+// corners otherwise; the two cubes sharing a face can then disagree (the classic cracks).
+static McTable build_mc_table(bool lorensen) {
     McTable M{};
     int ne = 0;
     for (int d = 0; d < 3; d++)
@@ -822,7 +831,10 @@ static McTable build_mc_table() {
                 std::vector<std::pair<int, int>> pairs;
                 if (ncr == 2) pairs.push_back({cr[0], cr[1]});
                 if (ncr == 4) {
-                    if (in[0]) pairs = {{3, 0}, {1, 2}};
+                    // around the inside corners (generated; Lorensen with <= 4 inside corners), else
+                    // around the outside ones
+                    const bool around_in = !lorensen || __builtin_popcount((unsigned)k) <= 4;
+                    if (in[0] == (around_in ? 1 : 0)) pairs = {{3, 0}, {1, 2}};
                     else pairs = {{0, 1}, {2, 3}};
                 }
                 for (auto [i, j] : pairs) {
@@ -854,9 +866,9 @@ static McTable build_mc_table() {
     return M;
 }
 
-static const McTable& mc_table() {
-    static const McTable M = build_mc_table();
-    return M;
+static const McTable& mc_table(int which = TSDF_MC_GENERATED) {
+    static const McTable G = build_mc_table(false), L = build_mc_table(true);
+    return which == TSDF_MC_LORENSEN ? L : G;
 }
 
 extern "C" {
@@ -880,6 +892,7 @@ void tsdf_default_params(tsdf_params* p) {
     p->allow_clear = 1;  // voxblox TsdfIntegratorBase::Config defaults
     p->use_weight_dropoff = 1;
     p->max_weight = 10000.0f;
+    p->depth_weight = 1;  // voxblox use_const_weight = false (upstream's default)
 }
 
 int tsdf_abi_version(void) { return TSDF_ABI_VERSION; }
@@ -909,7 +922,7 @@ void tsdf_destroy(tsdf_ctx* c) {
                    c->W2[0].ord_hist, c->W2[1].ord_hist,    c->W2[1].pair,    c->W2[1].blk,
                    c->W2[1].blk_n, c->W2[1].fb,        c->W2[1].smp,     c->W2[1].active,
                    c->W2[0].cagg,    c->W2[1].cagg,      c->W2[0].act,     c->W2[1].act,
-                   c->W2[0].spn,     c->W2[1].spn};
+                   c->W2[0].spn,     c->W2[1].spn,       c->W2[0].smw,     c->W2[1].smw};
     for (void* d : dev)
         if (d) (void)hipFree(d);
     for (int i = 0; i < 2; i++) {
@@ -957,7 +970,9 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
     c->R.carving = p->space_carving ? 1 : 0;
     c->R.tau2_lo = (float)(((double)c->R.tau * (1.0 - 0x1p-20)) * ((double)c->R.tau * (1.0 - 0x1p-20)));
     c->R.tau2_hi = (float)(((double)c->R.tau * (1.0 + 0x1p-20)) * ((double)c->R.tau * (1.0 + 0x1p-20)));
-    c->R.sem = p->semantics;
+    // internal sem 3: Voxblox with the 1/z^2 weight (per-sample weights stored by k_place)
+    c->R.depth_w = p->semantics == TSDF_SEM_VOXBLOX && p->depth_weight ? 1 : 0;
+    c->R.sem = c->R.depth_w ? 3 : p->semantics;
     c->R.allow_clear = p->allow_clear ? 1 : 0;
     c->R.dropoff = p->use_weight_dropoff ? 1 : 0;
     c->R.max_weight = p->max_weight;
@@ -1000,6 +1015,7 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
         const bool clearing = p->semantics == TSDF_SEM_VOXBLOX && p->allow_clear &&
                               std::isfinite(p->max_range);
         c->fused = p->walk == TSDF_WALK_SINGLE && !p->space_carving && !clearing && maxp <= 4 &&
+                   !c->R.depth_w &&
                    steps <= 32.0;
         c->nstep = steps <= 16.0 ? 16 : 32;
     }
@@ -1050,6 +1066,7 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
         HIPCHK(c, hipMalloc(&W.blk_n, (size_t)c->max_blocks * 2 * sizeof(uint32_t)));
         HIPCHK(c, hipMalloc(&W.fb, (size_t)W.max_fb * sizeof(uint4)));
         HIPCHK(c, hipMalloc(&W.smp, (size_t)W.max_smp * sizeof(uint2)));
+        if (c->R.depth_w) HIPCHK(c, hipMalloc(&W.smw, (size_t)W.max_smp * sizeof(float)));
         HIPCHK(c, hipMalloc(&W.spn, (size_t)W.max_spn * sizeof(uint32_t)));
         HIPCHK(c, hipMalloc(&W.ord_hist, 64 * 32 * sizeof(uint32_t)));
         HIPCHK(c, hipMalloc(&W.act, (size_t)c->max_blocks * sizeof(uint32_t)));
@@ -1096,7 +1113,12 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
         HIPCHK(c, hipMemcpyAsync(&c->G->retry, &retry, 4, hipMemcpyHostToDevice, c->stream));
     }
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    HIPCHK(c, upload_mc_table(mc_table().tab, mc_table().edge));
+    {
+        static uint8_t both[2][256][32];
+        std::memcpy(both[0], mc_table(TSDF_MC_GENERATED).tab, sizeof both[0]);
+        std::memcpy(both[1], mc_table(TSDF_MC_LORENSEN).tab, sizeof both[1]);
+        HIPCHK(c, upload_mc_table(both, mc_table().edge));
+    }
     return TSDF_OK;
 }
 
@@ -1126,13 +1148,38 @@ int tsdf_create(const tsdf_params* p, tsdf_ctx** out) {
     return TSDF_OK;
 }
 
-static void set_origin(BatchDesc& D, uint32_t s, const double o[3]) {
-    D.s[s].ox = (float)o[0];
-    D.s[s].oy = (float)o[1];
-    D.s[s].oz = (float)o[2];
-    D.s[s].odx = o[0];
-    D.s[s].ody = o[1];
-    D.s[s].odz = o[2];
+// A scan's ray origin and sensor z axis (the world frame's z axis unless a pose gives it)
+struct ScanPose {
+    double o[3];
+    float z[3];
+};
+
+static ScanPose pose_of_origin(const double o[3]) {
+    return ScanPose{{o[0], o[1], o[2]}, {0.0f, 0.0f, 1.0f}};
+}
+
+// pose = (x, y, z, qx, qy, qz, qw): the z axis is the third column of the rotation of the
+// normalised quaternion, computed in double and rounded to float (the oracle does the same)
+static ScanPose pose_of(const double q[7]) {
+    ScanPose P = pose_of_origin(q);
+    const double n = std::sqrt(q[3] * q[3] + q[4] * q[4] + q[5] * q[5] + q[6] * q[6]);
+    const double x = q[3] / n, y = q[4] / n, z = q[5] / n, w = q[6] / n;
+    P.z[0] = (float)(2.0 * (x * z + w * y));
+    P.z[1] = (float)(2.0 * (y * z - w * x));
+    P.z[2] = (float)(1.0 - 2.0 * (x * x + y * y));
+    return P;
+}
+
+static void set_pose(BatchDesc& D, uint32_t s, const ScanPose& P) {
+    D.s[s].ox = (float)P.o[0];
+    D.s[s].oy = (float)P.o[1];
+    D.s[s].oz = (float)P.o[2];
+    D.s[s].odx = P.o[0];
+    D.s[s].ody = P.o[1];
+    D.s[s].odz = P.o[2];
+    D.s[s].zx = P.z[0];
+    D.s[s].zy = P.z[1];
+    D.s[s].zz = P.z[2];
 }
 
 // The pending batch's device staging buffer (host and single device scans are queued there).  A
@@ -1164,11 +1211,11 @@ static int pend_stage_buffer(tsdf_ctx* c) {
     return TSDF_OK;
 }
 
-// Append a staged scan of n points seen from origin to the pending batch; launch it when full.
-static int pend_push(tsdf_ctx* c, uint64_t n, const double origin[3]) {
+// Append a staged scan of n points seen from pose P to the pending batch; launch it when full.
+static int pend_push(tsdf_ctx* c, uint64_t n, const ScanPose& P) {
     BatchDesc& D = c->pend;
     const uint32_t s = D.n_scans;
-    set_origin(D, s, origin);
+    set_pose(D, s, P);
     D.s[s + 1].off = D.s[s].off + (uint32_t)n;
     D.n_scans = s + 1;
     c->n_points_in += n;
@@ -1183,10 +1230,8 @@ static int pend_room(tsdf_ctx* c, uint64_t n) {
     return TSDF_OK;
 }
 
-int tsdf_integrate(tsdf_ctx* c, const void* pts, uint64_t n, uint32_t point_step,
-                   uint32_t xyz_offset, int32_t xyz_is_f64, const double origin[3]) {
-    if (!c) return TSDF_EINVAL;
-    if ((!pts && n) || !origin) return fail(c, TSDF_EINVAL, "null argument");
+static int integrate_impl(tsdf_ctx* c, const void* pts, uint64_t n, uint32_t point_step,
+                          uint32_t xyz_offset, int32_t xyz_is_f64, const ScanPose& P) {
     const uint32_t need = xyz_is_f64 ? 24u : 12u;
     if (point_step < need || xyz_offset > point_step - need)
         return fail(c, TSDF_EINVAL, "point_step/xyz_offset inconsistent");
@@ -1234,11 +1279,28 @@ int tsdf_integrate(tsdf_ctx* c, const void* pts, uint64_t n, uint32_t point_step
                                  h, n * 12, hipMemcpyHostToDevice, c->stream));
     }
     HIPCHK(c, hipEventRecord(c->stage_done[b], c->stream));
-    return pend_push(c, n, origin);
+    return pend_push(c, n, P);
 }
 
-int tsdf_integrate_batch_device(tsdf_ctx* c, const float* d_xyz, const uint64_t* offs,
-                                uint32_t n_scans, const double* origins) {
+int tsdf_integrate(tsdf_ctx* c, const void* pts, uint64_t n, uint32_t point_step,
+                   uint32_t xyz_offset, int32_t xyz_is_f64, const double origin[3]) {
+    if (!c) return TSDF_EINVAL;
+    if ((!pts && n) || !origin) return fail(c, TSDF_EINVAL, "null argument");
+    return integrate_impl(c, pts, n, point_step, xyz_offset, xyz_is_f64, pose_of_origin(origin));
+}
+
+int tsdf_integrate_pose(tsdf_ctx* c, const void* pts, uint64_t n, uint32_t point_step,
+                        uint32_t xyz_offset, int32_t xyz_is_f64, const double pose[7]) {
+    if (!c) return TSDF_EINVAL;
+    if ((!pts && n) || !pose) return fail(c, TSDF_EINVAL, "null argument");
+    const double qn = pose[3] * pose[3] + pose[4] * pose[4] + pose[5] * pose[5] + pose[6] * pose[6];
+    if (!(qn > 0.0) || !std::isfinite(qn)) return fail(c, TSDF_EINVAL, "pose quaternion is zero");
+    return integrate_impl(c, pts, n, point_step, xyz_offset, xyz_is_f64, pose_of(pose));
+}
+
+// origins: 3 doubles per scan (pose_stride 3) or poses: 7 per scan (pose_stride 7)
+static int batch_device_impl(tsdf_ctx* c, const float* d_xyz, const uint64_t* offs,
+                             uint32_t n_scans, const double* origins, int pose_stride) {
     if (!c) return TSDF_EINVAL;
     if (!offs || !origins || (!d_xyz && n_scans)) return fail(c, TSDF_EINVAL, "null argument");
     for (uint32_t s = 0; s < n_scans; s++) {
@@ -1259,7 +1321,8 @@ int tsdf_integrate_batch_device(tsdf_ctx* c, const float* d_xyz, const uint64_t*
         const uint64_t b0 = offs[s];
         while (s < n_scans && D.n_scans < c->max_batch &&
                offs[s + 1] - b0 <= c->batch_points) {
-            set_origin(D, D.n_scans, origins + 3 * (uint64_t)s);
+            const double* q = origins + (uint64_t)pose_stride * s;
+            set_pose(D, D.n_scans, pose_stride == 7 ? pose_of(q) : pose_of_origin(q));
             D.s[D.n_scans + 1].off = (uint32_t)(offs[s + 1] - b0);
             D.n_scans++;
             s++;
@@ -1269,6 +1332,23 @@ int tsdf_integrate_batch_device(tsdf_ctx* c, const float* d_xyz, const uint64_t*
         c->n_points_in += D.s[D.n_scans].off;
     }
     return TSDF_OK;
+}
+
+int tsdf_integrate_batch_device(tsdf_ctx* c, const float* d_xyz, const uint64_t* offs,
+                                uint32_t n_scans, const double* origins) {
+    return batch_device_impl(c, d_xyz, offs, n_scans, origins, 3);
+}
+
+int tsdf_integrate_batch_device_pose(tsdf_ctx* c, const float* d_xyz, const uint64_t* offs,
+                                     uint32_t n_scans, const double* poses) {
+    if (c && poses)
+        for (uint32_t s = 0; s < n_scans; s++) {
+            const double* q = poses + 7 * (uint64_t)s;
+            const double qn = q[3] * q[3] + q[4] * q[4] + q[5] * q[5] + q[6] * q[6];
+            if (!(qn > 0.0) || !std::isfinite(qn))
+                return fail(c, TSDF_EINVAL, "pose %u: quaternion is zero", s);
+        }
+    return batch_device_impl(c, d_xyz, offs, n_scans, poses, 7);
 }
 
 // A single device scan joins the pending batch like a host scan: its points are copied into the
@@ -1289,7 +1369,7 @@ int tsdf_integrate_device(tsdf_ctx* c, const float* d_xyz, uint64_t n, const dou
                                  d_xyz, n * 12, hipMemcpyDeviceToDevice, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
     }
-    return pend_push(c, n, origin);
+    return pend_push(c, n, pose_of_origin(origin));
 }
 
 int tsdf_sync(tsdf_ctx* c) {
@@ -1506,8 +1586,21 @@ int tsdf_mc_table(uint8_t* out) {
     return TSDF_OK;
 }
 
+int tsdf_mc_table_of(int32_t table, uint8_t* out) {
+    if (!out || (table != TSDF_MC_GENERATED && table != TSDF_MC_LORENSEN)) return TSDF_EINVAL;
+    std::memcpy(out, mc_table(table).tab, sizeof(mc_table(table).tab));
+    return TSDF_OK;
+}
+
 int tsdf_extract_mesh(tsdf_ctx* c, float min_weight, float* tri, uint64_t cap, uint64_t* n_tri) {
+    return tsdf_extract_mesh_table(c, min_weight, TSDF_MC_GENERATED, tri, cap, n_tri);
+}
+
+int tsdf_extract_mesh_table(tsdf_ctx* c, float min_weight, int32_t table, float* tri, uint64_t cap,
+                            uint64_t* n_tri) {
     if (!c || !n_tri) return TSDF_EINVAL;
+    if (table != TSDF_MC_GENERATED && table != TSDF_MC_LORENSEN)
+        return fail(c, TSDF_EINVAL, "unknown marching-cubes table %d", table);
     uint64_t nb = 0;
     int rc = pool_bricks(c, &nb);
     if (rc) return rc;
@@ -1535,7 +1628,7 @@ int tsdf_extract_mesh(tsdf_ctx* c, float min_weight, float* tri, uint64_t cap, u
     if (e == hipSuccess) e = hipMalloc(&dc, nb * 4);
     if (e == hipSuccess) e = hipMemcpyAsync(dk, keys.data(), nb * 8, hipMemcpyHostToDevice, c->stream);
     if (e == hipSuccess)
-        e = launch_mesh_count(c->T, c->Pl, dk, (uint32_t)nb, min_weight, dc, c->stream);
+        e = launch_mesh_count(c->T, c->Pl, dk, (uint32_t)nb, min_weight, table, dc, c->stream);
     if (e == hipSuccess) e = hipMemcpyAsync(cnt.data(), dc, nb * 4, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e == hipSuccess) {
@@ -1551,8 +1644,8 @@ int tsdf_extract_mesh(tsdf_ctx* c, float min_weight, float* tri, uint64_t cap, u
         if (e == hipSuccess)
             e = hipMemcpyAsync(doff, off.data(), nb * 8, hipMemcpyHostToDevice, c->stream);
         if (e == hipSuccess)
-            e = launch_mesh_emit(c->T, c->Pl, dk, (uint32_t)nb, min_weight, c->R.vs, doff, dt,
-                                 c->stream);
+            e = launch_mesh_emit(c->T, c->Pl, dk, (uint32_t)nb, min_weight, table, c->R.vs, doff,
+                                 dt, c->stream);
         if (e == hipSuccess) e = hipMemcpyAsync(tri, dt, total * 36, hipMemcpyDeviceToHost, c->stream);
         if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     }

@@ -96,6 +96,9 @@ struct RayConst {
     // TSDF_SEM_VDBFUSION_F64: vs and 1/vs in double, and the gate's threshold on
     // the squared distance behind the hit: (float)sqrt(d2) < tau  <=>  d2 < gate_d2
     double vs_d, inv_s_d, gate_d2;
+    // Voxblox 1/z^2 sample weights (tsdf_params.depth_weight; sem 3 internally, with per-sample
+    // weights in Work::smw)
+    int depth_w;
 };
 
 // fp32 pseudo-angle of (x, y) in [0, 4), monotone in atan2 (include/tsdf_hip.h tsdf_sector_of):
@@ -123,13 +126,16 @@ __host__ __device__ inline bool in_sector(const RayConst& R, float dx, float dy)
 // cover scan s, RPB rays each.  The host fills a BatchDesc; launch() uploads its n_scans + 1 used
 // records to a device ring slot, and the kernels get a BatchRef to them (a batch of up to 512
 // scans does not fit the kernel-argument segment).
+// zx, zy, zz: the sensor's z axis in the world frame (Voxblox's 1/z^2 weight, RayConst::depth_w)
 struct ScanRec {
     uint32_t off, blk;
     float ox, oy, oz;
-    uint32_t pad;
+    float zx;
     double odx, ody, odz;
+    float zy, zz;
+    uint32_t pad[2];
 };
-static_assert(sizeof(ScanRec) == 48, "ScanRec layout");
+static_assert(sizeof(ScanRec) == 64, "ScanRec layout");
 struct BatchDesc {
     uint32_t n_scans;
     uint32_t n_blocks;
@@ -166,6 +172,7 @@ struct Work {
     uint32_t* blk_n; // n_blocks * 2: runs in each list
     uint4* fb;       // fallback pairs: (tidx, scan, rank, 0)
     uint2* smp;  // x = truncated sdf (f32 bits), y = scan << 9 | local voxel
+    float* smw;  // Voxblox 1/z^2 (sem 3): each sample's weight, same index as smp
     uint4* active;  // (h, slot, toff, cnt) per active brick (k_compact)
     uint4* active_ord;  // the same records, largest size class first (k_order; k_integrate's list)
     uint32_t* ord_hist; // k_order: per (slice, size class) counts, then first positions
@@ -308,12 +315,13 @@ hipError_t launch_os_decode(const uint8_t* d_packets, uint32_t n_packets, const 
 hipError_t launch_os_xyz(const uint32_t* d_range, uint64_t n, const float* d_dir,
                          const float* d_off, const OsPose& P, float* d_xyz, hipStream_t st);
 // marching cubes (tsdf_mesh.hip)
-hipError_t upload_mc_table(const uint8_t tab[256][32], const uint8_t edge[12][2]);
+// both case tables (TSDF_MC_GENERATED, TSDF_MC_LORENSEN); `tab` selects one per launch
+hipError_t upload_mc_table(const uint8_t tab[2][256][32], const uint8_t edge[12][2]);
 hipError_t launch_mesh_count(const Table& T, const Pool& Pl, const uint64_t* d_keys, uint32_t nb,
-                             float min_weight, uint32_t* d_counts, hipStream_t st);
+                             float min_weight, int tab, uint32_t* d_counts, hipStream_t st);
 hipError_t launch_mesh_emit(const Table& T, const Pool& Pl, const uint64_t* d_keys, uint32_t nb,
-                            float min_weight, float vs, const uint64_t* d_offsets, float* d_tri,
-                            hipStream_t st);
+                            float min_weight, int tab, float vs, const uint64_t* d_offsets,
+                            float* d_tri, hipStream_t st);
 hipError_t launch_fill_u32(uint32_t* p, uint32_t v, uint64_t n, hipStream_t st);
 hipError_t launch_fill_u64(uint64_t* p, uint64_t v, uint64_t n, hipStream_t st);
 

@@ -86,7 +86,9 @@ template <int SEM, int MAXS, bool FUSED>
 __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchRef D, Table T, Work Wk, Pool Pl,
                                                           Globals* G, int parity, RayConst R) {
     constexpr int NSLOT = FUSED ? INT_SPT * SPAN : INT_PER;  // register-cached samples per thread
-    typedef typename std::conditional<SEM == 1, unsigned long long, uint32_t>::type CellB;
+    constexpr bool VB = SEM == 1 || SEM == 3;  // Voxblox fuse (3: per-sample weights in Work::smw)
+    constexpr int NW = SEM == 3 ? NSLOT : 1;    // register-cached sample weights per thread
+    typedef typename std::conditional<VB, unsigned long long, uint32_t>::type CellB;
     __shared__ unsigned long long cA[INT_CAP];  // live cell: sum of trunc(s w * 2^32)
     __shared__ CellB cB[INT_CAP];               // live cell: sample count / sum of trunc(w 2^32)
     const float tau = R.tau;
@@ -124,6 +126,7 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchRef D, Table T, 
     const CellT* cells = reinterpret_cast<const CellT*>(T.cell);
     struct BrickRegs {
         uint2 c[NSLOT];
+        float cw[NW];
         float s0, s1, w0, w1;
         CellT cell, cell2;
     };
@@ -159,6 +162,7 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchRef D, Table T, 
                 const uint32_t i = tid + j * INT_THREADS;
                 // base + i >= max_smp: capacity overflow (reported by k_compact)
                 B.c[j] = (i < n && base + i < Wk.max_smp) ? Wk.smp[base + i] : make_uint2(0u, ~0u);
+                if constexpr (SEM == 3) B.cw[j] = (i < n && base + i < Wk.max_smp) ? Wk.smw[base + i] : 0.0f;
             }
         }
         // two walks: absolute position of the brick's scan-tid samples -> relative to its segment
@@ -208,8 +212,11 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchRef D, Table T, 
         }
         const uint32_t h = cur.x, n = cur.w, base = cur.z;
         uint2 c[NSLOT];
+        float cw[NW];
 #pragma unroll
         for (int j = 0; j < NSLOT; j++) c[j] = B.c[j];
+#pragma unroll
+        for (int j = 0; j < NW; j++) cw[j] = B.cw[j];
         // samples [cq, cq + INT_CAP) (FUSED: spans [cq, cq + INT_SCH)) are in c[] (uniform)
         uint32_t cq = FUSED ? base : 0u;
         const uint32_t pend = FUSED ? base + n : 0u;  // FUSED: the brick's span end
@@ -224,6 +231,7 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchRef D, Table T, 
                 for (int j = 0; j < INT_PER; j++) {
                     const uint32_t i = q + tid + j * INT_THREADS;
                     c[j] = (i < n && base + i < Wk.max_smp) ? Wk.smp[base + i] : make_uint2(0u, ~0u);
+                    if constexpr (SEM == 3) cw[j] = (i < n && base + i < Wk.max_smp) ? Wk.smw[base + i] : 0.0f;
                 }
             }
         };
@@ -351,8 +359,10 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchRef D, Table T, 
                         const uint32_t l = c[j].y & 511u;
                         const uint32_t cell = sBase[l] + MASK_POPC(sMask[l] & (((MaskT)1 << w) - 1));
                         const float sv = __uint_as_float(c[j].x);
-                        if constexpr (SEM == 1) {
-                            const float wv = vb_weight(R, sv);
+                        if constexpr (VB) {
+                            float wv;
+                            if constexpr (SEM == 3) wv = cw[j];
+                            else wv = vb_weight(R, 1.0f, sv);
                             const long long fa = (long long)((sv * wv) * 4294967296.0f);
                             const long long fb = (long long)(wv * 4294967296.0f);
                             atomicAdd(&cA[cell], (unsigned long long)fa);
@@ -388,7 +398,7 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchRef D, Table T, 
                 for (uint32_t j = tid; j < ncell; j += INT_THREADS) {
                     const long long av = (long long)cA[j];
                     const float af = (float)((double)av * (1.0 / 4294967296.0));
-                    if constexpr (SEM == 1)
+                    if constexpr (VB)
                         cF[j] = make_float2(af, (float)((double)(long long)cB[j] * (1.0 / 4294967296.0)));
                     else
                         cF[j] = make_float2(af, (float)cB[j]);
@@ -462,7 +472,7 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchRef D, Table T, 
                     for (uint32_t k = 0; k < rem; k += 2) {
                         const uint64_t na = cV[min(cell + k + 2, INT_CAP - 1u)];
                         uint64_t nb;
-                        if constexpr (SEM == 1) {
+                        if constexpr (VB) {
                             vb_fuse(va, s, wt);
                             nb = cV[min(cell + k + 3, INT_CAP - 1u)];
                             float s2 = s, w2 = wt;
@@ -564,10 +574,16 @@ static void integrate_sem(const BatchRef& D, const RayConst& R, const Table& T, 
 template <bool FUSED>
 static void integrate_mode(const BatchRef& D, const RayConst& R, const Table& T, const Work& Wk,
                            const Pool& Pl, Globals* G, int parity, bool big, hipStream_t st) {
-    // SEM 2 (VDBFusion at double precision) fuses like SEM 0
+    // SEM 2 (VDBFusion at double precision) fuses like SEM 0; SEM 3 (Voxblox 1/z^2) never takes
+    // the single walk (tsdf_capi.cpp)
     if (R.sem == 1) {
         if (big) integrate_sem<1, MAX_BATCH, FUSED>(D, R, T, Wk, Pl, G, parity, st);
         else integrate_sem<1, 64, FUSED>(D, R, T, Wk, Pl, G, parity, st);
+    } else if (R.sem == 3) {
+        if constexpr (!FUSED) {
+            if (big) integrate_sem<3, MAX_BATCH, false>(D, R, T, Wk, Pl, G, parity, st);
+            else integrate_sem<3, 64, false>(D, R, T, Wk, Pl, G, parity, st);
+        }
     } else {
         if (big) integrate_sem<0, MAX_BATCH, FUSED>(D, R, T, Wk, Pl, G, parity, st);
         else integrate_sem<0, 64, FUSED>(D, R, T, Wk, Pl, G, parity, st);

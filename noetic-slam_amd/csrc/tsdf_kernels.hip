@@ -695,6 +695,7 @@ __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) v
     __shared__ uint16_t s_wpre[PLC_WORDS]; // run starts in the words before
     __shared__ float st_s[PLC_STAGE];      // staged samples
     __shared__ uint16_t st_l[PLC_STAGE];
+    __shared__ float st_w[SEM == 3 ? PLC_STAGE : 1];  // Voxblox 1/z^2: the samples' weights
     __shared__ uint32_t s_nst;             // staged samples (end of the last staged run)
 #ifdef TSDF_PLC_PHASE  // diagnostic build: thread 0's clock at the phase boundaries
     unsigned long long pt[6];
@@ -885,8 +886,10 @@ __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) v
                 if (stage) {
                     st_s[lpos + w] = s;
                     st_l[lpos + w] = (uint16_t)l;
+                    if constexpr (SEM == 3) st_w[lpos + w] = vb_weight(R, r.w0, s);
                 } else if (st && pos != NO_PAIR && pos + w < Wk.max_smp) {
                     Wk.smp[pos + w] = make_uint2(__float_as_uint(s), (t << 9) | l);
+                    if constexpr (SEM == 3) Wk.smw[pos + w] = vb_weight(R, r.w0, s);
                 }
                 w += g ? 1u : 0u;
                 if (!Walk<SEM>::step(r)) break;
@@ -910,8 +913,10 @@ __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) v
                     if (lpos != NO_PAIR && lpos + w < (uint32_t)PLC_STAGE) {
                         st_s[lpos + w] = s;
                         st_l[lpos + w] = (uint16_t)l;
+                        if constexpr (SEM == 3) st_w[lpos + w] = vb_weight(R, r.w0, s);
                     } else if (pos != NO_PAIR && pos + w < Wk.max_smp) {
                         Wk.smp[pos + w] = make_uint2(__float_as_uint(s), (t << 9) | l);
+                        if constexpr (SEM == 3) Wk.smw[pos + w] = vb_weight(R, r.w0, s);
                     }
                 }
                 w++;
@@ -936,8 +941,10 @@ __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) v
         const uint32_t b = s_base[slot];
         if (b != NO_PAIR) {
             const uint32_t dst = b + (j - s_loff[slot]);
-            if (dst < Wk.max_smp)
+            if (dst < Wk.max_smp) {
                 Wk.smp[dst] = make_uint2(__float_as_uint(st_s[j]), (t << 9) | st_l[j]);
+                if constexpr (SEM == 3) Wk.smw[dst] = st_w[j];
+            }
         }
     }
 #ifdef TSDF_PLC_PHASE
@@ -1047,7 +1054,8 @@ static int grid_for(uint64_t items, int per_block, int cap) {
 // (tsdf_capi.cpp) interleaves the cross-batch waits between them.
 hipError_t launch_count(const float* d_xyz, const BatchRef& D, const RayConst& R, const Table& T,
                         const Work& Wk, Globals* G, int parity, hipStream_t st) {
-    if (R.sem == 1) k_count<1><<<D.n_blocks, CNT_THREADS, 0, st>>>(d_xyz, D, R, T, Wk, G, parity);
+    // sem 3 (Voxblox 1/z^2) counts with Walk<1>: the weight only matters where it is stored
+    if (R.sem == 1 || R.sem == 3) k_count<1><<<D.n_blocks, CNT_THREADS, 0, st>>>(d_xyz, D, R, T, Wk, G, parity);
     else if (R.sem == 2) k_count<2><<<D.n_blocks, CNT_THREADS, 0, st>>>(d_xyz, D, R, T, Wk, G, parity);
     else k_count<0><<<D.n_blocks, CNT_THREADS, 0, st>>>(d_xyz, D, R, T, Wk, G, parity);
     return hipGetLastError();
@@ -1067,6 +1075,7 @@ hipError_t launch_compact(const BatchRef& D, const Table& T, const Work& Wk, Glo
 hipError_t launch_place(const float* d_xyz, const BatchRef& D, const RayConst& R, const Table& T,
                         const Work& Wk, Globals* G, int parity, hipStream_t st) {
     if (R.sem == 1) k_place<1><<<2 * D.n_blocks, PLC_THREADS, 0, st>>>(d_xyz, D, R, T, Wk, G, parity);
+    else if (R.sem == 3) k_place<3><<<2 * D.n_blocks, PLC_THREADS, 0, st>>>(d_xyz, D, R, T, Wk, G, parity);
     else if (R.sem == 2) k_place<2><<<2 * D.n_blocks, PLC_THREADS, 0, st>>>(d_xyz, D, R, T, Wk, G, parity);
     else k_place<0><<<2 * D.n_blocks, PLC_THREADS, 0, st>>>(d_xyz, D, R, T, Wk, G, parity);
     return hipGetLastError();

@@ -19,7 +19,7 @@
 
 namespace tsdf {
 
-__constant__ uint8_t c_mc[256][32];  // [case][0] = triangles, then 3 edge ids per triangle
+__constant__ uint8_t c_mc[2][256][32];  // per table (TSDF_MC_*): [case][0] = triangles, then 3 edge ids each
 __constant__ uint8_t c_edge[12][2];  // edge -> corners (a, b), b = a | axis bit
 
 constexpr int MESH_THREADS = 512;
@@ -75,7 +75,7 @@ __device__ __forceinline__ int mesh_case(const float* s_S, const uint8_t* s_ok, 
 __global__ __launch_bounds__(MESH_THREADS) void k_mesh_count(Table T, Pool Pl,
                                                             const uint64_t* __restrict__ keys,
                                                             uint32_t nb, float min_weight,
-                                                            uint32_t* __restrict__ counts) {
+                                                            uint32_t* __restrict__ counts, int tab) {
     __shared__ float s_S[TILE * TILE * TILE];
     __shared__ uint8_t s_ok[TILE * TILE * TILE];
     __shared__ uint32_t s_slot[8];
@@ -85,7 +85,7 @@ __global__ __launch_bounds__(MESH_THREADS) void k_mesh_count(Table T, Pool Pl,
         mesh_tile(T, Pl, keys[b], min_weight, s_S, s_ok, s_slot);
         float S[8];
         const int k = mesh_case(s_S, s_ok, threadIdx.x, S);
-        const uint32_t nt = k >= 0 ? c_mc[k][0] : 0u;
+        const uint32_t nt = k >= 0 ? c_mc[tab][k][0] : 0u;
         const uint32_t w = wave_sum<uint32_t>(nt);
         if ((threadIdx.x & 63) == 0 && w) atomicAdd(&s_sum, w);
         __syncthreads();
@@ -97,7 +97,7 @@ __global__ __launch_bounds__(MESH_THREADS) void k_mesh_count(Table T, Pool Pl,
 __global__ __launch_bounds__(MESH_THREADS) void k_mesh_emit(Table T, Pool Pl,
                                                            const uint64_t* __restrict__ keys,
                                                            uint32_t nb, float min_weight, float vs,
-                                                           const uint64_t* __restrict__ offsets,
+                                                           const uint64_t* __restrict__ offsets, int tab,
                                                            float* __restrict__ tri) {
     __shared__ float s_S[TILE * TILE * TILE];
     __shared__ uint8_t s_ok[TILE * TILE * TILE];
@@ -110,7 +110,7 @@ __global__ __launch_bounds__(MESH_THREADS) void k_mesh_emit(Table T, Pool Pl,
         float S[8];
         const int l = threadIdx.x;
         const int k = mesh_case(s_S, s_ok, l, S);
-        const uint32_t nt = k >= 0 ? c_mc[k][0] : 0u;
+        const uint32_t nt = k >= 0 ? c_mc[tab][k][0] : 0u;
         // exclusive scan of the lanes' triangle counts (cube order)
         const uint32_t incl = wave_incl_scan(nt);
         if (lane == 63) s_w[wid] = incl;
@@ -126,7 +126,7 @@ __global__ __launch_bounds__(MESH_THREADS) void k_mesh_emit(Table T, Pool Pl,
             float* out = tri + 9 * (offsets[b] + off + incl - nt);
             for (uint32_t t = 0; t < nt; t++) {
                 for (int j = 0; j < 3; j++) {
-                    const int ed = c_mc[k][1 + 3 * t + j];
+                    const int ed = c_mc[tab][k][1 + 3 * t + j];
                     const int a = c_edge[ed][0], bb = c_edge[ed][1];
                     const int ax = (a ^ bb) == 1 ? 0 : ((a ^ bb) == 2 ? 1 : 2);
                     const float tt = S[a] / (S[a] - S[bb]);
@@ -145,26 +145,27 @@ __global__ __launch_bounds__(MESH_THREADS) void k_mesh_emit(Table T, Pool Pl,
     }
 }
 
-hipError_t upload_mc_table(const uint8_t tab[256][32], const uint8_t edge[12][2]) {
-    hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(c_mc), tab, 256 * 32);
+hipError_t upload_mc_table(const uint8_t tab[2][256][32], const uint8_t edge[12][2]) {
+    hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(c_mc), tab, 2 * 256 * 32);
     if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(c_edge), edge, 12 * 2);
     return e;
 }
 
 hipError_t launch_mesh_count(const Table& T, const Pool& Pl, const uint64_t* d_keys, uint32_t nb,
-                             float min_weight, uint32_t* d_counts, hipStream_t st) {
+                             float min_weight, int tab, uint32_t* d_counts, hipStream_t st) {
     if (nb == 0) return hipSuccess;
     const uint32_t grid = nb < 4096u ? nb : 4096u;
-    k_mesh_count<<<grid, MESH_THREADS, 0, st>>>(T, Pl, d_keys, nb, min_weight, d_counts);
+    k_mesh_count<<<grid, MESH_THREADS, 0, st>>>(T, Pl, d_keys, nb, min_weight, d_counts, tab);
     return hipGetLastError();
 }
 
 hipError_t launch_mesh_emit(const Table& T, const Pool& Pl, const uint64_t* d_keys, uint32_t nb,
-                            float min_weight, float vs, const uint64_t* d_offsets, float* d_tri,
-                            hipStream_t st) {
+                            float min_weight, int tab, float vs, const uint64_t* d_offsets,
+                            float* d_tri, hipStream_t st) {
     if (nb == 0) return hipSuccess;
     const uint32_t grid = nb < 4096u ? nb : 4096u;
-    k_mesh_emit<<<grid, MESH_THREADS, 0, st>>>(T, Pl, d_keys, nb, min_weight, vs, d_offsets, d_tri);
+    k_mesh_emit<<<grid, MESH_THREADS, 0, st>>>(T, Pl, d_keys, nb, min_weight, vs, d_offsets, tab,
+                                               d_tri);
     return hipGetLastError();
 }
 

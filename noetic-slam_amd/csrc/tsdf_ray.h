@@ -198,6 +198,7 @@ struct VbState {
     int vx, vy, vz;
     int sx, sy, sz;
     int rem;               // steps left (RayCaster: ray_length_in_steps - current_step)
+    float w0;              // getVoxelWeight: 1, or 1 / z^2 (tsdf_params.depth_weight)
 };
 
 __device__ __forceinline__ void vb_axis(float ss, float es, int& v, int& st, float& tn, float& td,
@@ -213,8 +214,9 @@ __device__ __forceinline__ void vb_axis(float ss, float es, int& v, int& st, flo
 }
 
 // isPointValid + RayCaster setup; false when the ray is dropped.
-__device__ __forceinline__ bool vb_init(const RayConst& R, float ox, float oy, float oz, float px,
-                                        float py, float pz, VbState& r) {
+__device__ __forceinline__ bool vb_init(const RayConst& R, const BatchRef& D, uint32_t t,
+                                        float px, float py, float pz, VbState& r) {
+    const float ox = D.s[t].ox, oy = D.s[t].oy, oz = D.s[t].oz;
     const float dx = px - ox, dy = py - oy, dz = pz - oz;
     if (!in_sector(R, dx, dy)) return false;  // another GPU's azimuth sector
     const float depth = __builtin_sqrtf(dx * dx + (dy * dy + dz * dz));
@@ -252,6 +254,13 @@ __device__ __forceinline__ bool vb_init(const RayConst& R, float ox, float oy, f
     vb_axis(sy * R.inv_vs, ey * R.inv_vs, r.vy, r.sy, r.tny, r.tdy, steps);
     vb_axis(sz * R.inv_vs, ez * R.inv_vs, r.vz, r.sz, r.tnz, r.tdz, steps);
     r.rem = min(steps, MAX_DDA_STEPS - 1);
+    // TsdfIntegratorBase::getVoxelWeight: 1 / z^2 of the point's sensor-frame depth z (the scan's
+    // z axis dotted with p - o, Eigen's x + (y + z)); |z| <= kEpsilon (1e-6) gives 0
+    r.w0 = 1.0f;
+    if (R.depth_w) {
+        const float z = fabsf(D.s[t].zx * dx + (D.s[t].zy * dy + D.s[t].zz * dz));
+        r.w0 = z > 1e-6f ? 1.0f / (z * z) : 0.0f;
+    }
     r.px = px;
     r.dx = dx;
     r.dy = dy;
@@ -260,9 +269,9 @@ __device__ __forceinline__ bool vb_init(const RayConst& R, float ox, float oy, f
     return true;
 }
 
-// updateTsdfVoxel's weight for a sample (use_const_weight, optional dropoff)
-__device__ __forceinline__ float vb_weight(const RayConst& R, float sdf) {
-    float w = 1.0f;
+// updateTsdfVoxel's weight for a sample: the ray's getVoxelWeight w0, then the optional dropoff
+__device__ __forceinline__ float vb_weight(const RayConst& R, float w0, float sdf) {
+    float w = w0;
     if (R.dropoff && sdf < -R.vs) {
         w = (w * (R.tau + sdf)) / R.tau_m_vs;
         w = w > 0.0f ? w : 0.0f;
@@ -282,7 +291,7 @@ __device__ __forceinline__ bool vb_sample(const RayConst& R, float ox, float oy,
     const float proj = (ax * r.dx + (ay * r.dy + az * r.dz)) / r.depth;
     const float sdf = r.depth - proj;
     s = sdf;
-    return inl && vb_weight(R, sdf) >= VB_MIN_WEIGHT;
+    return inl && vb_weight(R, r.w0, sdf) >= VB_MIN_WEIGHT;
 }
 
 // nextRayIndex's advance: the first minimum of t_next (Eigen minCoeff) steps by its sign
@@ -363,7 +372,7 @@ struct Walk<1> {  // TSDF_SEM_VOXBLOX
     typedef VbState State;
     __device__ static __forceinline__ bool init(const RayConst& R, const BatchRef& D, uint32_t t,
                                                 float px, float py, float pz, State& r) {
-        return vb_init(R, D.s[t].ox, D.s[t].oy, D.s[t].oz, px, py, pz, r);
+        return vb_init(R, D, t, px, py, pz, r);
     }
     __device__ static __forceinline__ bool gate(const RayConst& R, float ox, float oy, float oz,
                                                 const State& r, bool check = true) {
@@ -391,6 +400,11 @@ struct Walk<1> {  // TSDF_SEM_VOXBLOX
     __device__ static __forceinline__ bool step(State& r) { return vb_step(r); }
     __device__ static __forceinline__ bool step_sel(State& r) { return vb_step_sel(r); }
 };
+
+// Voxblox with the 1/z^2 weight (internal sem 3): the same walk; k_place stores every sample's
+// weight (Work::smw) because k_integrate cannot recompute it from the sample
+template <>
+struct Walk<3> : Walk<1> {};
 
 // ------------------------------------------------------------------------------------------------
 // VDBFusion at upstream's own precisions (TSDF_SEM_VDBFUSION_F64; the bit-exact twin of

@@ -16,7 +16,7 @@ STATUS_NAMES = {
     TSDF_EHIP: "TSDF_EHIP", TSDF_ENODEV: "TSDF_ENODEV", TSDF_EOVERFLOW: "TSDF_EOVERFLOW",
 }
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 TILE_WORDS = 1028  # TSDF_TILE_WORDS: u32 words of one border-brick tile
 MAX_WORLD = 64
 SEM_VDBFUSION = 0
@@ -29,6 +29,7 @@ SEMANTICS = {"vdbfusion": SEM_VDBFUSION, "voxblox": SEM_VOXBLOX,
 KERNEL_KINDS = ("count", "compact", "place", "integrate", "walk", "spans")
 WALK_TWO = 0     # tsdf_params.walk: k_count + k_place (default)
 WALK_SINGLE = 1  # k_walk + k_spans when the band allows it
+MC_TABLES = {"generated": 0, "lorensen": 1}  # TSDF_MC_GENERATED, TSDF_MC_LORENSEN
 
 
 class TsdfParams(C.Structure):
@@ -58,6 +59,8 @@ class TsdfParams(C.Structure):
         ("max_bricks_hard", C.c_uint64),
         # ABI v5
         ("walk", C.c_int32),
+        # ABI v6
+        ("depth_weight", C.c_int32),
     ]
 
 
@@ -112,8 +115,10 @@ SIGNATURES = {
     "tsdf_destroy": (None, [P]),
     "tsdf_last_error": (C.c_char_p, [P]),
     "tsdf_integrate": (C.c_int, [P, P, C.c_uint64, C.c_uint32, C.c_uint32, C.c_int32, D3]),
+    "tsdf_integrate_pose": (C.c_int, [P, P, C.c_uint64, C.c_uint32, C.c_uint32, C.c_int32, D3]),
     "tsdf_integrate_device": (C.c_int, [P, P, C.c_uint64, D3]),
     "tsdf_integrate_batch_device": (C.c_int, [P, P, U64P, C.c_uint32, D3]),
+    "tsdf_integrate_batch_device_pose": (C.c_int, [P, P, U64P, C.c_uint32, D3]),
     "tsdf_sync": (C.c_int, [P]),
     "tsdf_query_dense": (C.c_int, [P, I3, I3, FP, FP]),
     "tsdf_num_bricks": (C.c_int, [P, U64P]),
@@ -132,6 +137,8 @@ SIGNATURES = {
     "tsdf_border_merge_device": (C.c_int, [P, P, U64P, C.c_uint32]),
     "tsdf_extract_mesh": (C.c_int, [P, C.c_float, FP, C.c_uint64, U64P]),
     "tsdf_mc_table": (C.c_int, [C.POINTER(C.c_uint8)]),
+    "tsdf_extract_mesh_table": (C.c_int, [P, C.c_float, C.c_int32, FP, C.c_uint64, U64P]),
+    "tsdf_mc_table_of": (C.c_int, [C.c_int32, C.POINTER(C.c_uint8)]),
     "tsdf_os_packet_bytes": (C.c_int, [C.POINTER(OsFormat), C.POINTER(C.c_uint32)]),
     "tsdf_os_decode_device": (C.c_int, [P, C.POINTER(OsFormat), P, C.c_uint32, P, P, P, P]),
     "tsdf_os_cartesian_device": (C.c_int, [P, P, C.c_uint64, P, P, C.POINTER(C.c_double), P]),

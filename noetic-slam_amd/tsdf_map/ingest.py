@@ -95,8 +95,9 @@ def cloud_xyz_layout(cloud):
 
 
 def ingest_bag(volume, path, cloud_topic=DLIO_CLOUD, pose_topic=DLIO_POSE, max_gap_ms=50.0):
-    """Integrate every cloud of `cloud_topic` (world frame) from the pose track's position at its
-    stamp.  Returns (integrated, skipped) cloud counts."""
+    """Integrate every cloud of `cloud_topic` (world frame) from the pose track's pose at its stamp
+    (position: the ray origin; orientation: the sensor axes).  Returns (integrated, skipped)
+    cloud counts."""
     bag = rosbag.BagReader(path)
     track = load_poses(bag, pose_topic)
     done = skipped = 0
@@ -107,7 +108,9 @@ def ingest_bag(volume, path, cloud_topic=DLIO_CLOUD, pose_topic=DLIO_POSE, max_g
             skipped += 1
             continue
         off, f64 = cloud_xyz_layout(c)
-        volume.integrate_cloud(c.data, c.width * c.height, c.point_step, off, pose[0],
-                               xyz_is_f64=f64)
+        # the full pose (x, y, z, qx, qy, qz, qw): the position is the ray origin, the
+        # orientation gives Voxblox's sensor z axis (tsdf_integrate_pose)
+        volume.integrate_cloud(c.data, c.width * c.height, c.point_step, off,
+                               np.concatenate([pose[0], pose[1]]), xyz_is_f64=f64)
         done += 1
     return done, skipped

@@ -37,7 +37,39 @@ def _origin_of(extrinsic):
         return np.ascontiguousarray(e.reshape(3))
     if e.shape == (4, 4):
         return np.ascontiguousarray(e[:3, 3])
-    raise ValueError("origin/extrinsic must be a (3,) array or a (4,4) matrix")
+    if e.shape == (7,):
+        return np.ascontiguousarray(e[:3])
+    raise ValueError("origin/extrinsic must be a (3,) array, a (7,) pose or a (4,4) matrix")
+
+
+def _quat_of(R):
+    """(qx, qy, qz, qw) of a 3x3 rotation (Shepperd's method, float64)."""
+    R = np.asarray(R, np.float64)
+    t = R[0, 0] + R[1, 1] + R[2, 2]
+    if t > 0:
+        s = math.sqrt(t + 1.0) * 2
+        return np.array([(R[2, 1] - R[1, 2]) / s, (R[0, 2] - R[2, 0]) / s, (R[1, 0] - R[0, 1]) / s,
+                         0.25 * s])
+    i = int(np.argmax([R[0, 0], R[1, 1], R[2, 2]]))
+    j, k = (i + 1) % 3, (i + 2) % 3
+    s = math.sqrt(1.0 + R[i, i] - R[j, j] - R[k, k]) * 2
+    q = np.empty(4)
+    q[i] = 0.25 * s
+    q[j] = (R[j, i] + R[i, j]) / s
+    q[k] = (R[k, i] + R[i, k]) / s
+    q[3] = (R[k, j] - R[j, k]) / s
+    return q
+
+
+def _pose_of(extrinsic):
+    """The (7,) pose (x, y, z, qx, qy, qz, qw) of a 4x4 extrinsic or a 7-vector; None for a bare
+    (3,) origin."""
+    e = np.asarray(extrinsic, dtype=np.float64)
+    if e.shape == (7,):
+        return np.ascontiguousarray(e)
+    if e.shape == (4, 4):
+        return np.ascontiguousarray(np.concatenate([e[:3, 3], _quat_of(e[:3, :3])]))
+    return None
 
 
 def _d3(a):
@@ -55,7 +87,7 @@ class TSDFVolume:
                  max_range=math.inf, max_bricks=1 << 20, max_points=1 << 18, device_id=0,
                  max_batch=32, pipeline=False, semantics="vdbfusion", allow_clear=True,
                  use_weight_dropoff=True, max_weight=10000.0, n_sectors=0, sector=0,
-                 sector_yaw0=0.0, max_bricks_hard=0, walk="two"):
+                 sector_yaw0=0.0, max_bricks_hard=0, walk="two", use_const_weight=True):
         self._lib = lib
         if semantics not in _abi.SEMANTICS:
             raise ValueError("semantics must be one of %s" % sorted(_abi.SEMANTICS))
@@ -82,6 +114,8 @@ class TSDFVolume:
         # "two": k_count + k_place (default); "single": rays walked once (k_walk + k_spans) when the
         # band allows it
         p.walk = {"two": _abi.WALK_TWO, "single": _abi.WALK_SINGLE}[walk]
+        # Voxblox getVoxelWeight: 1 (use_const_weight) or 1 / z^2 of the sensor-frame depth
+        p.depth_weight = 0 if use_const_weight else 1
         self.params = p
         self.semantics = semantics
         rc = lib.tsdf_create(C.byref(p), C.byref(self._ctx))
@@ -125,9 +159,15 @@ class TSDFVolume:
         if pts.dtype not in (np.float32, np.float64):
             raise TypeError("points dtype must be np.float32 or np.float64")
         pts = np.ascontiguousarray(pts)
-        o = _origin_of(extrinsic)
         is64 = pts.dtype == np.float64
         step = 24 if is64 else 12
+        pose = _pose_of(extrinsic)
+        if pose is not None:  # the sensor's orientation too (Voxblox 1/z^2 weights)
+            self._check(self._lib.tsdf_integrate_pose(self._ctx, pts.ctypes.data_as(C.c_void_p),
+                                                      pts.shape[0], step, 0, 1 if is64 else 0,
+                                                      _d3(pose)), "integrate_pose")
+            return
+        o = _origin_of(extrinsic)
         self._check(self._lib.tsdf_integrate(self._ctx, pts.ctypes.data_as(C.c_void_p),
                                              pts.shape[0], step, 0, 1 if is64 else 0, _d3(o)),
                     "integrate")
@@ -137,6 +177,13 @@ class TSDFVolume:
         buf = np.frombuffer(data, dtype=np.uint8)
         if buf.size < n * point_step:
             raise ValueError("buffer smaller than n * point_step")
+        pose = _pose_of(origin)
+        if pose is not None:
+            self._check(self._lib.tsdf_integrate_pose(self._ctx, buf.ctypes.data_as(C.c_void_p),
+                                                      int(n), int(point_step), int(xyz_offset),
+                                                      1 if xyz_is_f64 else 0, _d3(pose)),
+                        "integrate_cloud")
+            return
         o = _origin_of(origin)
         self._check(self._lib.tsdf_integrate(self._ctx, buf.ctypes.data_as(C.c_void_p), int(n),
                                              int(point_step), int(xyz_offset),
@@ -161,19 +208,21 @@ class TSDFVolume:
                                                w.ctypes.data_as(_abi.FP)), "query_dense")
         return s, w
 
-    def extract_triangle_mesh(self, fill_holes=True, min_weight=0.0):
+    def extract_triangle_mesh(self, fill_holes=True, min_weight=0.0, table="generated"):
         """VDBVolume.extract_triangle_mesh: (vertices (3T, 3) float32, triangles (T, 3) int64) —
         marching cubes over every cube of 8 observed voxels (W > 0, W >= min_weight), as a soup
         (each triangle owns its 3 vertices).  fill_holes is accepted for API compatibility; cubes
-        with an unobserved voxel are never meshed."""
+        with an unobserved voxel are never meshed.  table: "generated" (face-consistent, the
+        default) or "lorensen" (the classic table's ambiguity rule, VDBFusion's)."""
+        tab = _abi.MC_TABLES[table]
         n = C.c_uint64()
-        self._check(self._lib.tsdf_extract_mesh(self._ctx, float(min_weight), None, 0,
-                                                C.byref(n)), "extract_mesh")
+        self._check(self._lib.tsdf_extract_mesh_table(self._ctx, float(min_weight), tab, None, 0,
+                                                      C.byref(n)), "extract_mesh")
         t = np.empty((n.value, 9), np.float32)
         if n.value:
-            self._check(self._lib.tsdf_extract_mesh(self._ctx, float(min_weight),
-                                                    t.ctypes.data_as(_abi.FP), n.value,
-                                                    C.byref(n)), "extract_mesh")
+            self._check(self._lib.tsdf_extract_mesh_table(self._ctx, float(min_weight), tab,
+                                                          t.ctypes.data_as(_abi.FP), n.value,
+                                                          C.byref(n)), "extract_mesh")
         return t.reshape(-1, 3), np.arange(3 * t.shape[0], dtype=np.int64).reshape(-1, 3)
 
     def num_bricks(self):
@@ -285,13 +334,16 @@ class HipTSDFVolume(TSDFVolume):
                                                     _d3(o)), "integrate_device")
 
     def integrate_batch_device(self, d_xyz_ptr, scan_offsets, origins):
+        """origins: (n, 3) ray origins, or (n, 7) poses (x, y, z, qx, qy, qz, qw)."""
         offs = np.ascontiguousarray(scan_offsets, np.uint64)
-        org = np.ascontiguousarray(origins, np.float64).reshape(-1, 3)
+        a = np.asarray(origins, np.float64)
+        fn, k = ((self._lib.tsdf_integrate_batch_device_pose, 7) if a.ndim == 2 and a.shape[1] == 7
+                 else (self._lib.tsdf_integrate_batch_device, 3))
+        org = np.ascontiguousarray(a).reshape(-1, k)
         if offs.shape[0] != org.shape[0] + 1:
             raise ValueError("scan_offsets must have n_scans + 1 entries")
-        self._check(self._lib.tsdf_integrate_batch_device(
-            self._ctx, C.c_void_p(int(d_xyz_ptr)), offs.ctypes.data_as(_abi.U64P), org.shape[0],
-            org.ctypes.data_as(_abi.D3)), "integrate_batch_device")
+        self._check(fn(self._ctx, C.c_void_p(int(d_xyz_ptr)), offs.ctypes.data_as(_abi.U64P),
+                       org.shape[0], org.ctypes.data_as(_abi.D3)), "integrate_batch_device")
 
     def set_profiling(self, on=True):
         self._check(self._lib.tsdf_set_profiling(self._ctx, 1 if on else 0), "set_profiling")
@@ -304,12 +356,12 @@ class HipTSDFVolume(TSDFVolume):
 
 class TsdfIntegratorConfig:
     """voxblox TsdfIntegratorBase::Config (the fields this backend implements; defaults as
-    upstream).  use_const_weight must stay True: the 1/z^2 weight needs the sensor-frame point per
-    sample, which the world-frame boundary does not carry."""
+    upstream, use_const_weight = False: 1 / z^2 of the point's sensor-frame depth, the sensor axis
+    from T_G_C)."""
 
     def __init__(self, default_truncation_distance=0.1, max_weight=10000.0,
                  voxel_carving_enabled=True, min_ray_length_m=0.1, max_ray_length_m=5.0,
-                 use_const_weight=True, allow_clear=True, use_weight_dropoff=True):
+                 use_const_weight=False, allow_clear=True, use_weight_dropoff=True):
         self.default_truncation_distance = default_truncation_distance
         self.max_weight = max_weight
         self.voxel_carving_enabled = voxel_carving_enabled
@@ -326,8 +378,6 @@ class SimpleTsdfIntegrator:
     4x4 pose (float64, then float32) and integrates them from the pose's translation."""
 
     def __init__(self, config, voxel_size, volume_cls=None, **kw):
-        if not config.use_const_weight:
-            raise NotImplementedError("use_const_weight=False (1/z^2 weights) is not supported")
         cls = volume_cls or HipTSDFVolume
         self.config = config
         self.volume = cls(voxel_size, config.default_truncation_distance,
@@ -335,7 +385,8 @@ class SimpleTsdfIntegrator:
                           min_range=config.min_ray_length_m, max_range=config.max_ray_length_m,
                           semantics="voxblox", allow_clear=config.allow_clear,
                           use_weight_dropoff=config.use_weight_dropoff,
-                          max_weight=config.max_weight, **kw)
+                          max_weight=config.max_weight, use_const_weight=config.use_const_weight,
+                          **kw)
 
     def integratePointCloud(self, T_G_C, points_C, colors=None, freespace_points=False):  # noqa: N802
         if freespace_points:

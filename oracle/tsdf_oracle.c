@@ -73,6 +73,7 @@ struct tsdf_ctx {
     float vs, inv_vs, tau;
     float bg;   /* background distance: tau (VDBFusion) or 0 (Voxblox TsdfVoxel) */
     int sem;    /* TSDF_SEM_* */
+    float zax[3]; /* the current scan's sensor z axis (tsdf_integrate_pose; else world z) */
     /* azimuth-sector filter (tsdf_params.n_sectors > 1): pseudo-angle interval [sec_lo, sec_hi),
      * cyclic when sec_wrap (include/tsdf_hip.h tsdf_sector_of) */
     int sec_on, sec_wrap;
@@ -235,6 +236,7 @@ void tsdf_default_params(tsdf_params* p) {
     p->allow_clear = 1;        /* voxblox TsdfIntegratorBase::Config defaults */
     p->use_weight_dropoff = 1;
     p->max_weight = 10000.0f;
+    p->depth_weight = 1; /* voxblox use_const_weight = false (upstream's default) */
 }
 
 int tsdf_abi_version(void) { return TSDF_ABI_VERSION; }
@@ -256,6 +258,7 @@ int tsdf_create(const tsdf_params* params, tsdf_ctx** out) {
     c->inv_vs = 1.0f / c->vs;
     c->tau = (float)params->sdf_trunc;
     c->sem = params->semantics;
+    c->zax[0] = 0.0f; c->zax[1] = 0.0f; c->zax[2] = 1.0f;
     c->bg = c->sem == TSDF_SEM_VOXBLOX ? 0.0f : c->tau;
     c->mode = ORACLE_MODE_SCAN_FUSED;
     {
@@ -472,9 +475,11 @@ static int64_t walk_ray_vdb(tsdf_ctx* c, const double p[3], const double o[3], v
  *                   t_next = (max(0, sign) - (start_s - cur)) / r; t_step = sign / r
  *   nextRayIndex:   steps + 1 voxels; after each, the axis of the FIRST minimum of t_next
  *                   (Eigen minCoeff: ties -> lower axis) advances by its sign
- *   updateTsdfVoxel (use_const_weight): c = (v + 1/2) vs;
+ *   getVoxelWeight: use_const_weight -> w = 1; else w = 1 / z^2, z the point's sensor-frame depth
+ *                   (|z| <= 1e-6 -> 0; tsdf_params.depth_weight, the axis from the scan's pose)
+ *   updateTsdfVoxel: c = (v + 1/2) vs;
  *                   sdf = |p - o| - ((c - o).(p - o)) / |p - o|     (computeDistance, projective)
- *                   w = 1; dropoff: sdf < -vs -> w = (w (tau + sdf)) / (tau - vs), max(w, 0)
+ *                   dropoff: sdf < -vs -> w = (w (tau + sdf)) / (tau - vs), max(w, 0)
  *                   W' = W + w (W' < kFloatEpsilon: no update); S' = (sdf w + S W) / W'
  *                   S = S' > 0 ? min(tau, S') : max(-tau, S');  W = min(max_weight, W')
  * Stated deviations:
@@ -504,6 +509,13 @@ static int64_t walk_ray_vb(tsdf_ctx* c, float px, float py, float pz, float ox, 
         clearing = 1;
     }
     const float ux = dx / depth, uy = dy / depth, uz = dz / depth;
+    /* TsdfIntegratorBase::getVoxelWeight: use_const_weight -> 1; else 1 / z^2 of the point's
+     * sensor-frame depth z = zaxis . (p - o) (Eigen's x + (y + z)), 0 for |z| <= kEpsilon 1e-6 */
+    float w0 = 1.0f;
+    if (c->p.depth_weight) {
+        const float z = fabsf(c->zax[0] * dx + (c->zax[1] * dy + c->zax[2] * dz));
+        w0 = z > 1e-6f ? 1.0f / (z * z) : 0.0f;
+    }
     float ex, ey, ez, sx, sy, sz;
     if (clearing) {
         float len = depth - tau;
@@ -547,7 +559,7 @@ static int64_t walk_ray_vb(tsdf_ctx* c, float px, float py, float pz, float ox, 
             const float ax = cx - ox, ay = cy - oy, az = cz - oz; /* v_voxel_origin */
             const float proj = (ax * dx + (ay * dy + az * dz)) / depth; /* dist_G_V */
             const float sdf = depth - proj;
-            float w = 1.0f;
+            float w = w0;
             if (c->p.use_weight_dropoff && sdf < -vs) {
                 w = (w * (tau + sdf)) / (tau - vs);
                 w = w > 0.0f ? w : 0.0f;
@@ -790,8 +802,34 @@ int tsdf_oracle_set_threads(tsdf_ctx* c, int n) {
     return TSDF_OK;
 }
 
+static int integrate_scan(tsdf_ctx* c, const void* pts, uint64_t n, uint32_t point_step,
+                          uint32_t xyz_offset, int32_t xyz_is_f64, const double origin[3]);
+
 int tsdf_integrate(tsdf_ctx* c, const void* pts, uint64_t n, uint32_t point_step,
                    uint32_t xyz_offset, int32_t xyz_is_f64, const double origin[3]) {
+    if (!c) return TSDF_EINVAL;
+    c->zax[0] = 0.0f; c->zax[1] = 0.0f; c->zax[2] = 1.0f;
+    return integrate_scan(c, pts, n, point_step, xyz_offset, xyz_is_f64, origin);
+}
+
+/* pose = (x, y, z, qx, qy, qz, qw): the scan's sensor z axis is the third column of the rotation
+ * of the normalised quaternion, in double, rounded to float (the GPU library's pose_of) */
+int tsdf_integrate_pose(tsdf_ctx* c, const void* pts, uint64_t n, uint32_t point_step,
+                        uint32_t xyz_offset, int32_t xyz_is_f64, const double pose[7]) {
+    if (!c) return TSDF_EINVAL;
+    if (!pose) return set_err(c, TSDF_EINVAL, "null argument");
+    const double qn = pose[3] * pose[3] + pose[4] * pose[4] + pose[5] * pose[5] + pose[6] * pose[6];
+    if (!(qn > 0.0) || !isfinite(qn)) return set_err(c, TSDF_EINVAL, "pose quaternion is zero");
+    const double nn = sqrt(pose[3] * pose[3] + pose[4] * pose[4] + pose[5] * pose[5] + pose[6] * pose[6]);
+    const double x = pose[3] / nn, y = pose[4] / nn, z = pose[5] / nn, w = pose[6] / nn;
+    c->zax[0] = (float)(2.0 * (x * z + w * y));
+    c->zax[1] = (float)(2.0 * (y * z - w * x));
+    c->zax[2] = (float)(1.0 - 2.0 * (x * x + y * y));
+    return integrate_scan(c, pts, n, point_step, xyz_offset, xyz_is_f64, pose);
+}
+
+static int integrate_scan(tsdf_ctx* c, const void* pts, uint64_t n, uint32_t point_step,
+                          uint32_t xyz_offset, int32_t xyz_is_f64, const double origin[3]) {
     if (!c || (!pts && n) || !origin) return set_err(c, TSDF_EINVAL, "null argument");
     const uint32_t need = xyz_is_f64 ? 24u : 12u;
     if (point_step < need || xyz_offset > point_step - need)
@@ -1211,7 +1249,7 @@ int tsdf_border_merge_device(tsdf_ctx* c, const uint32_t* recv, const uint64_t* 
  *   Output: triangle soup, 9 floats per triangle, bricks in (z, y, x) order, cubes by their min
  *   voxel's in-brick index z*64 + y*8 + x, triangles in table order. */
 
-static uint8_t mc_tab[256][32]; /* [case][0] = triangles, then 3 edge ids each */
+static uint8_t mc_tabs[2][256][32]; /* TSDF_MC_*: [case][0] = triangles, then 3 edge ids each */
 static int mc_edge_a[12], mc_edge_b[12];
 static int mc_ready = 0;
 
@@ -1222,11 +1260,10 @@ static int mc_edge_of(int a, int b) {
     return -1;
 }
 
-static void mc_build(void) {
-    int ne = 0;
-    for (int d = 0; d < 3; d++)
-        for (int base = 0; base < 8; base++)
-            if (!(base & (1 << d))) { mc_edge_a[ne] = base; mc_edge_b[ne] = base | (1 << d); ne++; }
+/* TSDF_MC_LORENSEN: the classic table's ambiguity rule -- an ambiguous face pairs its crossings
+ * around the inside corners when at most 4 cube corners are inside, around the outside corners
+ * otherwise (Lorensen & Cline's complement symmetry; neighbouring cubes can then disagree) */
+static void mc_build_table(int lorensen, uint8_t mc_tab[256][32]) {
     for (int k = 0; k < 256; k++) {
         int nxt[12];
         for (int e = 0; e < 12; e++) nxt[e] = -1;
@@ -1247,7 +1284,8 @@ static void mc_build(void) {
                 int pi[2], pj[2], np = 0;
                 if (ncr == 2) { pi[0] = cr[0]; pj[0] = cr[1]; np = 1; }
                 else if (ncr == 4) {
-                    if (in[0]) { pi[0] = 3; pj[0] = 0; pi[1] = 1; pj[1] = 2; }
+                    const int around_in = !lorensen || __builtin_popcount((unsigned)k) <= 4;
+                    if (in[0] == around_in) { pi[0] = 3; pj[0] = 0; pi[1] = 1; pj[1] = 2; }
                     else { pi[0] = 0; pj[0] = 1; pi[1] = 2; pj[1] = 3; }
                     np = 2;
                 }
@@ -1275,19 +1313,38 @@ static void mc_build(void) {
         }
         mc_tab[k][0] = (uint8_t)nt;
     }
+}
+
+static void mc_build(void) {
+    int ne = 0;
+    for (int d = 0; d < 3; d++)
+        for (int base = 0; base < 8; base++)
+            if (!(base & (1 << d))) { mc_edge_a[ne] = base; mc_edge_b[ne] = base | (1 << d); ne++; }
+    mc_build_table(0, mc_tabs[TSDF_MC_GENERATED]);
+    mc_build_table(1, mc_tabs[TSDF_MC_LORENSEN]);
     mc_ready = 1;
 }
 
-int tsdf_mc_table(uint8_t* out) {
-    if (!out) return TSDF_EINVAL;
+int tsdf_mc_table(uint8_t* out) { return tsdf_mc_table_of(TSDF_MC_GENERATED, out); }
+
+int tsdf_mc_table_of(int32_t table, uint8_t* out) {
+    if (!out || (table != TSDF_MC_GENERATED && table != TSDF_MC_LORENSEN)) return TSDF_EINVAL;
     if (!mc_ready) mc_build();
-    memcpy(out, mc_tab, sizeof mc_tab);
+    memcpy(out, mc_tabs[table], sizeof mc_tabs[table]);
     return TSDF_OK;
 }
 
 int tsdf_extract_mesh(tsdf_ctx* c, float min_weight, float* tri, uint64_t cap, uint64_t* n_tri) {
+    return tsdf_extract_mesh_table(c, min_weight, TSDF_MC_GENERATED, tri, cap, n_tri);
+}
+
+int tsdf_extract_mesh_table(tsdf_ctx* c, float min_weight, int32_t table, float* tri,
+                            uint64_t cap, uint64_t* n_tri) {
     if (!c || !n_tri) return TSDF_EINVAL;
+    if (table != TSDF_MC_GENERATED && table != TSDF_MC_LORENSEN)
+        return set_err(c, TSDF_EINVAL, "unknown marching-cubes table");
     if (!mc_ready) mc_build();
+    const uint8_t(*mc_tab)[32] = mc_tabs[table];
     uint64_t nb = 0;
     brick_ent* e = list_bricks(c, &nb);
     if (!e) return TSDF_ENOMEM;

@@ -63,8 +63,9 @@ def test_default_params_roundtrip():
     assert p.voxel_size == 0.05 and p.sdf_trunc == 0.15 and p.brick_side == 8
     assert p.space_carving == 0 and np.isinf(p.max_range)
     assert p.walk == _abi.WALK_TWO == 0  # ABI v5: two walks unless the single walk is asked for
-    # the ctypes mirror ends where the C struct ends (ABI v5 appended `walk`)
-    assert _abi.TsdfParams._fields_[-1][0] == "walk"
+    assert p.depth_weight == 1  # ABI v6: Voxblox's 1/z^2 weight, upstream's default
+    # the ctypes mirror ends where the C struct ends (ABI v6 appended `depth_weight`)
+    assert _abi.TsdfParams._fields_[-1][0] == "depth_weight"
 
 
 def test_header_kernel_kinds_match_the_binding():

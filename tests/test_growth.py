@@ -154,3 +154,42 @@ def test_sector_sample_list_grows(sim, walk):
     for p, q in scans:
         o.integrate(p, q)
     assert bitwise(g, o)
+
+
+@pytest.mark.parametrize("pipeline", [False, True])
+def test_metrics_drain_replay_keeps_staged_input(sim, tmp_path, pipeline):
+    """the metrics-ring drain inside a launch can run a capacity replay while a host
+    batch is already staged.  Hundreds of 1-scan batches with the metrics log on and a pool that
+    keeps growing put overflows into that window; the field must still be the oracle's, bit for bit
+    (each pending batch reads its own staging buffer, whatever the batch parity after a replay)."""
+    g = hip(max_bricks=16, max_batch=1, pipeline=pipeline)
+    g.set_metrics_log(tmp_path / "m.jsonl")
+    o = ora()
+    for k in range(600):
+        pts, org = sim.scan(k % 300)
+        pts = np.ascontiguousarray(pts[(k * 7) % 64::64])
+        g.integrate(pts, org)
+        o.integrate(pts, org)
+    g.sync()
+    st = g.stats()
+    assert st["n_grows"] >= 3 and st["n_replayed"] >= 1
+    assert bitwise(g, o)
+
+
+def test_device_scans_queue_and_free_the_buffer(sim):
+    """tsdf_integrate_device copies the scan into the pending batch before returning (ABI v6): the
+    caller overwrites its buffer right after each call, and the field is still the oracle's."""
+    import torch
+    g = hip(max_bricks=64, max_batch=4)
+    o = ora()
+    buf = torch.empty((1 << 16, 3), dtype=torch.float32, device="cuda")
+    for k in range(10):
+        pts, org = sim.scan(k)
+        pts = decimate(pts, 8)
+        buf[:pts.shape[0]] = torch.from_numpy(pts).cuda()
+        g.integrate_device(buf.data_ptr(), pts.shape[0], org)
+        buf.fill_(1e9)  # the caller's buffer is free once the call returned
+        o.integrate(pts, org)
+    g.sync()
+    assert bitwise(g, o)
+    assert g.stats()["n_batches"] <= 4  # queued: 10 scans in batches of 4

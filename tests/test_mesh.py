@@ -143,3 +143,73 @@ def test_gpu_scan_mesh_bitwise(sim):
         vg, _ = g.extract_triangle_mesh(min_weight=mw)
         assert vo.shape[0] > 1000
         assert vg.shape == vo.shape and np.array_equal(vg, vo), mw
+
+
+def table_of(lib, which):
+    buf = (C.c_uint8 * (256 * 32))()
+    assert lib.tsdf_mc_table_of(which, buf) == 0
+    return np.frombuffer(buf, np.uint8).reshape(256, 32).copy()
+
+
+def _ambiguous_face(k):
+    """Some cube face has its two inside corners on a diagonal."""
+    for d in range(3):
+        u, w = (d + 1) % 3, (d + 2) % 3
+        for s in range(2):
+            q = [(s << d) | (a << u) | (b << w) for a, b in ((0, 0), (1, 0), (1, 1), (0, 1))]
+            i = [(k >> c) & 1 for c in q]
+            if i[0] == i[2] and i[1] == i[3] and i[0] != i[1]:
+                return True
+    return False
+
+
+def test_lorensen_table_rule():
+    """TSDF_MC_LORENSEN (VDBFusion's classic table rule): it differs from the
+    generated table exactly on the cases with an ambiguous face and more than 4 inside corners,
+    and the product library builds the same table as the oracle."""
+    from tsdf_map._lib import load_hip_library
+    g = table_of(oracle.load(), 0)
+    lo = table_of(oracle.load(), 1)
+    assert np.array_equal(lo, table_of(load_hip_library(), 1))
+    assert np.array_equal(g, table(oracle.load()))
+    differ = {k for k in range(256) if not np.array_equal(g[k], lo[k])}
+    expect = {k for k in range(256) if _ambiguous_face(k) and bin(k).count("1") > 4}
+    assert differ == expect and len(differ) > 0
+    edges = [(b, b | (1 << d)) for d in range(3) for b in range(8) if not b & (1 << d)]
+    for k in range(256):  # still on sign-change edges
+        for e in lo[k, 1:1 + 3 * lo[k, 0]]:
+            a, b = edges[e]
+            assert ((k >> a) & 1) != ((k >> b) & 1), (k, e)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("radius", [0.37, 1.1])
+def test_gpu_sphere_mesh_lorensen_bitwise(radius):
+    from tsdf_map import HipTSDFVolume
+    bricks = sphere_bricks(radius)
+    o = oracle.OracleTSDFVolume(VS, TAU)
+    o.import_bricks(*bricks)
+    g = HipTSDFVolume(VS, TAU, max_bricks=1 << 16, max_points=1 << 12)
+    g.import_bricks(*bricks)
+    vo, _ = o.extract_triangle_mesh(table="lorensen")
+    vg, _ = g.extract_triangle_mesh(table="lorensen")
+    assert vg.shape == vo.shape and np.array_equal(vg, vo)
+
+
+@pytest.mark.gpu
+def test_gpu_scan_mesh_lorensen_bitwise(sim):
+    """Integrated scans (noisy surfaces: ambiguous cubes occur) meshed with the classic table, GPU
+    == oracle bit for bit; the two tables' meshes differ only where ambiguous cubes are."""
+    from conftest import decimate
+    from tsdf_map import HipTSDFVolume
+    o = oracle.OracleTSDFVolume(VS, TAU)
+    g = HipTSDFVolume(VS, TAU, max_bricks=1 << 18)
+    for k in range(6):
+        p, org = sim.scan(k)
+        p = decimate(p, 4)
+        o.integrate(p, org)
+        g.integrate(p, org)
+    vo, _ = o.extract_triangle_mesh(table="lorensen")
+    vg, _ = g.extract_triangle_mesh(table="lorensen")
+    assert vo.shape[0] > 1000
+    assert vg.shape == vo.shape and np.array_equal(vg, vo)

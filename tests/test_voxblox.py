@@ -224,3 +224,83 @@ def test_gpu_voxblox_query_background(sim):
     g.integrate(decimate(p, 16), org)
     s, w = g.query_dense([-600, -600, -100], [-598, -598, -98])
     assert (s == 0).all() and (w == 0).all()
+
+
+# -- Voxblox's default weight: 1 / z^2 of the sensor-frame depth (use_const_weight = False) -----
+
+def _zaxis(q):
+    """The sensor z axis of pose quaternion q (x, y, z, w) as the libraries compute it."""
+    x, y, z, w = np.asarray(q, np.float64) / np.linalg.norm(q)
+    return np.array([2 * (x * z + w * y), 2 * (y * z - w * x), 1 - 2 * (x * x + y * y)]).astype(F)
+
+
+@pytest.mark.parametrize("pitch", [0.0, 0.4, -1.1])
+def test_depth_weight_is_inverse_z_squared(pitch):
+    """One ray, no dropoff: every voxel's weight is getVoxelWeight(point_C) = 1 / z^2 with z the
+    point's depth along the sensor's z axis (here pitched about y by `pitch`)."""
+    o = np.array([0.012, 0.013, 0.011])
+    q = (0.0, math.sin(pitch / 2), 0.0, math.cos(pitch / 2))
+    p = (o + [3.0, 0.4, -1.2]).astype(F)
+    vol = ora(use_const_weight=False, use_weight_dropoff=False)
+    vol.integrate(p[None], np.concatenate([o, q]))
+    _, _, w = vol.export_voxels()
+    zx, zy, zz = _zaxis(q)
+    d = p - o.astype(F)
+    z = abs(zx * d[0] + (zy * d[1] + zz * d[2]))
+    w0 = F(1.0) / (z * z)
+    assert w.size > 3 and np.all(w == w0), (w[:3], w0)
+    # the const-weight mode (and the default integrate's world z axis) are unchanged
+    c = ora(use_weight_dropoff=False)
+    c.integrate(p[None], o)
+    assert np.all(c.export_voxels()[2] == 1.0)
+
+
+def test_depth_weight_tiny_z_gives_zero_weight():
+    """|z| <= kEpsilon: weight 0, the samples are dropped (deviation 2)."""
+    o = np.array([0.012, 0.013, 0.011])
+    p = (o + [3.0, 0.4, 0.0]).astype(F)  # z = 0 along the world z axis
+    vol = ora(use_const_weight=False)
+    vol.integrate(p[None], o)
+    assert vol.export_voxels()[0].shape[0] == 0
+
+
+def _posed_scans(sim, ks, decim):
+    out = []
+    for j, k in enumerate(ks):
+        p, org = sim.scan(k)
+        a, b = 0.3 * j - 0.2, 0.15 * j
+        q = np.array([math.sin(a / 2) * math.cos(b), math.sin(a / 2) * math.sin(b), 0.1 * j,
+                      math.cos(a / 2)])
+        out.append((decimate(p, decim), np.concatenate([org, q])))
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kw", [
+    dict(),
+    dict(use_weight_dropoff=False),
+    dict(space_carving=True, max_range=5.0, min_range=0.1),   # voxblox's defaults
+], ids=["dropoff", "no-dropoff", "upstream-defaults"])
+def test_gpu_voxblox_depth_weight_bitwise(sim, kw):
+    k = 32 if kw.get("space_carving") else 4
+    scans = _posed_scans(sim, (0, 1, 2, 30), k)
+    g, o = run_both(scans, use_const_weight=False, **kw)
+    assert assert_bitwise(g, o) > 1000
+    gw = g.export_voxels()[2]
+    assert np.unique(gw).size > 100  # weights are not counts any more
+
+
+@pytest.mark.gpu
+def test_gpu_voxblox_depth_weight_batch_device_poses(sim):
+    """tsdf_integrate_batch_device_pose: device-resident scans with one pose each, 3 per batch."""
+    import torch
+    scans = _posed_scans(sim, range(7), 4)
+    g = hip(use_const_weight=False, max_batch=3)
+    o = ora(use_const_weight=False)
+    x = torch.from_numpy(np.concatenate([p for p, _ in scans])).cuda()
+    offs = np.cumsum([0] + [p.shape[0] for p, _ in scans])
+    g.integrate_batch_device(x.data_ptr(), offs, np.stack([q for _, q in scans]))
+    for p, q in scans:
+        o.integrate(p, q)
+    g.sync()
+    assert assert_bitwise(g, o) > 1000
