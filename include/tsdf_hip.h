@@ -186,6 +186,17 @@ int tsdf_integrate(tsdf_ctx* ctx, const void* pts, uint64_t n, uint32_t point_st
 int tsdf_integrate_pose(tsdf_ctx* ctx, const void* pts, uint64_t n, uint32_t point_step,
                         uint32_t xyz_offset, int32_t xyz_is_f64, const double pose[7]);
 
+/* ABI v6: the live multi-GPU input path.  One host cloud for n_ctx contexts that
+ * shard it by azimuth sector, one context per GPU: ctxs[k] was created with n_sectors = n_ctx,
+ * sector = k and the same sector_yaw0 (n_ctx = 1: one unsharded context).  Every point is
+ * classified once on the host (tsdf_sector_of's rule) and each context receives only its
+ * sector's points, so a scan crosses PCIe once in total, split over the GPUs' links, instead of
+ * once per GPU.  pose as in tsdf_integrate_pose.  Call from the one thread that uses these
+ * contexts; each context's queue behaves as after tsdf_integrate_pose. */
+int tsdf_integrate_sectors(tsdf_ctx* const* ctxs, uint32_t n_ctx, const void* pts, uint64_t n,
+                           uint32_t point_step, uint32_t xyz_offset, int32_t xyz_is_f64,
+                           const double pose[7]);
+
 /* One scan already in device memory: d_xyz = n packed float32 triplets (12 B per point).  The
  * points are copied (device to device) into the pending batch's staging before the call returns,
  * so d_xyz may be reused or freed at once; the scan joins the pending batch like a host scan (see

@@ -1289,6 +1289,117 @@ int tsdf_integrate(tsdf_ctx* c, const void* pts, uint64_t n, uint32_t point_step
     return integrate_impl(c, pts, n, point_step, xyz_offset, xyz_is_f64, pose_of_origin(origin));
 }
 
+// One host cloud for N sector-sharded contexts (the live N-GPU input path): every
+// point is classified once (the kernels' in_sector rule on each context's bounds) and packed into
+// its context's pinned staging; each context then copies only its sector's points to its GPU, so a
+// scan crosses PCIe once in total, split over the N links.
+int tsdf_integrate_sectors(tsdf_ctx* const* ctxs, uint32_t n_ctx, const void* pts, uint64_t n,
+                           uint32_t point_step, uint32_t xyz_offset, int32_t xyz_is_f64,
+                           const double pose[7]) {
+    if (!ctxs || n_ctx == 0 || n_ctx > TSDF_MAX_WORLD) return TSDF_EINVAL;
+    for (uint32_t k = 0; k < n_ctx; k++)
+        if (!ctxs[k]) return TSDF_EINVAL;
+    tsdf_ctx* c0 = ctxs[0];
+    if ((!pts && n) || !pose) return fail(c0, TSDF_EINVAL, "null argument");
+    const uint32_t need = xyz_is_f64 ? 24u : 12u;
+    if (point_step < need || xyz_offset > point_step - need)
+        return fail(c0, TSDF_EINVAL, "point_step/xyz_offset inconsistent");
+    const double qn = pose[3] * pose[3] + pose[4] * pose[4] + pose[5] * pose[5] + pose[6] * pose[6];
+    if (!(qn > 0.0) || !std::isfinite(qn)) return fail(c0, TSDF_EINVAL, "pose quaternion is zero");
+    for (uint32_t k = 0; k < n_ctx; k++) {
+        const tsdf_ctx* c = ctxs[k];
+        const bool sharded = n_ctx == 1 ? c->p.n_sectors <= 1 : c->p.n_sectors == n_ctx;
+        if (!sharded || (n_ctx > 1 && (c->p.sector != k || c->p.sector_yaw0 != c0->p.sector_yaw0)))
+            return fail(c0, TSDF_EINVAL, "context %u is not sector %u of %u (same sector_yaw0)", k,
+                        k, n_ctx);
+        if (n > c->max_points)  // a context may receive every point
+            return fail(c0, TSDF_EINVAL, "scan of %llu points exceeds max_points of context %u",
+                        (unsigned long long)n, k);
+    }
+    const ScanPose P = pose_of(pose);
+    const float ox = (float)P.o[0], oy = (float)P.o[1];
+    // room in every pending batch, and each context's free pinned buffer
+    float* h[TSDF_MAX_WORLD];
+    int hb[TSDF_MAX_WORLD];
+    for (uint32_t k = 0; k < n_ctx; k++) {
+        tsdf_ctx* c = ctxs[k];
+        HIPCHK(c, hipSetDevice(c->device));
+        const int rc = pend_room(c, n);
+        if (rc) return rc;
+        hb[k] = c->stage_cur;
+        c->stage_cur ^= 1;
+        HIPCHK(c, hipEventSynchronize(c->stage_done[hb[k]]));
+        h[k] = c->h_stage[hb[k]];
+    }
+    // classify + pack, in point chunks over c0's staging threads: count per (part, sector), then
+    // each part writes its points at its prefix (the parts keep the input order within a sector)
+    const char* base = static_cast<const char*>(pts);
+    auto xyz_at = [&](uint64_t i, float v[3]) {
+        const char* q = base + i * point_step + xyz_offset;
+        if (xyz_is_f64) {
+            double d[3];
+            std::memcpy(d, q, sizeof d);
+            v[0] = (float)d[0];
+            v[1] = (float)d[1];
+            v[2] = (float)d[2];
+        } else {
+            std::memcpy(v, q, 12);
+        }
+    };
+    auto sector_of = [&](const float v[3]) -> int {
+        const float dx = v[0] - ox, dy = v[1] - oy;
+        for (uint32_t k = 0; k < n_ctx; k++)
+            if (in_sector(ctxs[k]->R, dx, dy)) return (int)k;
+        return -1;  // NaN: no sector (every kernel would drop the ray)
+    };
+    const int parts = (c0->pack && n >= (1u << 15)) ? c0->pack->parts() : 1;
+    std::vector<uint64_t> cnt((size_t)parts * n_ctx, 0), at((size_t)parts * n_ctx, 0);
+    auto count = [&](int part) {
+        const uint64_t i0 = n * part / parts, i1 = n * (part + 1) / parts;
+        float v[3];
+        for (uint64_t i = i0; i < i1; i++) {
+            xyz_at(i, v);
+            const int k = sector_of(v);
+            if (k >= 0) cnt[(size_t)part * n_ctx + k]++;
+        }
+    };
+    auto scatter = [&](int part) {
+        const uint64_t i0 = n * part / parts, i1 = n * (part + 1) / parts;
+        uint64_t pos[TSDF_MAX_WORLD];
+        for (uint32_t k = 0; k < n_ctx; k++) pos[k] = at[(size_t)part * n_ctx + k];
+        float v[3];
+        for (uint64_t i = i0; i < i1; i++) {
+            xyz_at(i, v);
+            const int k = sector_of(v);
+            if (k >= 0) std::memcpy(h[k] + 3 * pos[k]++, v, 12);
+        }
+    };
+    if (parts > 1) c0->pack->run(count);
+    else count(0);
+    std::vector<uint64_t> tot(n_ctx, 0);
+    for (uint32_t k = 0; k < n_ctx; k++)
+        for (int q = 0; q < parts; q++) {
+            at[(size_t)q * n_ctx + k] = tot[k];
+            tot[k] += cnt[(size_t)q * n_ctx + k];
+        }
+    if (parts > 1) c0->pack->run(scatter);
+    else scatter(0);
+    // each context: its sector's points to its GPU, into its pending batch
+    for (uint32_t k = 0; k < n_ctx; k++) {
+        tsdf_ctx* c = ctxs[k];
+        HIPCHK(c, hipSetDevice(c->device));
+        int rc = pend_stage_buffer(c);
+        if (rc) return rc;
+        if (tot[k])
+            HIPCHK(c, hipMemcpyAsync(c->stage2[c->pend_stage] + 3 * (uint64_t)c->pend.s[c->pend.n_scans].off,
+                                     h[k], tot[k] * 12, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipEventRecord(c->stage_done[hb[k]], c->stream));
+        rc = pend_push(c, tot[k], P);
+        if (rc) return rc;
+    }
+    return TSDF_OK;
+}
+
 int tsdf_integrate_pose(tsdf_ctx* c, const void* pts, uint64_t n, uint32_t point_step,
                         uint32_t xyz_offset, int32_t xyz_is_f64, const double pose[7]) {
     if (!c) return TSDF_EINVAL;

@@ -7,10 +7,15 @@
 // deskewed cloud with the scan time (reference src/dlio/src/dlio/odom.cc:447) but publishes /pose at
 // the IMU rate stamped with imu_stamp (odom.cc:318,383).  A cloud's ray origin is therefore the pose
 // track evaluated at the cloud's stamp: linear interpolation of the position between the bracketing
-// samples (slerp of the orientation, which the world-frame cloud does not need), the exact sample
-// when a stamp matches.  A cloud newer than the newest pose waits (bounded queue) until the track
-// passes its stamp; a cloud older than the track or across a gap wider than max_gap_ms is dropped
-// and counted.  /path (nav_msgs/Path, appended per scan, odom.cc:358-432) can feed the same track.
+// samples and slerp of the orientation (the sensor axes: Voxblox's 1/z^2 weight), the exact sample
+// when a stamp matches; the scan goes to tsdf_integrate_pose.  A cloud newer than the newest pose
+// waits (bounded queue) until the track passes its stamp; a cloud older than the track or across a
+// gap wider than max_gap_ms is dropped and counted.  /path (nav_msgs/Path, appended per scan,
+// odom.cc:358-432) can feed the same track.
+//
+// No copy of the cloud is made here: a waiting cloud is held by a reference to the caller's
+// message (a shared_ptr keep-alive, e.g. the ROS ConstPtr), and tsdf_integrate_pose itself copies
+// the points into pinned staging before it returns.
 #pragma once
 
 #include <algorithm>
@@ -18,6 +23,7 @@
 #include <cstdint>
 #include <cstring>
 #include <deque>
+#include <memory>
 #include <vector>
 
 #include "../../include/tsdf_hip.h"
@@ -45,14 +51,16 @@ class PoseTrack {
     int64_t newest() const { return v_.empty() ? INT64_MIN : v_.back().t_ns; }
     int64_t oldest() const { return v_.empty() ? INT64_MAX : v_.front().t_ns; }
 
-    // Position at t_ns (ingest.py PoseTrack.at, the same double ops); false outside the track or
-    // across a gap wider than max_gap_ms.
-    bool at(int64_t t_ns, double max_gap_ms, double out[3]) const {
+    // Pose at t_ns as (x, y, z, qx, qy, qz, qw) (ingest.py PoseTrack.at, the same double ops:
+    // linear position, slerp orientation); false outside the track or across a gap wider than
+    // max_gap_ms.
+    bool at(int64_t t_ns, double max_gap_ms, double out[7]) const {
         if (v_.empty() || t_ns < v_.front().t_ns || t_ns > v_.back().t_ns) return false;
         auto it = std::lower_bound(v_.begin(), v_.end(), t_ns,
                                    [](const Pose& a, int64_t t) { return a.t_ns < t; });
         if (it->t_ns == t_ns) {
             std::memcpy(out, it->p, sizeof it->p);
+            std::memcpy(out + 3, it->q, sizeof it->q);
             return true;
         }
         const Pose& b = *it;
@@ -60,7 +68,28 @@ class PoseTrack {
         if ((double)(b.t_ns - a.t_ns) > max_gap_ms * 1e6) return false;
         const double f = (double)(t_ns - a.t_ns) / (double)(b.t_ns - a.t_ns);
         for (int k = 0; k < 3; k++) out[k] = a.p[k] + f * (b.p[k] - a.p[k]);
+        slerp(a.q, b.q, f, out + 3);
         return true;
+    }
+
+    // ingest.py _slerp: shortest arc, normalised lerp above a dot of 0.9995
+    static void slerp(const double q0[4], const double q1_in[4], double f, double out[4]) {
+        double q1[4], d = 0.0;
+        for (int k = 0; k < 4; k++) d += q0[k] * q1_in[k];
+        const double s = d < 0.0 ? -1.0 : 1.0;
+        for (int k = 0; k < 4; k++) q1[k] = s * q1_in[k];
+        d *= s;
+        if (d > 0.9995) {
+            for (int k = 0; k < 4; k++) out[k] = q0[k] + f * (q1[k] - q0[k]);
+        } else {
+            const double th = std::acos(d);
+            const double a = std::sin((1.0 - f) * th), b = std::sin(f * th), c = std::sin(th);
+            for (int k = 0; k < 4; k++) out[k] = (a * q0[k] + b * q1[k]) / c;
+        }
+        double n = 0.0;
+        for (int k = 0; k < 4; k++) n += out[k] * out[k];
+        n = std::sqrt(n);
+        for (int k = 0; k < 4; k++) out[k] /= n;
     }
 
    private:
@@ -84,16 +113,18 @@ class MapCore {
         return release(false);
     }
 
-    // One PointCloud2 payload (copied: the caller's message may go at once).
-    int on_cloud(int64_t stamp_ns, const void* data, uint64_t n, uint32_t point_step,
-                 uint32_t xyz_offset, int32_t xyz_is_f64) {
+    // One PointCloud2 payload.  `keep` owns the bytes at `data` (the message): it is held while the
+    // cloud waits for its pose and released once the library has copied the points.
+    int on_cloud(int64_t stamp_ns, std::shared_ptr<const void> keep, const void* data, uint64_t n,
+                 uint32_t point_step, uint32_t xyz_offset, int32_t xyz_is_f64) {
         Pending c;
         c.t_ns = stamp_ns;
         c.n = n;
         c.step = point_step;
         c.xoff = xyz_offset;
         c.f64 = xyz_is_f64;
-        c.data.assign((const uint8_t*)data, (const uint8_t*)data + (size_t)n * point_step);
+        c.keep = std::move(keep);
+        c.data = data;
         pending_.push_back(std::move(c));
         if (pending_.size() > max_pending_) {  // the pose stream stalled: oldest cloud goes
             pending_.pop_front();
@@ -114,7 +145,8 @@ class MapCore {
         uint64_t n;
         uint32_t step, xoff;
         int32_t f64;
-        std::vector<uint8_t> data;
+        std::shared_ptr<const void> keep;  // the message owning `data`
+        const void* data;
     };
 
     int release(bool final_) {
@@ -122,8 +154,8 @@ class MapCore {
             Pending& c = pending_.front();
             if (!final_ && !track_.empty() && c.t_ns > track_.newest()) break;  // wait for poses
             if (!final_ && track_.empty()) break;
-            double origin[3];
-            if (!track_.at(c.t_ns, max_gap_ms_, origin)) {
+            double pose[7];
+            if (!track_.at(c.t_ns, max_gap_ms_, pose)) {
                 if (c.t_ns < track_.oldest() || track_.empty() || c.t_ns > track_.newest())
                     counts_.dropped_old++;
                 else
@@ -131,7 +163,7 @@ class MapCore {
                 pending_.pop_front();
                 continue;
             }
-            const int rc = tsdf_integrate(ctx_, c.data.data(), c.n, c.step, c.xoff, c.f64, origin);
+            const int rc = tsdf_integrate_pose(ctx_, c.data, c.n, c.step, c.xoff, c.f64, pose);
             pending_.pop_front();
             if (rc != TSDF_OK) return rc;
             counts_.integrated++;

@@ -17,7 +17,11 @@
 // tsdf_export_bricks: u64 n_bricks, then n_bricks * (i32 coords[3]), n_bricks * 512 f32 sdf,
 // n_bricks * 512 f32 w.
 //
-// usage: tsdf_replay <in.scans> <out.bricks> [voxel_size sdf_trunc [semantics]]
+// usage: tsdf_replay <in.scans> <out.bricks> [voxel_size sdf_trunc [semantics [max_batch]]]
+//   semantics: vdbfusion (default), vdbfusion_f64, voxblox (1/z^2 weight, upstream's default) or
+//   voxblox_const (use_const_weight); max_batch: scans per GPU batch (the node's ~max_batch).
+// The time from the first integrate to the end of tsdf_sync is printed as the node-path rate.
+#include <chrono>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -63,7 +67,13 @@ int main(int argc, char** argv) {
         p.voxel_size = std::atof(argv[3]);
         p.sdf_trunc = std::atof(argv[4]);
     }
-    if (argc >= 6 && std::string(argv[5]) == "voxblox") p.semantics = TSDF_SEM_VOXBLOX;
+    if (argc >= 6) {
+        const std::string sem = argv[5];
+        if (sem == "voxblox" || sem == "voxblox_const") p.semantics = TSDF_SEM_VOXBLOX;
+        if (sem == "voxblox_const") p.depth_weight = 0;
+        if (sem == "vdbfusion_f64") p.semantics = TSDF_SEM_VDBFUSION_F64;
+    }
+    if (argc >= 7) p.max_batch = (uint32_t)std::atoi(argv[6]);
     File in(argv[1], "rb");
     if (!in.f) {
         std::perror(argv[1]);
@@ -73,40 +83,75 @@ int main(int argc, char** argv) {
     int rc = tsdf_create(&p, &ctx);
     if (rc != TSDF_OK) return die(ctx, "tsdf_create", rc);
 
-    // the callback body: one PointCloud2 per scan, integrated as it arrives (the library copies
-    // the points before returning, so the buffer is reused at once)
-    std::vector<uint8_t> cloud;
-    uint64_t n_scans = 0;
+    // The input is read into memory first (one buffer per message, owned like a ROS ConstPtr), so
+    // the timed part is the node's work: the callback bodies, the library's staging and the GPU.
+    struct Msg {
+        char type;
+        int64_t t;
+        tsdf_map::Pose pose;
+        uint64_t n;
+        uint32_t step, xoff;
+        int32_t f64;
+        double origin[3];
+        std::shared_ptr<std::vector<uint8_t>> data;
+    };
+    std::vector<Msg> msgs;
     char magic[8] = {0};
     const bool topics = std::fread(magic, 1, 8, in.f) == 8 && std::memcmp(magic, "TSDFSTR2", 8) == 0;
     if (!topics) std::rewind(in.f);
-    tsdf_map::MapCore core(ctx);
-    for (; topics;) {  // the node's subscriptions, in arrival order
-        char type = 0;
-        int64_t t = 0;
-        if (std::fread(&type, 1, 1, in.f) != 1) break;
-        if (std::fread(&t, sizeof t, 1, in.f) != 1) break;
-        if (type == 'P') {
-            tsdf_map::Pose ps;
-            ps.t_ns = t;
-            if (std::fread(ps.p, sizeof(double), 3, in.f) != 3 ||
-                std::fread(ps.q, sizeof(double), 4, in.f) != 4)
-                break;
-            rc = core.on_pose(ps);
-        } else if (type == 'C') {
-            uint64_t n = 0;
-            uint32_t step = 0, xoff = 0;
-            int32_t f64 = 0;
-            if (std::fread(&n, sizeof n, 1, in.f) != 1 || std::fread(&step, 4, 1, in.f) != 1 ||
-                std::fread(&xoff, 4, 1, in.f) != 1 || std::fread(&f64, 4, 1, in.f) != 1)
-                break;
-            cloud.resize((size_t)n * step);
-            if (n && std::fread(cloud.data(), step, n, in.f) != n) break;
-            rc = core.on_cloud(t, cloud.data(), n, step, xoff, f64);
+    for (;;) {
+        Msg m{};
+        if (topics) {
+            if (std::fread(&m.type, 1, 1, in.f) != 1) break;
+            if (std::fread(&m.t, sizeof m.t, 1, in.f) != 1) break;
+            if (m.type == 'P') {
+                m.pose.t_ns = m.t;
+                if (std::fread(m.pose.p, sizeof(double), 3, in.f) != 3 ||
+                    std::fread(m.pose.q, sizeof(double), 4, in.f) != 4)
+                    break;
+                msgs.push_back(m);
+                continue;
+            }
+            if (m.type != 'C') {
+                std::fprintf(stderr, "tsdf_replay: bad record type %d\n", (int)m.type);
+                tsdf_destroy(ctx);
+                return 1;
+            }
         } else {
-            std::fprintf(stderr, "tsdf_replay: bad record type %d\n", (int)type);
+            m.type = 'S';
+        }
+        if (std::fread(&m.n, sizeof m.n, 1, in.f) != 1) break;
+        if (std::fread(&m.step, 4, 1, in.f) != 1 || std::fread(&m.xoff, 4, 1, in.f) != 1 ||
+            std::fread(&m.f64, 4, 1, in.f) != 1 ||
+            (!topics && std::fread(m.origin, sizeof(double), 3, in.f) != 3)) {
+            std::fprintf(stderr, "tsdf_replay: truncated record %zu\n", msgs.size());
             tsdf_destroy(ctx);
             return 1;
+        }
+        m.data = std::make_shared<std::vector<uint8_t>>((size_t)m.n * m.step);
+        if (m.n && std::fread(m.data->data(), m.step, m.n, in.f) != m.n) {
+            std::fprintf(stderr, "tsdf_replay: truncated data of record %zu\n", msgs.size());
+            tsdf_destroy(ctx);
+            return 1;
+        }
+        msgs.push_back(std::move(m));
+    }
+
+    // the callback bodies: scans go through MapCore (topic stream: the node's object) or straight
+    // to tsdf_integrate (one PointCloud2 per scan; the library copies the points before it returns)
+    uint64_t n_scans = 0;
+    tsdf_map::MapCore core(ctx);
+    const auto t_start = std::chrono::steady_clock::now();
+    for (Msg& m : msgs) {
+        if (m.type == 'P') {
+            rc = core.on_pose(m.pose);
+        } else if (m.type == 'C') {
+            const void* bytes = m.data->data();
+            rc = core.on_cloud(m.t, std::move(m.data), bytes, m.n, m.step, m.xoff, m.f64);
+        } else {
+            rc = tsdf_integrate(ctx, m.data->data(), m.n, m.step, m.xoff, m.f64, m.origin);
+            m.data.reset();
+            n_scans++;
         }
         if (rc != TSDF_OK) {
             const int r = die(ctx, "tsdf_integrate", rc);
@@ -124,36 +169,12 @@ int main(int argc, char** argv) {
                     (unsigned long long)core.counts().dropped_gap,
                     (unsigned long long)core.counts().dropped_queue);
     }
-    for (; !topics;) {
-        uint64_t n = 0;
-        uint32_t step = 0, xoff = 0;
-        int32_t f64 = 0;
-        double origin[3];
-        if (std::fread(&n, sizeof n, 1, in.f) != 1) break;
-        if (std::fread(&step, sizeof step, 1, in.f) != 1 ||
-            std::fread(&xoff, sizeof xoff, 1, in.f) != 1 ||
-            std::fread(&f64, sizeof f64, 1, in.f) != 1 ||
-            std::fread(origin, sizeof(double), 3, in.f) != 3) {
-            std::fprintf(stderr, "tsdf_replay: truncated header of scan %llu\n",
-                         (unsigned long long)n_scans);
-            tsdf_destroy(ctx);
-            return 1;
-        }
-        cloud.resize((size_t)n * step);
-        if (n && std::fread(cloud.data(), step, n, in.f) != n) {
-            std::fprintf(stderr, "tsdf_replay: truncated data of scan %llu\n",
-                         (unsigned long long)n_scans);
-            tsdf_destroy(ctx);
-            return 1;
-        }
-        rc = tsdf_integrate(ctx, cloud.data(), n, step, xoff, f64, origin);
-        if (rc != TSDF_OK) {
-            const int r = die(ctx, "tsdf_integrate", rc);
-            tsdf_destroy(ctx);
-            return r;
-        }
-        n_scans++;
-    }
+    rc = tsdf_sync(ctx);
+    if (rc != TSDF_OK) return die(ctx, "tsdf_sync", rc);
+    const double secs =
+        std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
+    std::printf("tsdf_replay: rate %.1f scans/s (%llu scans in %.3f s, read + integrate + sync)\n",
+                secs > 0 ? (double)n_scans / secs : 0.0, (unsigned long long)n_scans, secs);
 
     // the node's map write-out
     uint64_t nb = 0;

@@ -25,6 +25,7 @@
 #include <sensor_msgs/PointField.h>
 
 #include <cstdio>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -67,21 +68,27 @@ class TsdfMapNode {
         int max_bricks = 1 << 20;
         pnh.param("max_bricks", max_bricks, max_bricks);  // initial pool; grows on demand
         p.max_bricks = (uint64_t)max_bricks;
-        std::string sem;
-        pnh.param<std::string>("semantics", sem, "vdbfusion");
+        std::string sem;  // default: VDBFusion at upstream's own precisions
+        pnh.param<std::string>("semantics", sem, "vdbfusion_f64");
         if (sem == "voxblox") {  // backend idx 2's rule
             p.semantics = TSDF_SEM_VOXBLOX;
             pnh.param("max_ray_length_m", p.max_range, 5.0);
             double mw = 10000.0;
             pnh.param("max_weight", mw, mw);
             p.max_weight = (float)mw;
-            bool clear = true, drop = true;
+            bool clear = true, drop = true, const_w = false;  // voxblox's Config defaults
             pnh.param("allow_clear", clear, clear);
             pnh.param("use_weight_dropoff", drop, drop);
+            pnh.param("use_const_weight", const_w, const_w);  // false: 1 / z^2 (the pose's z axis)
             p.allow_clear = clear ? 1 : 0;
             p.use_weight_dropoff = drop ? 1 : 0;
+            p.depth_weight = const_w ? 0 : 1;
         } else if (sem == "vdbfusion_f64") {  // upstream's precisions
             p.semantics = TSDF_SEM_VDBFUSION_F64;
+        } else if (sem != "vdbfusion") {  // the fp32 restatement
+            ROS_FATAL("unknown semantics '%s' (vdbfusion_f64, vdbfusion, voxblox)", sem.c_str());
+            ros::shutdown();
+            return;
         }
         if (tsdf_create(&p, &ctx_) != TSDF_OK) {
             ROS_FATAL("tsdf_create failed (see stderr)");
@@ -138,8 +145,12 @@ class TsdfMapNode {
             return;
         }
         const uint64_t n = (uint64_t)msg->width * msg->height;
-        check(core_->on_cloud((int64_t)msg->header.stamp.toNSec(), msg->data.data(), n,
-                              msg->point_step, (uint32_t)xoff, f64),
+        // no copy: MapCore holds the message itself while the cloud waits for its pose (the
+        // deleter keeps a reference to the ConstPtr), and the library copies the points once,
+        // into pinned staging
+        std::shared_ptr<const void> keep(msg.get(), [m = msg](const void*) mutable { m.reset(); });
+        check(core_->on_cloud((int64_t)msg->header.stamp.toNSec(), std::move(keep), msg->data.data(),
+                              n, msg->point_step, (uint32_t)xoff, f64),
               "integrate");
     }
 

@@ -7,8 +7,8 @@ in the reference snapshot and so are listed but not constructibl
 from ._abi import BRICK_SIDE, BRICK_VOX  # noqa: F401
 from ._lib import HIP_LIB, load_hip_library  # noqa: F401
 from .volume import (HipTSDFVolume, SimpleTsdfIntegrator, TSDFVolume,  # noqa: F401
-                     TsdfError, TsdfIntegratorConfig, bricks_to_voxels, sector_ids,
-                     select_sector)
+                     TsdfError, TsdfIntegratorConfig, bricks_to_voxels, integrate_sectors,
+                     sector_ids, select_sector)
 
 MAP_BACKENDS = {
     0: "CHAD TSDF (absent from the reference snapshot)",
@@ -26,7 +26,7 @@ def make_backend(idx=MAP_BACKEND_IDX, **kw):
         return HipTSDFVolume(**kw)
     if idx in (2, 3) and kw.pop("on_gpu", False):
         # the MI355X backend restating CPU backend idx 2 (Voxblox) or 3 (VDBFusion) semantics
-        return HipTSDFVolume(semantics="voxblox" if idx == 2 else "vdbfusion", **kw)
+        return HipTSDFVolume(semantics="voxblox" if idx == 2 else "vdbfusion_f64", **kw)
     if idx in MAP_BACKENDS:
         raise NotImplementedError("MAP_BACKEND_IDX=%d: %s" % (idx, MAP_BACKENDS[idx]))
     raise ValueError("unknown MAP_BACKEND_IDX %r" % idx)

@@ -116,6 +116,8 @@ SIGNATURES = {
     "tsdf_last_error": (C.c_char_p, [P]),
     "tsdf_integrate": (C.c_int, [P, P, C.c_uint64, C.c_uint32, C.c_uint32, C.c_int32, D3]),
     "tsdf_integrate_pose": (C.c_int, [P, P, C.c_uint64, C.c_uint32, C.c_uint32, C.c_int32, D3]),
+    "tsdf_integrate_sectors": (C.c_int, [C.POINTER(P), C.c_uint32, P, C.c_uint64, C.c_uint32,
+                                         C.c_uint32, C.c_int32, D3]),
     "tsdf_integrate_device": (C.c_int, [P, P, C.c_uint64, D3]),
     "tsdf_integrate_batch_device": (C.c_int, [P, P, U64P, C.c_uint32, D3]),
     "tsdf_integrate_batch_device_pose": (C.c_int, [P, P, U64P, C.c_uint32, D3]),

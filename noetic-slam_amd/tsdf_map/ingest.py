@@ -8,6 +8,7 @@ its stamp: linear in position, slerp in orientation, between the bracketing pose
 outside the track or next to a gap wider than `max_gap_ms` are skipped (and counted).
 """
 import bisect
+import math
 
 import numpy as np
 
@@ -18,16 +19,28 @@ DLIO_POSE = "/robot/dlio/odom_node/pose"
 
 
 def _slerp(q0, q1, a):
-    q0, q1 = np.asarray(q0, np.float64), np.asarray(q1, np.float64)
-    d = float(np.dot(q0, q1))
-    if d < 0.0:
-        q1, d = -q1, -d
+    """Shortest-arc slerp (normalised lerp above a dot of 0.9995), op for op the C++ twin's
+    (host/tsdf_map_core.h PoseTrack::slerp: sequential sums, libm acos / sin), so the node and the
+    ingest give the same bits."""
+    q0 = [float(v) for v in q0]
+    q1 = [float(v) for v in q1]
+    d = 0.0
+    for k in range(4):
+        d += q0[k] * q1[k]
+    sg = -1.0 if d < 0.0 else 1.0
+    q1 = [sg * v for v in q1]
+    d *= sg
     if d > 0.9995:
-        q = q0 + a * (q1 - q0)
+        q = [q0[k] + a * (q1[k] - q0[k]) for k in range(4)]
     else:
-        th = np.arccos(d)
-        q = (np.sin((1.0 - a) * th) * q0 + np.sin(a * th) * q1) / np.sin(th)
-    return q / np.linalg.norm(q)
+        th = math.acos(d)
+        x, y, z = math.sin((1.0 - a) * th), math.sin(a * th), math.sin(th)
+        q = [(x * q0[k] + y * q1[k]) / z for k in range(4)]
+    n = 0.0
+    for k in range(4):
+        n += q[k] * q[k]
+    n = math.sqrt(n)
+    return np.array([v / n for v in q], np.float64)
 
 
 class PoseTrack:

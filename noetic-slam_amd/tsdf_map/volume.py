@@ -310,6 +310,25 @@ class TSDFVolume:
         self._check(self._lib.tsdf_reset_stats(self._ctx), "reset_stats")
 
 
+def integrate_sectors(volumes, points, extrinsic):
+    """tsdf_integrate_sectors: one host cloud for the sector-sharded contexts `volumes` (volume k
+    created with n_sectors = len(volumes), sector = k, one per GPU): classified and split on the
+    host, each volume receives only its sector's points (live N-GPU input)."""
+    pts = np.ascontiguousarray(points)
+    if pts.ndim != 2 or pts.shape[1] != 3 or pts.dtype not in (np.float32, np.float64):
+        raise ValueError("points must be np.ndarray(n, 3) of float32 / float64")
+    pose = _pose_of(extrinsic)
+    if pose is None:
+        pose = np.concatenate([_origin_of(extrinsic), [0.0, 0.0, 0.0, 1.0]])
+    v0 = volumes[0]
+    ctxs = (C.c_void_p * len(volumes))(*[v._ctx.value for v in volumes])
+    is64 = pts.dtype == np.float64
+    rc = v0._lib.tsdf_integrate_sectors(ctxs, len(volumes), pts.ctypes.data_as(C.c_void_p),
+                                        pts.shape[0], 24 if is64 else 12, 0, 1 if is64 else 0,
+                                        _d3(np.ascontiguousarray(pose, np.float64)))
+    v0._check(rc, "integrate_sectors")
+
+
 def bricks_to_voxels(coords, sdf, weight):
     coords = np.asarray(coords, np.int64).reshape(-1, 3)
     s = np.asarray(sdf, np.float32).reshape(-1, 8, 8, 8)

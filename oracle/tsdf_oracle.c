@@ -889,6 +889,18 @@ static int integrate_scan(tsdf_ctx* c, const void* pts, uint64_t n, uint32_t poi
 
 int tsdf_sync(tsdf_ctx* c) { return c ? TSDF_OK : TSDF_EINVAL; }
 
+/* The GPU library's diagnostics, present so that a C++ host links against either library: the
+ * oracle records no kernel times and writes no per-batch metrics log. */
+int tsdf_set_profiling(tsdf_ctx* c, int32_t on) {
+    (void)on;
+    return c ? TSDF_OK : TSDF_EINVAL;
+}
+
+int tsdf_set_metrics_log(tsdf_ctx* c, const char* path) {
+    if (!c) return TSDF_EINVAL;
+    return path ? set_err(c, TSDF_EINVAL, "the oracle writes no metrics log") : TSDF_OK;
+}
+
 int tsdf_query_dense(tsdf_ctx* c, const int32_t lo[3], const int32_t hi[3], float* sdf,
                      float* weight) {
     if (!c || !lo || !hi) return TSDF_EINVAL;

@@ -69,7 +69,8 @@ def test_replay_driver_against_oracle_library(tmp_path, sim, semantics):
     subprocess.check_call([str(exe), str(tmp_path / "in.scans"), str(tmp_path / "out.bricks"),
                            "0.05", "0.15", semantics])
     got = bricks_to_voxels(*read_bricks(tmp_path / "out.bricks"))
-    ref = oracle_voxels(scans, semantics=semantics)
+    # tsdf_default_params: Voxblox's 1/z^2 weight (upstream's default), the world z axis here
+    ref = oracle_voxels(scans, semantics=semantics, use_const_weight=False)
     assert got[0].shape[0] > 1000
     for a, b in zip(got, ref):
         assert np.array_equal(a, b)
@@ -86,7 +87,7 @@ def test_replay_driver_on_gpu_bitwise(tmp_path, sim, semantics):
                           "0.15", semantics], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stderr
     got = bricks_to_voxels(*read_bricks(tmp_path / "out.bricks"))
-    ref = oracle_voxels(scans, semantics=semantics)
+    ref = oracle_voxels(scans, semantics=semantics, use_const_weight=False)
     assert got[0].shape[0] > 1000
     assert np.array_equal(got[0], ref[0]) and np.array_equal(got[2], ref[2])
     assert np.array_equal(got[1].view(np.uint32), ref[1].view(np.uint32))
@@ -94,7 +95,7 @@ def test_replay_driver_on_gpu_bitwise(tmp_path, sim, semantics):
 
 # ---- the node's two subscriptions: clouds paired with the 100 Hz pose track (host/tsdf_map_core.h)
 
-def topic_stream(sim):
+def topic_stream(sim, tilt=0.0):
     """(records, expected clouds with their origins): DLIO-like arrival order — poses at 100 Hz,
     each cloud stamped 3 ms after a pose sample and arriving before the sample that brackets it;
     one cloud older than the track and one inside a 60 ms pose gap are dropped."""
@@ -105,7 +106,10 @@ def topic_stream(sim):
 
     def pose(t):
         a = (t - t0) * 1e-9
-        return (2.0 + 3.0 * np.cos(0.3 * a), -1.0 + 3.0 * np.sin(0.3 * a), 0.05 * a), (0, 0, 0, 1)
+        # tilt: the sensor pitches and yaws over time (its z axis matters for Voxblox's 1/z^2)
+        h, r = 0.5 * tilt * a, 0.5 * (0.3 * a)
+        q = (np.sin(h) * np.cos(r), np.sin(h) * np.sin(r), np.cos(h) * np.sin(r), np.cos(h) * np.cos(r))
+        return (2.0 + 3.0 * np.cos(0.3 * a), -1.0 + 3.0 * np.sin(0.3 * a), 0.05 * a), q
 
     clouds = {0: 0, 1: 1, 2: 5, 3: 9}
     recs.append(("C", t0 - 5_000_000, decimate(sim.scan(7)[0], 16)))  # before the track: dropped
@@ -127,7 +131,7 @@ def topic_stream(sim):
     p, q = pose(t)
     track.add(t, p, q)
     recs.append(("P", t, (p, q)))
-    return recs, [(pts, track.at(tc)[0]) for tc, pts in want]
+    return recs, [(pts, np.concatenate(track.at(tc))) for tc, pts in want]
 
 
 def write_topics(path, recs):
@@ -163,15 +167,37 @@ def test_topic_stream_pairs_poses_like_ingest(tmp_path, sim):
         assert np.array_equal(a, b)
 
 
-@pytest.mark.gpu
-def test_topic_stream_on_gpu_bitwise(tmp_path, sim):
-    exe = os.path.join(REPO, "noetic-slam_amd", "lib", "tsdf_replay")
-    recs, want = topic_stream(sim)
+def test_topic_stream_voxblox_depth_weight_pairs_orientation(tmp_path, sim):
+    """The slerped orientation reaches the library (tsdf_integrate_pose): Voxblox's 1/z^2 weights
+    of a tilting sensor equal integrating the clouds with ingest's poses (the same slerp)."""
+    lib = oracle.load()
+    del lib
+    exe = tmp_path / "tsdf_replay_oracle"
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-o", str(exe),
+                           os.path.join(HOST, "tsdf_replay.cpp"),
+                           "-L" + os.path.dirname(oracle.LIB_PATH), "-ltsdf_oracle",
+                           "-Wl,-rpath," + os.path.dirname(oracle.LIB_PATH)])
+    recs, want = topic_stream(sim, tilt=0.7)
     write_topics(tmp_path / "in.topics", recs)
-    out = subprocess.run([exe, str(tmp_path / "in.topics"), str(tmp_path / "out.bricks")],
-                         capture_output=True, text=True, timeout=120)
+    subprocess.run([str(exe), str(tmp_path / "in.topics"), str(tmp_path / "out.bricks"), "0.05",
+                    "0.15", "voxblox"], capture_output=True, text=True, check=True)
+    got = bricks_to_voxels(*read_bricks(tmp_path / "out.bricks"))
+    ref = oracle_voxels(want, semantics="voxblox", use_const_weight=False)
+    assert np.unique(got[2]).size > 50  # depth weights, not counts
+    for a, b in zip(got, ref):
+        assert np.array_equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("semantics", ["vdbfusion", "voxblox"])
+def test_topic_stream_on_gpu_bitwise(tmp_path, sim, semantics):
+    exe = os.path.join(REPO, "noetic-slam_amd", "lib", "tsdf_replay")
+    recs, want = topic_stream(sim, tilt=0.7)
+    write_topics(tmp_path / "in.topics", recs)
+    out = subprocess.run([exe, str(tmp_path / "in.topics"), str(tmp_path / "out.bricks"), "0.05",
+                          "0.15", semantics], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stderr
     got = bricks_to_voxels(*read_bricks(tmp_path / "out.bricks"))
-    ref = oracle_voxels(want)
+    ref = oracle_voxels(want, semantics=semantics, use_const_weight=False)
     assert np.array_equal(got[0], ref[0]) and np.array_equal(got[2], ref[2])
     assert np.array_equal(got[1].view(np.uint32), ref[1].view(np.uint32))

@@ -195,3 +195,29 @@ def test_border_reduce_two_processes(tmp_path, sim):
     ri, rs, rw = ref.export_voxels()
     assert np.array_equal(mi, ri) and np.array_equal(mw, rw)
     assert np.max(np.abs(ms - rs)) <= 1e-5
+
+
+@pytest.mark.parametrize("n,f64", [(3, False), (4, True)])
+def test_integrate_sectors_host_split_bitwise(sim, n, f64):
+    """tsdf_integrate_sectors (the live N-GPU input): one host cloud classified and
+    split on the host over n sector contexts equals each context integrating the full cloud with
+    its in-kernel sector filter (the oracle), bit for bit; the sectors' rays add up to the scan."""
+    from tsdf_map import integrate_sectors
+    yaw0 = 0.4
+    g = [hip(n_sectors=n, sector=r, sector_yaw0=yaw0, max_batch=2) for r in range(n)]
+    o = [ora(n_sectors=n, sector=r, sector_yaw0=yaw0) for r in range(n)]
+    rays = 0
+    for k in (0, 1, 9):
+        pts, org = sim.scan(k)
+        pts = np.ascontiguousarray(pts[::2])
+        if f64:
+            pts = pts.astype(np.float64)
+        q = np.array([0.0, 0.0, np.sin(0.1 * k), np.cos(0.1 * k)])
+        integrate_sectors(g, pts, np.concatenate([org, q]))
+        for v in o:
+            v.integrate(pts, org)
+        rays += pts.shape[0]
+    for r in range(n):
+        g[r].sync()
+        assert voxels_equal_bitwise(g[r].export_voxels(), o[r].export_voxels()), r
+    assert sum(v.stats()["n_points_in"] for v in g) == rays  # each point went to one context

@@ -1,0 +1,50 @@
+"""The ROS1 node source (noetic-slam_amd/ros/tsdf_map_node.cpp) compiled and run off ROS: the
+image has no ROS, so tests/ros_stubs stand in for roscpp and the four message types the node uses
+(the node had never been compiled by anything).  Linked against the oracle library
+(same C-ABI), the node's own main() runs; the stub spin() replays a DLIO-like topic stream into
+its subscriptions, and the map the node writes at shutdown must equal integrating the same clouds
+from the pose track (tests/test_host_replay.py's stream)."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle
+from conftest import REPO
+from test_host_replay import oracle_voxels, read_bricks, topic_stream, write_topics
+from tsdf_map import bricks_to_voxels
+
+NODE = os.path.join(REPO, "noetic-slam_amd", "ros", "tsdf_map_node.cpp")
+STUBS = os.path.join(REPO, "tests", "ros_stubs")
+
+
+@pytest.fixture(scope="module")
+def node_exe(tmp_path_factory):
+    oracle.load()
+    exe = tmp_path_factory.mktemp("node") / "tsdf_map_node"
+    subprocess.check_call(["g++", "-O1", "-std=c++17", "-Wall", "-Wextra", "-Werror", "-I", STUBS,
+                           "-o", str(exe), NODE, "-L" + os.path.dirname(oracle.LIB_PATH),
+                           "-ltsdf_oracle", "-Wl,-rpath," + os.path.dirname(oracle.LIB_PATH)])
+    return str(exe)
+
+
+@pytest.mark.parametrize("semantics", ["vdbfusion_f64", "vdbfusion", "voxblox"])
+def test_node_runs_topic_stream(tmp_path, sim, node_exe, semantics):
+    recs, want = topic_stream(sim, tilt=0.5)
+    write_topics(tmp_path / "in.topics", recs)
+    out = tmp_path / "map.bricks"
+    env = dict(os.environ, TSDF_STUB_STREAM=str(tmp_path / "in.topics"),
+               TSDF_STUB_PARAMS="map_path=%s;min_range=0;semantics=%s;max_ray_length_m=1000" %
+                                (out, semantics))
+    r = subprocess.run([node_exe], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert "saved" in r.stderr
+    got = bricks_to_voxels(*read_bricks(out))
+    kw = dict(semantics=semantics)
+    if semantics == "voxblox":
+        kw.update(max_range=1000.0, use_const_weight=False)  # the node's voxblox defaults
+    ref = oracle_voxels(want, **kw)
+    assert got[0].shape[0] > 1000
+    for a, b in zip(got, ref):
+        assert np.array_equal(a, b)
