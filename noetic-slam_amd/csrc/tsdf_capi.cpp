@@ -922,7 +922,8 @@ void tsdf_destroy(tsdf_ctx* c) {
                    c->W2[0].ord_hist, c->W2[1].ord_hist,    c->W2[1].pair,    c->W2[1].blk,
                    c->W2[1].blk_n, c->W2[1].fb,        c->W2[1].smp,     c->W2[1].active,
                    c->W2[0].cagg,    c->W2[1].cagg,      c->W2[0].act,     c->W2[1].act,
-                   c->W2[0].spn,     c->W2[1].spn,       c->W2[0].smw,     c->W2[1].smw};
+                   c->W2[0].spn,     c->W2[1].spn,       c->W2[0].smw,     c->W2[1].smw,
+                   c->W2[0].plan,    c->W2[1].plan};
     for (void* d : dev)
         if (d) (void)hipFree(d);
     for (int i = 0; i < 2; i++) {
@@ -1064,6 +1065,7 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
         HIPCHK(c, hipMalloc(&W.pair, (c->fused ? 4 : slots) * sizeof(uint32_t)));
         HIPCHK(c, hipMalloc(&W.blk, (size_t)c->max_blocks * 2 * HCAP * sizeof(uint4)));
         HIPCHK(c, hipMalloc(&W.blk_n, (size_t)c->max_blocks * 2 * sizeof(uint32_t)));
+        HIPCHK(c, hipMalloc(&W.plan, (size_t)c->max_blocks * 2 * PLAN_STRIDE * sizeof(uint32_t)));
         HIPCHK(c, hipMalloc(&W.fb, (size_t)W.max_fb * sizeof(uint4)));
         HIPCHK(c, hipMalloc(&W.smp, (size_t)W.max_smp * sizeof(uint2)));
         if (c->R.depth_w) HIPCHK(c, hipMalloc(&W.smw, (size_t)W.max_smp * sizeof(float)));
@@ -1346,32 +1348,42 @@ int tsdf_integrate_sectors(tsdf_ctx* const* ctxs, uint32_t n_ctx, const void* pt
             std::memcpy(v, q, 12);
         }
     };
+    // the kernels' in_sector test on each context's bounds, with the pseudo-angle formed once
     auto sector_of = [&](const float v[3]) -> int {
-        const float dx = v[0] - ox, dy = v[1] - oy;
-        for (uint32_t k = 0; k < n_ctx; k++)
-            if (in_sector(ctxs[k]->R, dx, dy)) return (int)k;
+        const float a = pseudo_angle(v[0] - ox, v[1] - oy);
+        for (uint32_t k = 0; k < n_ctx; k++) {
+            const RayConst& R = ctxs[k]->R;
+            if (!R.sec_on) return 0;
+            if (R.sec_wrap ? (a >= R.sec_lo || a < R.sec_hi) : (a >= R.sec_lo && a < R.sec_hi))
+                return (int)k;
+        }
         return -1;  // NaN: no sector (every kernel would drop the ray)
     };
     const int parts = (c0->pack && n >= (1u << 15)) ? c0->pack->parts() : 1;
     std::vector<uint64_t> cnt((size_t)parts * n_ctx, 0), at((size_t)parts * n_ctx, 0);
+    std::vector<int8_t> sec(n);  // each point's sector, from the counting pass
     auto count = [&](int part) {
         const uint64_t i0 = n * part / parts, i1 = n * (part + 1) / parts;
+        uint64_t cl[TSDF_MAX_WORLD] = {};  // local counts (the parts' rows share cache lines)
         float v[3];
         for (uint64_t i = i0; i < i1; i++) {
             xyz_at(i, v);
             const int k = sector_of(v);
-            if (k >= 0) cnt[(size_t)part * n_ctx + k]++;
+            sec[i] = (int8_t)k;
+            if (k >= 0) cl[k]++;
         }
+        for (uint32_t k = 0; k < n_ctx; k++) cnt[(size_t)part * n_ctx + k] = cl[k];
     };
     auto scatter = [&](int part) {
         const uint64_t i0 = n * part / parts, i1 = n * (part + 1) / parts;
         uint64_t pos[TSDF_MAX_WORLD];
         for (uint32_t k = 0; k < n_ctx; k++) pos[k] = at[(size_t)part * n_ctx + k];
-        float v[3];
         for (uint64_t i = i0; i < i1; i++) {
+            const int k = sec[i];
+            if (k < 0) continue;
+            float v[3];
             xyz_at(i, v);
-            const int k = sector_of(v);
-            if (k >= 0) std::memcpy(h[k] + 3 * pos[k]++, v, 12);
+            std::memcpy(h[k] + 3 * pos[k]++, v, 12);
         }
     };
     if (parts > 1) c0->pack->run(count);

@@ -49,6 +49,15 @@ constexpr int RPB = TSDF_RPB;          // rays per k_count / k_place block (one 
 constexpr int HCAP = TSDF_HCAP;        // LDS brick-hash slots per k_count block (~300-800 used)
 constexpr int LDS_PROBES = 64;         // probe limit before a pair takes the global fallback
 constexpr int MAX_IN_BRICK = 22;       // a line visits at most 8+8+8-2 voxels of an 8^3 brick
+// k_place's LDS staging: samples per workgroup (6 B each; 4 workgroups per CU), the bitmap words
+// of run starts, and the staging plan k_count hands over per half block (Work::plan: the bitmap
+// words, their exclusive popcount prefix as u16 pairs, then the staged sample count)
+#ifndef TSDF_PLC_STAGE
+#define TSDF_PLC_STAGE 3800
+#endif
+constexpr int PLC_STAGE = TSDF_PLC_STAGE;
+constexpr int PLC_WORDS = (PLC_STAGE + 31) / 32;
+constexpr int PLAN_STRIDE = ((PLC_WORDS + (PLC_WORDS + 1) / 2 + 1) + 15) & ~15;
 // single-walk front end (tsdf_walk.hip): rays per k_walk workgroup (one per lane; half an RPB
 // block) and samples per span record
 constexpr int WLK_THREADS = RPB / 2;
@@ -170,6 +179,7 @@ struct Work {
                      // rank in the (brick, scan) cell,
                      // run offset in the workgroup's sample order, run samples | LDS slot << 16)
     uint32_t* blk_n; // n_blocks * 2: runs in each list
+    uint32_t* plan;  // n_blocks * 2 * PLAN_STRIDE: k_place's staging plan per half (k_count)
     uint4* fb;       // fallback pairs: (tidx, scan, rank, 0)
     uint2* smp;  // x = truncated sdf (f32 bits), y = scan << 9 | local voxel
     float* smw;  // Voxblox 1/z^2 (sem 3): each sample's weight, same index as smp

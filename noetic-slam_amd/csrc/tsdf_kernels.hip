@@ -92,6 +92,9 @@ __global__ __launch_bounds__(CNT_THREADS, SEM == 2 ? TSDF_F64_COUNT_WAVES : 1) v
     __shared__ unsigned long long red[2][CNT_THREADS / 64];
     __shared__ unsigned long long s_wsum[CNT_THREADS / 64];
     __shared__ uint32_t s_wcnt[CNT_THREADS / 64];
+#ifndef TSDF_NO_PLAN
+    __shared__ uint32_t s_bm[2][PLC_WORDS];  // per half: staging positions where a run starts
+#endif
     Counters* C = &G->ctr[parity];  // zeroed by the previous batch of this parity (k_finish)
     // sector sharding: every GPU sees every scan, and a block of 1024 consecutive rays (~3 degrees
     // of azimuth) usually lies wholly in one sector; the workgroups take the blocks k_sector_flags
@@ -108,6 +111,9 @@ __global__ __launch_bounds__(CNT_THREADS, SEM == 2 ? TSDF_F64_COUNT_WAVES : 1) v
         s_key[j] = EMPTY_KEY;
         s_cnt[j] = 0u;
     }
+#ifndef TSDF_NO_PLAN
+    for (int j = threadIdx.x; j < 2 * PLC_WORDS; j += CNT_THREADS) (&s_bm[0][0])[j] = 0u;
+#endif
     __syncthreads();
     const uint32_t maxp = Wk.maxp;
     uint32_t valid = 0, npairs = 0;
@@ -317,6 +323,15 @@ __global__ __launch_bounds__(CNT_THREADS, SEM == 2 ? TSDF_F64_COUNT_WAVES : 1) v
         if (threadIdx.x == CNT_THREADS - 1) {
             Wk.blk_n[2 * bx] = totc & 0xFFFFu;
             Wk.blk_n[2 * bx + 1] = totc >> 16;
+#ifndef TSDF_NO_PLAN
+            // each half's staged sample count: its samples, up to the staging capacity
+            unsigned long long tot = 0;
+            for (int w = 0; w < CNT_THREADS / 64; w++) tot += s_wsum[w];
+            Wk.plan[(size_t)(2 * bx) * PLAN_STRIDE + PLAN_STRIDE - 1] =
+                min((uint32_t)tot, (uint32_t)PLC_STAGE);
+            Wk.plan[(size_t)(2 * bx + 1) * PLAN_STRIDE + PLAN_STRIDE - 1] =
+                min((uint32_t)(tot >> 32), (uint32_t)PLC_STAGE);
+#endif
         }
     }
     // The thread's SPT slots go to the global table in three batched stages, so their round trips
@@ -365,13 +380,41 @@ __global__ __launch_bounds__(CNT_THREADS, SEM == 2 ? TSDF_F64_COUNT_WAVES : 1) v
         }
         if (n0) {
             bt0[idx0++] = make_uint4(tx, rk, off0, n0 | ((uint32_t)slot << 16));
+#ifndef TSDF_NO_PLAN
+            if (off0 < (uint32_t)PLC_STAGE) atomicOr(&s_bm[0][off0 >> 5], 1u << (off0 & 31));
+#endif
             off0 += n0;
         }
         if (n1) {
             bt1[idx1++] = make_uint4(tx, rk + n0, off1, n1 | ((uint32_t)slot << 16));
+#ifndef TSDF_NO_PLAN
+            if (off1 < (uint32_t)PLC_STAGE) atomicOr(&s_bm[1][off1 >> 5], 1u << (off1 & 31));
+#endif
             off1 += n1;
         }
     }
+#ifndef TSDF_NO_PLAN
+    // k_place's staging plan for each half: the run-start bitmap and its exclusive popcount
+    // prefix per word (wave h writes half h's)
+    __syncthreads();
+    {
+        const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+        if (wv < 2) {
+            constexpr int WPL = (PLC_WORDS + 63) / 64;
+            static_assert(WPL == 2, "two bitmap words per lane");
+            uint32_t* pl = Wk.plan + (size_t)(2 * bx + wv) * PLAN_STRIDE;
+            const int w0 = 2 * ln, w1 = 2 * ln + 1;
+            const uint32_t b0 = w0 < PLC_WORDS ? s_bm[wv][w0] : 0u;
+            const uint32_t b1 = w1 < PLC_WORDS ? s_bm[wv][w1] : 0u;
+            const uint32_t c0 = (uint32_t)__popc(b0), cs = c0 + (uint32_t)__popc(b1);
+            const uint32_t pre = wave_incl_scan(cs) - cs;
+            if (w0 < PLC_WORDS) pl[w0] = b0;
+            if (w1 < PLC_WORDS) pl[w1] = b1;
+            // the prefix of words w0, w1 as one u16 pair (little endian: w0 low)
+            if (w0 < PLC_WORDS) pl[PLC_WORDS + ln] = (pre & 0xFFFFu) | ((pre + c0) << 16);
+        }
+    }
+#endif
     // block-reduce the stats, one atomic per block on a shard picked by block index
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     unsigned long long v = wave_sum<unsigned long long>(valid);
@@ -678,25 +721,22 @@ __global__ __launch_bounds__(CMP_THREADS) void k_compact_write(uint32_t n_scans,
 #define TSDF_PLC_PHASE
 #endif
 constexpr int PLC_THREADS = RPB / 2;  // one ray per lane, half a k_count workgroup's rays
-#ifndef TSDF_PLC_STAGE
-#define TSDF_PLC_STAGE 3800
-#endif
-constexpr int PLC_STAGE = TSDF_PLC_STAGE;  // staged samples per workgroup (6 B each; 4 workgroups per CU)
 
 template <int SEM>
 __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) void k_place(const float* __restrict__ xyz, BatchRef D,
                                                       RayConst R, Table T, Work Wk,
                                                       const Globals* __restrict__ G, int parity) {
-    constexpr int PLC_WORDS = (PLC_STAGE + 31) / 32;
     __shared__ uint32_t s_base[HCAP];      // run -> first sample of the run in the brick segment
     __shared__ uint16_t s_loff[HCAP];      // run -> offset in the workgroup's sample order
     __shared__ uint16_t s_ord[HCAP];       // staged runs in staging order
     __shared__ uint32_t s_bits[PLC_WORDS]; // staging positions where a run starts
-    __shared__ uint16_t s_wpre[PLC_WORDS]; // run starts in the words before
+    __shared__ uint16_t s_wpre[(PLC_WORDS + 1) & ~1]; // run starts in the words before
     __shared__ float st_s[PLC_STAGE];      // staged samples
     __shared__ uint16_t st_l[PLC_STAGE];
     __shared__ float st_w[SEM == 3 ? PLC_STAGE : 1];  // Voxblox 1/z^2: the samples' weights
+#if defined(TSDF_NO_PLAN) || defined(TSDF_ABLATE_PL_EMPTY)
     __shared__ uint32_t s_nst;             // staged samples (end of the last staged run)
+#endif
 #ifdef TSDF_PLC_PHASE  // diagnostic build: thread 0's clock at the phase boundaries
     unsigned long long pt[6];
     if (threadIdx.x == 0) pt[0] = clock64();
@@ -737,6 +777,15 @@ __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) v
     const uint32_t nruns = Wk.blk_n[wb];
     static_assert(PLC_THREADS <= HCAP, "a lane's first list entry lies inside the list");
     const uint4 e0 = bt[threadIdx.x];
+#ifndef TSDF_NO_PLAN
+    // k_count's staging plan: bitmap words, their prefix (u16 pairs) and the staged count
+    const uint32_t* pl = Wk.plan + (size_t)wb * PLAN_STRIDE;
+    static_assert(PLC_WORDS <= PLC_THREADS, "one bitmap word per lane");
+    const uint32_t plan_bits = threadIdx.x < (uint32_t)PLC_WORDS ? pl[threadIdx.x] : 0u;
+    const uint32_t plan_pre =
+        threadIdx.x < (uint32_t)((PLC_WORDS + 1) / 2) ? pl[PLC_WORDS + threadIdx.x] : 0u;
+    const uint32_t plan_nst = pl[PLAN_STRIDE - 1];
+#endif
     // a run's absolute sample position is its (brick, scan) cell (absolute after k_compact) + its
     // rank
     const uint32_t base0 = (threadIdx.x < nruns && e0.x != NO_PAIR)
@@ -747,9 +796,15 @@ __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) v
     const bool ok = i < r1 && Walk<SEM>::init(R, D, t, px, py, pz, r);
     // sector sharding: a half block without a ray of this GPU's sector has no samples to place
     if (R.sec_on && !__syncthreads_or(ok)) return;
+#ifndef TSDF_NO_PLAN
+    if (threadIdx.x < (uint32_t)PLC_WORDS) s_bits[threadIdx.x] = plan_bits;
+    if (threadIdx.x < (uint32_t)((PLC_WORDS + 1) / 2))
+        reinterpret_cast<uint32_t*>(s_wpre)[threadIdx.x] = plan_pre;
+#else
     for (int j = threadIdx.x; j < PLC_WORDS; j += PLC_THREADS) s_bits[j] = 0u;
     if (threadIdx.x == 0) s_nst = 0u;
     __syncthreads();
+#endif
 #ifdef TSDF_PLC_PHASE
     if (threadIdx.x == 0) pt[1] = clock64();
 #endif
@@ -763,8 +818,12 @@ __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) v
         s_loff[slot] = stg ? (uint16_t)e.z : (uint16_t)0xFFFFu;
         if (stg) {
             s_ord[j] = (uint16_t)slot;
+#ifdef TSDF_NO_PLAN
             atomicOr(&s_bits[e.z >> 5], 1u << (e.z & 31));
             atomicMax(&s_nst, min(e.z + n, (uint32_t)PLC_STAGE));
+#else
+            (void)n;
+#endif
         }
     };
     if (threadIdx.x < nruns) fill(threadIdx.x, e0, base0);
@@ -779,6 +838,7 @@ __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) v
 #ifdef TSDF_ABLATE_PL_PROLOGUE  // diagnostic build: the prologue (loads, run tables) only
     if (D.n_scans != 0xFFFFFFFFu) return;
 #endif
+#ifdef TSDF_NO_PLAN
     if (threadIdx.x < 64) {  // exclusive prefix of run starts per bitmap word (one wave)
         constexpr int WPL = (PLC_WORDS + 63) / 64;
         uint32_t cnt[WPL], sum = 0;
@@ -798,6 +858,7 @@ __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) v
         }
     }
     __syncthreads();
+#endif
 #ifdef TSDF_PLC_PHASE
     if (threadIdx.x == 0) pt[3] = clock64();
 #endif
@@ -931,8 +992,10 @@ __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) v
     // copy-out: one lane per staged sample; its run = the last run start at or before it
 #ifdef TSDF_ABLATE_PL_NOCOPY
     const uint32_t nst = 0;
-#else
+#elif defined(TSDF_NO_PLAN)
     const uint32_t nst = s_nst;
+#else
+    const uint32_t nst = plan_nst;
 #endif
     for (uint32_t j = threadIdx.x; j < nst; j += PLC_THREADS) {
         const uint32_t wd = j >> 5;
