@@ -128,14 +128,21 @@ struct PackPool {
     int parts() const { return (int)th.size() + 1; }
     // f(part) for part = 0 .. parts() - 1, part 0 on the calling thread
     void run(const std::function<void(int)>& f) {
+        start(f, 0);
+        f(0);
+        wait();
+    }
+    // the workers run f(base + 1) .. f(base + workers) while the caller goes on; wait() joins
+    void start(const std::function<void(int)>& f, int base) {
         {
             std::lock_guard<std::mutex> l(m);
-            job = f;
+            job = base ? std::function<void(int)>([f, base](int part) { f(base + part); }) : f;
             busy = (int)th.size();
             gen++;
         }
         go.notify_all();
-        f(0);
+    }
+    void wait() {
         std::unique_lock<std::mutex> l(m);
         done.wait(l, [&] { return busy == 0; });
     }
@@ -213,6 +220,8 @@ struct tsdf_ctx {
     // (tsdf_params.walk) and the band's walk fits nstep register slots per ray
     bool fused = false;
     int nstep = 0;
+    // batches of at most small_ns scans take k_integrate_small (TSDF_SMALL_NS; 0: never)
+    int small_ns = 8;
     // host-pointer path: pinned double buffer per scan; the pending batch's points are staged in
     // stage2[batch parity]
     float* h_stage[2] = {nullptr, nullptr};
@@ -259,6 +268,10 @@ struct tsdf_ctx {
     struct BatchInfo { uint64_t id; uint32_t scans; uint64_t points; };
     std::vector<BatchInfo> metrics_info;  // host-side facts of the batches not yet reported
     PackPool* pack = nullptr;  // host staging threads (tsdf_integrate of strided records)
+    // tsdf_integrate_sectors' packed scan (xyz, then the sector per point) when this context
+    // leads the split: cache-resident between its two passes
+    std::vector<float> split_xyz;
+    std::vector<int8_t> split_sec;
     uint64_t n_grows = 0, n_replayed = 0;
 };
 
@@ -365,6 +378,8 @@ static int launch(tsdf_ctx* c, const float* d_xyz, BatchDesc& D) {
     HIPCHK(c, hipMemcpyAsync(ds, hs, (D.n_scans + 1) * sizeof(ScanRec), hipMemcpyHostToDevice, st));
     HIPCHK(c, hipEventRecord(c->ring_ev[slot], st));
     const BatchRef B{D.n_scans, D.n_blocks, ds};
+    // a small batch (a live node's 1-8 scans) fuses wave-per-brick, in table order (no k_order)
+    const bool small = !c->fused && D.n_scans <= (uint32_t)c->small_ns;
     const int k_front = c->fused ? KIND_WALK : KIND_COUNT;
     const int k_back = c->fused ? KIND_SPANS : KIND_PLACE;
     if (D.n_blocks) {
@@ -376,7 +391,7 @@ static int launch(tsdf_ctx* c, const float* d_xyz, BatchDesc& D) {
         if (tm) tm->begin(KIND_COMPACT, st);
         HIPCHK(c, launch_compact(B, T, W, c->G, par, c->fused, st));
 #ifndef TSDF_NO_ORDER
-        HIPCHK(c, launch_order(W, c->G, par, st));
+        if (!small) HIPCHK(c, launch_order(W, c->G, par, st));
 #endif
         if (tm) tm->end(KIND_COMPACT, st);
     }
@@ -390,13 +405,17 @@ static int launch(tsdf_ctx* c, const float* d_xyz, BatchDesc& D) {
     if (c->batch_id > 0 && cross) HIPCHK(c, hipStreamWaitEvent(st, c->ev_integ[par ^ 1], 0));
     if (D.n_blocks) {
         if (tm) tm->begin(KIND_INTEGRATE, st);
+        if (small) {
+            HIPCHK(c, launch_integrate_small(B, c->R, T, W, c->Pl, c->G, par, st));
+        } else {
 #ifndef TSDF_NO_ORDER
-        Work Wi = W;
-        Wi.active = W.active_ord;  // largest bricks first (k_order)
-        HIPCHK(c, launch_integrate(B, c->R, T, Wi, c->Pl, c->G, par, c->fused, c->max_batch > 64, st));
+            Work Wi = W;
+            Wi.active = W.active_ord;  // largest bricks first (k_order)
+            HIPCHK(c, launch_integrate(B, c->R, T, Wi, c->Pl, c->G, par, c->fused, c->max_batch > 64, st));
 #else
-        HIPCHK(c, launch_integrate(B, c->R, T, W, c->Pl, c->G, par, c->fused, c->max_batch > 64, st));
+            HIPCHK(c, launch_integrate(B, c->R, T, W, c->Pl, c->G, par, c->fused, c->max_batch > 64, st));
 #endif
+        }
         if (tm) tm->end(KIND_INTEGRATE, st);
     }
     HIPCHK(c, launch_finish(c->G, par, (uint32_t)c->batch_id, st));
@@ -1075,6 +1094,7 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
         HIPCHK(c, hipMalloc(&c->stage2[q], c->batch_points * 3 * sizeof(float)));
     }
     HIPCHK(c, hipMalloc(&c->G, sizeof(Globals)));
+    if (const char* e = std::getenv("TSDF_SMALL_NS")) c->small_ns = std::max(0, std::min(8, std::atoi(e)));
     {
         // host staging threads: 3 workers + the caller (TSDF_PACK_THREADS overrides; 1 = none)
         int nt = 4;
@@ -1333,42 +1353,71 @@ int tsdf_integrate_sectors(tsdf_ctx* const* ctxs, uint32_t n_ctx, const void* pt
         HIPCHK(c, hipEventSynchronize(c->stage_done[hb[k]]));
         h[k] = c->h_stage[hb[k]];
     }
-    // classify + pack, in point chunks over c0's staging threads: count per (part, sector), then
-    // each part writes its points at its prefix (the parts keep the input order within a sector)
+    // Two passes over point chunks, on the staging threads of ALL the contexts (each GPU's host
+    // share): (1) read the records once, pack xyz into c0's scratch and classify each point,
+    // counting per (part, sector); (2) copy the packed points, still in cache, to their sector's
+    // pinned buffer at the part's prefix (the parts keep the input order within a sector).
     const char* base = static_cast<const char*>(pts);
-    auto xyz_at = [&](uint64_t i, float v[3]) {
-        const char* q = base + i * point_step + xyz_offset;
-        if (xyz_is_f64) {
-            double d[3];
-            std::memcpy(d, q, sizeof d);
-            v[0] = (float)d[0];
-            v[1] = (float)d[1];
-            v[2] = (float)d[2];
-        } else {
-            std::memcpy(v, q, 12);
+    // The sector of a point: the starts s_k of the N sectors, rotated to ascending order
+    // u_j = s_(r+j), give sector (r + #{j: a >= u_j} - 1) mod N -- the kernels' in_sector test on
+    // every context's [lo, hi) bounds (the wrap sector holds a < u_0 and a >= u_(N-1)), one
+    // pseudo-angle and N compares per point.  NaN: no sector (every kernel drops the ray).
+    const bool sharded = n_ctx > 1 && c0->R.sec_on;
+    float u[TSDF_MAX_WORLD];
+    uint32_t r0 = 0;
+    if (sharded) {
+        for (uint32_t k = 1; k < n_ctx; k++)
+            if (ctxs[k]->R.sec_lo < ctxs[r0]->R.sec_lo) r0 = k;
+        for (uint32_t j = 0; j < n_ctx; j++) {
+            u[j] = ctxs[(r0 + j) % n_ctx]->R.sec_lo;
+            if (j && !(u[j] > u[j - 1]))
+                return fail(c0, TSDF_EINVAL, "sector starts of the contexts are not distinct");
         }
+    }
+    // parts: c0's pool (caller + workers), then every other context's workers
+    int pbase[TSDF_MAX_WORLD + 1];
+    pbase[0] = 0;
+    for (uint32_t k = 0; k < n_ctx; k++)
+        pbase[k + 1] = pbase[k] + (ctxs[k]->pack ? ctxs[k]->pack->parts() - (k ? 1 : 0) : (k ? 0 : 1));
+    const int parts = n >= (1u << 15) ? pbase[n_ctx] : 1;
+    auto run_parts = [&](const std::function<void(int)>& f) {
+        if (parts == 1) return f(0);
+        for (uint32_t k = 1; k < n_ctx; k++)
+            if (ctxs[k]->pack) ctxs[k]->pack->start(f, pbase[k] - 1);
+        if (c0->pack) c0->pack->run(f);
+        else f(0);
+        for (uint32_t k = 1; k < n_ctx; k++)
+            if (ctxs[k]->pack) ctxs[k]->pack->wait();
     };
-    // the kernels' in_sector test on each context's bounds, with the pseudo-angle formed once
-    auto sector_of = [&](const float v[3]) -> int {
-        const float a = pseudo_angle(v[0] - ox, v[1] - oy);
-        for (uint32_t k = 0; k < n_ctx; k++) {
-            const RayConst& R = ctxs[k]->R;
-            if (!R.sec_on) return 0;
-            if (R.sec_wrap ? (a >= R.sec_lo || a < R.sec_hi) : (a >= R.sec_lo && a < R.sec_hi))
-                return (int)k;
-        }
-        return -1;  // NaN: no sector (every kernel would drop the ray)
-    };
-    const int parts = (c0->pack && n >= (1u << 15)) ? c0->pack->parts() : 1;
+    if (c0->split_xyz.size() < 3 * n) {
+        c0->split_xyz.resize(3 * n);
+        c0->split_sec.resize(n);
+    }
+    float* xyz = c0->split_xyz.data();
+    int8_t* sec = c0->split_sec.data();
     std::vector<uint64_t> cnt((size_t)parts * n_ctx, 0), at((size_t)parts * n_ctx, 0);
-    std::vector<int8_t> sec(n);  // each point's sector, from the counting pass
-    auto count = [&](int part) {
+    auto classify = [&](int part) {
         const uint64_t i0 = n * part / parts, i1 = n * (part + 1) / parts;
         uint64_t cl[TSDF_MAX_WORLD] = {};  // local counts (the parts' rows share cache lines)
-        float v[3];
         for (uint64_t i = i0; i < i1; i++) {
-            xyz_at(i, v);
-            const int k = sector_of(v);
+            const char* q = base + i * point_step + xyz_offset;
+            float* v = xyz + 3 * i;
+            if (xyz_is_f64) {
+                double d[3];
+                std::memcpy(d, q, sizeof d);
+                v[0] = (float)d[0];
+                v[1] = (float)d[1];
+                v[2] = (float)d[2];
+            } else {
+                std::memcpy(v, q, 12);
+            }
+            int k = 0;
+            if (sharded) {
+                const float a = pseudo_angle(v[0] - ox, v[1] - oy);
+                int c = 0;
+                for (uint32_t j = 0; j < n_ctx; j++) c += a >= u[j] ? 1 : 0;
+                k = a != a ? -1 : (int)((r0 + n_ctx + (uint32_t)c - 1u) % n_ctx);
+            }
             sec[i] = (int8_t)k;
             if (k >= 0) cl[k]++;
         }
@@ -1376,26 +1425,23 @@ int tsdf_integrate_sectors(tsdf_ctx* const* ctxs, uint32_t n_ctx, const void* pt
     };
     auto scatter = [&](int part) {
         const uint64_t i0 = n * part / parts, i1 = n * (part + 1) / parts;
-        uint64_t pos[TSDF_MAX_WORLD];
-        for (uint32_t k = 0; k < n_ctx; k++) pos[k] = at[(size_t)part * n_ctx + k];
+        float* dst[TSDF_MAX_WORLD];
+        for (uint32_t k = 0; k < n_ctx; k++) dst[k] = h[k] + 3 * at[(size_t)part * n_ctx + k];
         for (uint64_t i = i0; i < i1; i++) {
             const int k = sec[i];
             if (k < 0) continue;
-            float v[3];
-            xyz_at(i, v);
-            std::memcpy(h[k] + 3 * pos[k]++, v, 12);
+            std::memcpy(dst[k], xyz + 3 * i, 12);
+            dst[k] += 3;
         }
     };
-    if (parts > 1) c0->pack->run(count);
-    else count(0);
+    run_parts(classify);
     std::vector<uint64_t> tot(n_ctx, 0);
     for (uint32_t k = 0; k < n_ctx; k++)
         for (int q = 0; q < parts; q++) {
             at[(size_t)q * n_ctx + k] = tot[k];
             tot[k] += cnt[(size_t)q * n_ctx + k];
         }
-    if (parts > 1) c0->pack->run(scatter);
-    else scatter(0);
+    run_parts(scatter);
     // each context: its sector's points to its GPU, into its pending batch
     for (uint32_t k = 0; k < n_ctx; k++) {
         tsdf_ctx* c = ctxs[k];

@@ -280,6 +280,10 @@ hipError_t launch_rehash(const Table& T, uint32_t n, Globals* G, hipStream_t st)
 // Orders the batch's active bricks by size class, largest first (k_integrate's load balance).
 hipError_t launch_order(const Work& Wk, Globals* G, int parity, hipStream_t st);
 // fused: samples through the span list (single walk); big: batches of more than 64 scans
+// k_integrate_small: batches of at most a few scans, one wave per brick (tsdf_integrate.hip)
+hipError_t launch_integrate_small(const BatchRef& D, const RayConst& R, const Table& T,
+                                  const Work& Wk, const Pool& Pl, Globals* G, int parity,
+                                  hipStream_t st);
 hipError_t launch_integrate(const BatchRef& D, const RayConst& R, const Table& T, const Work& Wk,
                             const Pool& Pl, Globals* G, int parity, bool fused, bool big,
                             hipStream_t st);

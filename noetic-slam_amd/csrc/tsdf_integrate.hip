@@ -543,25 +543,168 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchRef D, Table T, 
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// k_integrate_small: the same update for batches of at most SMALL_NS scans (a live node's 1-8 scan
+// batches), one WAVE per brick instead of a workgroup.  With few scans a voxel's chain is at most
+// SMALL_NS steps, so the window / mask / live-cell machinery of k_integrate (six workgroup barriers
+// per brick) costs more than it saves: here a wave keeps its brick's 512 (S, W) in registers (voxel
+// lane + 64 k, k < 8), and takes the brick's scans in order:
+//   accumulate scan t's samples (one contiguous segment) into dense per-voxel LDS cells
+//   (int64 fixed-point sum, count / weight sum) with LDS atomics, then every lane fuses its 8
+//   voxels' cells with the same arithmetic as k_integrate's chains and clears them.
+// No barrier (wave-private LDS), no k_order (the list is taken in table order), four bricks per
+// workgroup.  The field is bitwise k_integrate's (tests/test_gpu_parity.py small-batch cases).
+constexpr int SML_WAVES = 4;
+template <int SEM>
+__global__ __launch_bounds__(SML_WAVES * 64) void k_integrate_small(BatchRef D, Table T, Work Wk,
+                                                                   Pool Pl, Globals* G, int parity,
+                                                                   RayConst R) {
+    constexpr bool VB = SEM == 1 || SEM == 3;
+    typedef typename std::conditional<VB, unsigned long long, uint32_t>::type CellB;
+    __shared__ unsigned long long sA[SML_WAVES][BRICK_VOX];
+    __shared__ CellB sB[SML_WAVES][BRICK_VOX];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    unsigned long long* A = sA[wid];
+    CellB* Bc = sB[wid];
+    Counters* C = &G->ctr[parity];
+    const uint32_t n_active = min(C->n_active, Wk.max_active);
+    const uint32_t ns = D.n_scans;
+    const bool commit = !(G->retry && (C->ovf || G->failed));
+    const float tau = R.tau;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        A[lane + 64 * k] = 0ull;
+        Bc[lane + 64 * k] = 0;
+    }
+    uint32_t nvox = 0, ndirty = 0;
+    const uint32_t stride = gridDim.x * SML_WAVES;
+    uint32_t a = blockIdx.x * SML_WAVES + wid;
+    uint4 rec = a < n_active ? Wk.active[a] : make_uint4(0u, 0u, 0u, 0u);
+    for (; a < n_active; a += stride) {
+        const uint4 cur = rec;
+        if (a + stride < n_active) rec = Wk.active[a + stride];  // the next brick's record
+        const uint32_t h = cur.x, base = cur.z, n = cur.w;
+        const bool has = cur.y < T.max_bricks;
+        // lane t <= ns: start of scan t's samples relative to the segment (ns: the end)
+        const uint32_t cst = (uint32_t)lane < ns ? T.cell[(size_t)h * T.cell_stride + lane] - base : n;
+        const float* Sg = Pl.sdf + (size_t)(has ? cur.y : 0) * BRICK_VOX;
+        const float* Wg = Pl.weight + (size_t)(has ? cur.y : 0) * BRICK_VOX;
+        float s[8], w[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            s[k] = has ? Sg[lane + 64 * k] : R.bg;
+            w[k] = has ? Wg[lane + 64 * k] : 0.0f;
+        }
+        uint32_t dirty = 0;
+        for (uint32_t t = 0; t < ns; t++) {
+            const uint32_t q0 = __shfl(cst, (int)t), q1 = __shfl(cst, (int)t + 1);
+            if (q0 == q1) continue;  // uniform: no sample of scan t in this brick
+            for (uint32_t i = q0 + lane; i < q1; i += 64) {
+                if (base + i >= Wk.max_smp) continue;  // capacity overflow (reported by k_compact)
+                const uint2 c = Wk.smp[base + i];
+                const uint32_t l = c.y & 511u;
+                const float sv = __uint_as_float(c.x);
+                if constexpr (VB) {
+                    float wv;
+                    if constexpr (SEM == 3) wv = Wk.smw[base + i];
+                    else wv = vb_weight(R, 1.0f, sv);
+                    atomicAdd(&A[l], (unsigned long long)(long long)((sv * wv) * 4294967296.0f));
+                    atomicAdd(&Bc[l], (unsigned long long)(long long)(wv * 4294967296.0f));
+                } else {
+                    atomicAdd(&A[l], (unsigned long long)(long long)(sv * 4294967296.0f));
+                    atomicAdd(&Bc[l], 1u);
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the cells complete
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const uint32_t v = lane + 64 * k;
+                const CellB b = Bc[v];
+                if (b == 0) continue;  // every live cell has b > 0 (Voxblox: w >= 2^-16)
+                const float fa = (float)((double)(long long)A[v] * (1.0 / 4294967296.0));
+                A[v] = 0ull;
+                Bc[v] = 0;
+                if constexpr (VB) {
+                    const float fb = (float)((double)(long long)b * (1.0 / 4294967296.0));
+                    const float nw = w[k] + fb;
+                    float sn = (fa + s[k] * w[k]) / nw;
+                    sn = sn > 0.0f ? (sn < tau ? sn : tau) : (-tau < sn ? sn : -tau);
+                    const bool ok = !(nw < 1e-6f);
+                    s[k] = ok ? sn : s[k];
+                    w[k] = ok ? (nw < R.max_weight ? nw : R.max_weight) : w[k];
+                } else {
+                    const float nw = w[k] + (float)b;
+                    s[k] = (s[k] * w[k] + fa) / nw;
+                    w[k] = nw;
+                }
+                dirty |= 1u << k;
+                nvox++;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // cleared before the next scan
+            __builtin_amdgcn_wave_barrier();
+        }
+        if (has && commit) {
+            float* So = Pl.sdf + (size_t)cur.y * BRICK_VOX;
+            float* Wo = Pl.weight + (size_t)cur.y * BRICK_VOX;
+#pragma unroll
+            for (int k = 0; k < 8; k++)
+                if (dirty & (1u << k)) {
+                    So[lane + 64 * k] = s[k];
+                    Wo[lane + 64 * k] = w[k];
+                }
+        }
+        ndirty += __popc(dirty);
+        // zero the brick's cell row (k_compact prefixes whole uint4 groups) for the next batch
+        for (uint32_t q = lane; q < T.cell_stride; q += 64) T.cell[(size_t)h * T.cell_stride + q] = 0u;
+    }
+    const unsigned long long v = wave_sum<unsigned long long>(nvox);
+    const unsigned long long d = wave_sum<unsigned long long>(ndirty);
+    if (lane == 0) {
+        if (v) atomicAdd(&C->n_vox[blockIdx.x & 7], v);  // -> G->tot_vox at k_finish
+        if (d) atomicAdd(&C->n_dirty[blockIdx.x & 7], d);
+    }
+}
+
 // Grid = exactly the workgroups the device holds at once (CUs x resident workgroups per CU, from
 // the occupancy API: VGPRs or LDS, whichever binds): every workgroup of the grid-stride loop starts
 // at once, none waits for a second dispatch round.
+template <typename K>
+static int resident_grid(K kernel, int threads, int fallback_per_cu) {
+    int dev = 0, cus = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, 0) != hipSuccess ||
+        cus <= 0 || per_cu <= 0) {
+        cus = 256;
+        per_cu = fallback_per_cu;
+    }
+    return cus * per_cu;
+}
+
 template <int SEM, int MAXS, bool FUSED>
 static int integrate_grid() {
     static int grid = 0;
-    if (grid == 0) {
-        int dev = 0, cus = 0, per_cu = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_integrate<SEM, MAXS, FUSED>,
-                                                         INT_THREADS, 0) != hipSuccess ||
-            cus <= 0 || per_cu <= 0) {
-            cus = 256;
-            per_cu = INT_BLOCKS_PER_CU;
-        }
-        grid = cus * per_cu;
-    }
+    if (grid == 0) grid = resident_grid(k_integrate<SEM, MAXS, FUSED>, INT_THREADS, INT_BLOCKS_PER_CU);
     return grid;
+}
+
+template <int SEM>
+static void integrate_small_sem(const BatchRef& D, const RayConst& R, const Table& T, const Work& Wk,
+                                const Pool& Pl, Globals* G, int parity, hipStream_t st) {
+    static int grid = 0;
+    if (grid == 0) grid = resident_grid(k_integrate_small<SEM>, SML_WAVES * 64, 4);
+    k_integrate_small<SEM><<<grid, SML_WAVES * 64, 0, st>>>(D, T, Wk, Pl, G, parity, R);
+}
+
+hipError_t launch_integrate_small(const BatchRef& D, const RayConst& R, const Table& T,
+                                  const Work& Wk, const Pool& Pl, Globals* G, int parity,
+                                  hipStream_t st) {
+    // SEM 2 (VDBFusion at double precision) fuses like SEM 0
+    if (R.sem == 1) integrate_small_sem<1>(D, R, T, Wk, Pl, G, parity, st);
+    else if (R.sem == 3) integrate_small_sem<3>(D, R, T, Wk, Pl, G, parity, st);
+    else integrate_small_sem<0>(D, R, T, Wk, Pl, G, parity, st);
+    return hipGetLastError();
 }
 
 template <int SEM, int MAXS, bool FUSED>

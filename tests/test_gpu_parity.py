@@ -106,6 +106,36 @@ def test_batch_composition_is_invisible(sim):
         assert np.array_equal(x, y)
 
 
+@pytest.mark.parametrize("semantics", ["vdbfusion", "vdbfusion_f64", "voxblox", "voxblox_z2"])
+def test_small_batch_kernel_bitwise(sim, monkeypatch, semantics):
+    """Batches of <= 8 scans fuse in k_integrate_small (one wave per brick, dense LDS cells, no
+    k_order); TSDF_SMALL_NS=0 forces k_integrate.  Both equal the oracle bit for bit at 1, 3 and 8
+    scans per batch, on a full scan (long per-voxel runs of one scan) and with carving."""
+    from tsdf_map import bricks_to_voxels
+    kw = dict(semantics="voxblox", use_const_weight=False) if semantics == "voxblox_z2" else \
+        dict(semantics=semantics)
+    full = [sim.scan(0)] + [(decimate(p, 4), org) for p, org in (sim.scan(k) for k in range(1, 6))]
+    carve = [(decimate(p, 16), org) for p, org in (sim.scan(k) for k in range(4))]
+    for scans, extra in ((full, {}), (carve, dict(space_carving=True, max_range=20.0))):
+        o = ora(**kw, **extra)
+        for p, org in scans:
+            o.integrate(p, org)
+        ref = o.export_voxels()
+        for mb in (1, 3, 8):
+            got = {}
+            for small in ("8", "0") if mb != 3 else ("8",):
+                monkeypatch.setenv("TSDF_SMALL_NS", small)
+                g = hip(max_batch=mb, **kw, **extra)
+                for p, org in scans:
+                    g.integrate(p, org)
+                got[small] = g.export_bricks()  # the same batches: the same pool slots
+            for x, y in zip(bricks_to_voxels(*got["8"]), ref):
+                assert np.array_equal(x, y), (mb, extra)
+            if "0" in got:
+                for x, y in zip(got["8"], got["0"]):
+                    assert np.array_equal(x, y), (mb, extra)
+
+
 def test_pipelined_and_64_scan_batches_bitwise(sim):
     """Overlapped batches (tsdf_params.pipeline: batch b+1's count/compact/place beside batch b's
     integrate, two streams) and 64-scan batches give the oracle's bits, through the host queue and

@@ -197,7 +197,7 @@ def test_border_reduce_two_processes(tmp_path, sim):
     assert np.max(np.abs(ms - rs)) <= 1e-5
 
 
-@pytest.mark.parametrize("n,f64", [(3, False), (4, True)])
+@pytest.mark.parametrize("n,f64", [(3, False), (4, True), (8, False)])
 def test_integrate_sectors_host_split_bitwise(sim, n, f64):
     """tsdf_integrate_sectors (the live N-GPU input): one host cloud classified and
     split on the host over n sector contexts equals each context integrating the full cloud with
@@ -210,13 +210,18 @@ def test_integrate_sectors_host_split_bitwise(sim, n, f64):
     for k in (0, 1, 9):
         pts, org = sim.scan(k)
         pts = np.ascontiguousarray(pts[::2])
+        # rays along every sector start (boundary ties) and NaN rows (no sector: dropped)
+        th = yaw0 + 2 * np.pi * np.arange(n) / n
+        edge = org[None, :] + np.stack([7.0 * np.cos(th), 7.0 * np.sin(th), np.zeros(n)], 1)
+        pts = np.concatenate([pts, edge.astype(np.float32),
+                              np.full((3, 3), np.nan, np.float32)]).astype(np.float32)
         if f64:
             pts = pts.astype(np.float64)
         q = np.array([0.0, 0.0, np.sin(0.1 * k), np.cos(0.1 * k)])
         integrate_sectors(g, pts, np.concatenate([org, q]))
         for v in o:
             v.integrate(pts, org)
-        rays += pts.shape[0]
+        rays += pts.shape[0] - 3
     for r in range(n):
         g[r].sync()
         assert voxels_equal_bitwise(g[r].export_voxels(), o[r].export_voxels()), r
