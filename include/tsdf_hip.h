@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define TSDF_ABI_VERSION 6
+#define TSDF_ABI_VERSION 7
 #define TSDF_MAX_BATCH 512 /* scans per GPU batch (see tsdf_params.max_batch) */
 #define TSDF_BRICK_SIDE 8 /* voxels per brick edge: a brick is 8^3 = 512 voxels */
 
@@ -248,6 +248,12 @@ int tsdf_get_stats(tsdf_ctx* ctx, tsdf_stats* out);
 int tsdf_reset_stats(tsdf_ctx* ctx);
 /* Record HIP events around every kernel (per-kind device time in tsdf_stats.kernel_ms). */
 int tsdf_set_profiling(tsdf_ctx* ctx, int32_t on);
+/* ABI v7: which launches profiling times.  Kinds whose bit (1 << TSDF_K_*) is in every_mask are
+ * timed on every batch, the other kinds on every period-th batch (period 1: every batch; the
+ * default is every kind on every batch).  A timed kernel records its own dispatch timestamps, which
+ * costs the stream ~5 us per timed launch; bench.py times the dominant kernel on every batch and
+ * samples the rest. */
+int tsdf_set_profiling_period(tsdf_ctx* ctx, uint32_t every_mask, uint32_t period);
 
 /* Append one JSON line per finished GPU batch to the file at `path` (NULL: stop), written at
  * tsdf_sync / read-outs (and every ~250 batches): batch id, scans, points, valid rays, (ray, brick)

@@ -35,13 +35,17 @@ static_assert(TSDF_TILE_WORDS == TILE_WORDS && TSDF_MAX_WORLD == MAX_WORLD, "bor
 namespace {
 
 struct EventTimer final : KernelTimer {
-    struct Rec { int kind; uint64_t batch; hipEvent_t a, b; };
+    struct Rec { int kind; uint64_t batch; hipEvent_t a, b; bool own_a; };
     uint64_t cur_batch = 0;  // the batch being launched (set by launch())
     bool per_batch = false;  // keep per-batch times for the metrics log
     std::vector<std::pair<uint64_t, std::array<double, KIND_N>>> batch_ms;
     std::vector<hipEvent_t> free_ev;
     std::vector<Rec> pending;
     hipEvent_t open_ev[KIND_N] = {};
+    bool open_own[KIND_N] = {};  // open_ev[k] is not also the end of an earlier record
+    uint32_t every_mask = ~0u;   // kinds timed on every batch (tsdf_set_profiling_period)
+    uint32_t period = 1;         // the other kinds: every period-th batch
+    bool want(int kind) const { return ((every_mask >> kind) & 1u) || cur_batch % period == 0; }
     double ms[KIND_N] = {};
     uint64_t launches[KIND_N] = {};
 
@@ -57,14 +61,33 @@ struct EventTimer final : KernelTimer {
     }
     void begin(int kind, hipStream_t st) override {
         open_ev[kind] = get();
+        open_own[kind] = true;
         if (open_ev[kind]) (void)hipEventRecord(open_ev[kind], st);
     }
     void end(int kind, hipStream_t st) override {
         hipEvent_t e = get();
         if (!e || !open_ev[kind]) return;
         (void)hipEventRecord(e, st);
-        pending.push_back({kind, cur_batch, open_ev[kind], e});
+        pending.push_back({kind, cur_batch, open_ev[kind], e, open_own[kind]});
         open_ev[kind] = nullptr;
+    }
+    // events the kernel launch itself records (its dispatch packet's timestamps: KTime)
+    KTime timing(int kind) {
+        hipEvent_t a = get(), b = get();
+        if (!a || !b) return {};
+        pending.push_back({kind, cur_batch, a, b, true});
+        return {a, b};
+    }
+    // end `done` and begin `open` with ONE event, for kernels launched back to back on one stream
+    // (every timing event is a queue barrier with a timestamp: ~4 us each per batch)
+    void next(int done, int open, hipStream_t st) {
+        hipEvent_t e = get();
+        if (!e || !open_ev[done]) return begin(open, st);
+        (void)hipEventRecord(e, st);
+        pending.push_back({done, cur_batch, open_ev[done], e, open_own[done]});
+        open_ev[done] = nullptr;
+        open_ev[open] = e;
+        open_own[open] = false;
     }
     // call only after the stream drained
     void harvest() {
@@ -79,7 +102,7 @@ struct EventTimer final : KernelTimer {
                     batch_ms.back().second[r.kind] += t;
                 }
             }
-            free_ev.push_back(r.a);
+            if (r.own_a) free_ev.push_back(r.a);  // else it is an earlier record's b
             free_ev.push_back(r.b);
         }
         pending.clear();
@@ -89,7 +112,10 @@ struct EventTimer final : KernelTimer {
         std::fill(launches, launches + KIND_N, 0);
     }
     ~EventTimer() override {
-        for (auto& r : pending) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
+        for (auto& r : pending) {
+            if (r.own_a) (void)hipEventDestroy(r.a);
+            (void)hipEventDestroy(r.b);
+        }
         for (auto e : free_ev) (void)hipEventDestroy(e);
     }
 };
@@ -382,41 +408,43 @@ static int launch(tsdf_ctx* c, const float* d_xyz, BatchDesc& D) {
     const bool small = !c->fused && D.n_scans <= (uint32_t)c->small_ns;
     const int k_front = c->fused ? KIND_WALK : KIND_COUNT;
     const int k_back = c->fused ? KIND_SPANS : KIND_PLACE;
+    // per-kernel times: the two-walk kernels record their own dispatch timestamps (KTime, no
+    // marker packets); the single walk's stages are bracketed by marker events
+    auto kt = [&](int kind) { return tm && !c->fused && tm->want(kind) ? tm->timing(kind) : KTime{}; };
     if (D.n_blocks) {
-        if (tm) tm->begin(k_front, st);
+        if (tm && c->fused) tm->begin(k_front, st);
         if (c->R.sec_on) HIPCHK(c, launch_sector_flags(d_xyz, B, c->R, W, c->G, par, st));
         if (c->fused) HIPCHK(c, launch_walk(d_xyz, B, c->R, T, W, c->G, par, c->nstep, st));
-        else HIPCHK(c, launch_count(d_xyz, B, c->R, T, W, c->G, par, st));
-        if (tm) tm->end(k_front, st);
-        if (tm) tm->begin(KIND_COMPACT, st);
-        HIPCHK(c, launch_compact(B, T, W, c->G, par, c->fused, st));
-#ifndef TSDF_NO_ORDER
+        else HIPCHK(c, launch_count(d_xyz, B, c->R, T, W, c->G, par, st, kt(KIND_COUNT)));
+        if (tm && c->fused) tm->next(k_front, KIND_COMPACT, st);
+        HIPCHK(c, launch_compact(B, T, W, c->G, par, c->fused, st, kt(KIND_COMPACT)));
+#if defined(TSDF_SEPARATE_ORDER) && !defined(TSDF_NO_ORDER)
         if (!small) HIPCHK(c, launch_order(W, c->G, par, st));
 #endif
-        if (tm) tm->end(KIND_COMPACT, st);
     }
-    HIPCHK(c, hipEventRecord(c->ev_compact[par], st));
+    if (cross && c->p.pipeline) HIPCHK(c, hipEventRecord(c->ev_compact[par], st));  // batch b+1's wait
     if (D.n_blocks) {
-        if (tm) tm->begin(k_back, st);
+        if (tm && c->fused) tm->next(KIND_COMPACT, k_back, st);
         if (c->fused) HIPCHK(c, launch_spans(B, c->R, T, W, c->G, par, c->nstep, st));
-        else HIPCHK(c, launch_place(d_xyz, B, c->R, T, W, c->G, par, st));
-        if (tm) tm->end(k_back, st);
+        else HIPCHK(c, launch_place(d_xyz, B, c->R, T, W, c->G, par, st, kt(KIND_PLACE)));
+        if (tm && c->fused) tm->end(k_back, st);
     }
     if (c->batch_id > 0 && cross) HIPCHK(c, hipStreamWaitEvent(st, c->ev_integ[par ^ 1], 0));
     if (D.n_blocks) {
-        if (tm) tm->begin(KIND_INTEGRATE, st);
+        if (tm && c->fused) tm->begin(KIND_INTEGRATE, st);
         if (small) {
-            HIPCHK(c, launch_integrate_small(B, c->R, T, W, c->Pl, c->G, par, st));
+            HIPCHK(c, launch_integrate_small(B, c->R, T, W, c->Pl, c->G, par, st, kt(KIND_INTEGRATE)));
         } else {
 #ifndef TSDF_NO_ORDER
             Work Wi = W;
-            Wi.active = W.active_ord;  // largest bricks first (k_order)
-            HIPCHK(c, launch_integrate(B, c->R, T, Wi, c->Pl, c->G, par, c->fused, c->max_batch > 64, st));
+            Wi.active = W.active_ord;  // largest bricks first (k_compact's size order)
 #else
-            HIPCHK(c, launch_integrate(B, c->R, T, W, c->Pl, c->G, par, c->fused, c->max_batch > 64, st));
+            const Work& Wi = W;
 #endif
+            HIPCHK(c, launch_integrate(B, c->R, T, Wi, c->Pl, c->G, par, c->fused, c->max_batch > 64, st,
+                                       kt(KIND_INTEGRATE)));
         }
-        if (tm) tm->end(KIND_INTEGRATE, st);
+        if (tm && c->fused) tm->end(KIND_INTEGRATE, st);
     }
     HIPCHK(c, launch_finish(c->G, par, (uint32_t)c->batch_id, st));
     HIPCHK(c, hipEventRecord(c->ev_integ[par], st));
@@ -1089,7 +1117,9 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
         HIPCHK(c, hipMalloc(&W.smp, (size_t)W.max_smp * sizeof(uint2)));
         if (c->R.depth_w) HIPCHK(c, hipMalloc(&W.smw, (size_t)W.max_smp * sizeof(float)));
         HIPCHK(c, hipMalloc(&W.spn, (size_t)W.max_spn * sizeof(uint32_t)));
-        HIPCHK(c, hipMalloc(&W.ord_hist, 64 * 32 * sizeof(uint32_t)));
+        // (slice, size class) histogram, then first positions (k_compact; zero between batches)
+        HIPCHK(c, hipMalloc(&W.ord_hist, 2 * 64 * 32 * sizeof(uint32_t)));
+        HIPCHK(c, hipMemset(W.ord_hist, 0, 2 * 64 * 32 * sizeof(uint32_t)));
         HIPCHK(c, hipMalloc(&W.act, (size_t)c->max_blocks * sizeof(uint32_t)));
         HIPCHK(c, hipMalloc(&c->stage2[q], c->batch_points * 3 * sizeof(float)));
     }
@@ -1936,6 +1966,15 @@ int tsdf_set_profiling(tsdf_ctx* c, int32_t on) {
     }
     if (!on && c->timer) { delete c->timer; c->timer = nullptr; }
     return (on && !c->timer) ? TSDF_ENOMEM : TSDF_OK;
+}
+
+int tsdf_set_profiling_period(tsdf_ctx* c, uint32_t every_mask, uint32_t period) {
+    if (!c) return TSDF_EINVAL;
+    if (period == 0) return fail(c, TSDF_EINVAL, "profiling period must be >= 1");
+    if (!c->timer) return fail(c, TSDF_EINVAL, "profiling is off (tsdf_set_profiling)");
+    c->timer->every_mask = every_mask;
+    c->timer->period = period;
+    return TSDF_OK;
 }
 
 int tsdf_set_metrics_log(tsdf_ctx* c, const char* path) {

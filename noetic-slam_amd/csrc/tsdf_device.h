@@ -25,6 +25,7 @@
 //           active[..] uint4                    bricks touched by the batch: (table index, pool
 //                                               slot, sample segment offset, sample count)
 #pragma once
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -185,7 +186,7 @@ struct Work {
     float* smw;  // Voxblox 1/z^2 (sem 3): each sample's weight, same index as smp
     uint4* active;  // (h, slot, toff, cnt) per active brick (k_compact)
     uint4* active_ord;  // the same records, largest size class first (k_order; k_integrate's list)
-    uint32_t* ord_hist; // k_order: per (slice, size class) counts, then first positions
+    uint32_t* ord_hist; // per (slice, size class): counts [64][32], then first positions [64][32]
     uint4* cagg;    // k_compact: per table chunk (touched bricks, samples, new bricks), then bases
     uint32_t* act;  // sector sharding: the k_count blocks holding a ray of this GPU's sector (n_act)
     uint32_t* spn;  // single walk: span records (sample position | (samples - 1) << 30), per brick
@@ -248,6 +249,22 @@ enum KernelKind {
 };
 
 // Optional per-kernel HIP-event timing (profiling mode); implemented in tsdf_capi.cpp.
+// Kernel timing through the dispatch packets: a launch given start / stop events records the
+// kernel's own begin / end timestamps (hipExtLaunchKernel), with no marker packet in the stream.
+// A stage of several kernels takes start on its first launch and stop on its last.
+struct KTime {
+    hipEvent_t start = nullptr, stop = nullptr;
+};
+template <typename... KArgs, typename... Args>
+inline void tlaunch(void (*kern)(KArgs...), dim3 grid, dim3 block, hipStream_t st, hipEvent_t e0,
+                    hipEvent_t e1, Args... args) {
+    if (!e0 && !e1) {
+        kern<<<grid, block, 0, st>>>(args...);
+        return;
+    }
+    hipExtLaunchKernelGGL(kern, grid, block, 0, st, e0, e1, 0, args...);
+}
+
 struct KernelTimer {
     virtual void begin(int kind, hipStream_t st) = 0;
     virtual void end(int kind, hipStream_t st) = 0;
@@ -255,7 +272,7 @@ struct KernelTimer {
 };
 
 hipError_t launch_count(const float* d_xyz, const BatchRef& D, const RayConst& R, const Table& T,
-                        const Work& Wk, Globals* G, int parity, hipStream_t st);
+                        const Work& Wk, Globals* G, int parity, hipStream_t st, const KTime& kt = {});
 // table chunks of k_compact (Work::cagg holds two uint4 per chunk)
 constexpr uint32_t CMP_CHUNK = 1024;
 inline uint64_t compact_chunks(uint64_t cap) { return (cap + CMP_CHUNK - 1) / CMP_CHUNK; }
@@ -266,14 +283,14 @@ hipError_t launch_sector_flags(const float* d_xyz, const BatchRef& D, const RayC
 // fused: the single-walk path's 64-bit cells (samples | spans << 32; after k_compact_write the
 // relative sample prefix | absolute span position, with the totals at scan n_scans)
 hipError_t launch_compact(const BatchRef& D, const Table& T, const Work& Wk, Globals* G,
-                          int parity, bool fused, hipStream_t st);
+                          int parity, bool fused, hipStream_t st, const KTime& kt = {});
 // single-walk front end (tsdf_walk.hip); nstep = 16 or 32 register slots per ray
 hipError_t launch_walk(const float* d_xyz, const BatchRef& D, const RayConst& R, const Table& T,
                        const Work& Wk, Globals* G, int parity, int nstep, hipStream_t st);
 hipError_t launch_spans(const BatchRef& D, const RayConst& R, const Table& T, const Work& Wk,
                         Globals* G, int parity, int nstep, hipStream_t st);
 hipError_t launch_place(const float* d_xyz, const BatchRef& D, const RayConst& R, const Table& T,
-                        const Work& Wk, Globals* G, int parity, hipStream_t st);
+                        const Work& Wk, Globals* G, int parity, hipStream_t st, const KTime& kt = {});
 hipError_t launch_finish(Globals* G, int parity, uint32_t batch_id, hipStream_t st);
 // capacity growth: re-insert pool slots [0, n) of the new table from brick_keys
 hipError_t launch_rehash(const Table& T, uint32_t n, Globals* G, hipStream_t st);
@@ -283,10 +300,10 @@ hipError_t launch_order(const Work& Wk, Globals* G, int parity, hipStream_t st);
 // k_integrate_small: batches of at most a few scans, one wave per brick (tsdf_integrate.hip)
 hipError_t launch_integrate_small(const BatchRef& D, const RayConst& R, const Table& T,
                                   const Work& Wk, const Pool& Pl, Globals* G, int parity,
-                                  hipStream_t st);
+                                  hipStream_t st, const KTime& kt = {});
 hipError_t launch_integrate(const BatchRef& D, const RayConst& R, const Table& T, const Work& Wk,
                             const Pool& Pl, Globals* G, int parity, bool fused, bool big,
-                            hipStream_t st);
+                            hipStream_t st, const KTime& kt = {});
 hipError_t launch_query_dense(const Table& T, const Pool& Pl, const int lo[3], const int dims[3],
                               float bg, float* d_sdf, float* d_w, hipStream_t st);
 hipError_t launch_import(const Table& T, const Pool& Pl, const int32_t* d_coords, uint32_t n,

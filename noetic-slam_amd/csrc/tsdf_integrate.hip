@@ -691,53 +691,56 @@ static int integrate_grid() {
 
 template <int SEM>
 static void integrate_small_sem(const BatchRef& D, const RayConst& R, const Table& T, const Work& Wk,
-                                const Pool& Pl, Globals* G, int parity, hipStream_t st) {
+                                const Pool& Pl, Globals* G, int parity, hipStream_t st,
+                                const KTime& kt) {
     static int grid = 0;
     if (grid == 0) grid = resident_grid(k_integrate_small<SEM>, SML_WAVES * 64, 4);
-    k_integrate_small<SEM><<<grid, SML_WAVES * 64, 0, st>>>(D, T, Wk, Pl, G, parity, R);
+    tlaunch(k_integrate_small<SEM>, grid, SML_WAVES * 64, st, kt.start, kt.stop, D, T, Wk, Pl, G,
+            parity, R);
 }
 
 hipError_t launch_integrate_small(const BatchRef& D, const RayConst& R, const Table& T,
                                   const Work& Wk, const Pool& Pl, Globals* G, int parity,
-                                  hipStream_t st) {
+                                  hipStream_t st, const KTime& kt) {
     // SEM 2 (VDBFusion at double precision) fuses like SEM 0
-    if (R.sem == 1) integrate_small_sem<1>(D, R, T, Wk, Pl, G, parity, st);
-    else if (R.sem == 3) integrate_small_sem<3>(D, R, T, Wk, Pl, G, parity, st);
-    else integrate_small_sem<0>(D, R, T, Wk, Pl, G, parity, st);
+    if (R.sem == 1) integrate_small_sem<1>(D, R, T, Wk, Pl, G, parity, st, kt);
+    else if (R.sem == 3) integrate_small_sem<3>(D, R, T, Wk, Pl, G, parity, st, kt);
+    else integrate_small_sem<0>(D, R, T, Wk, Pl, G, parity, st, kt);
     return hipGetLastError();
 }
 
 template <int SEM, int MAXS, bool FUSED>
 static void integrate_sem(const BatchRef& D, const RayConst& R, const Table& T, const Work& Wk,
-                          const Pool& Pl, Globals* G, int parity, hipStream_t st) {
-    k_integrate<SEM, MAXS, FUSED><<<integrate_grid<SEM, MAXS, FUSED>(), INT_THREADS, 0, st>>>(
-        D, T, Wk, Pl, G, parity, R);
+                          const Pool& Pl, Globals* G, int parity, hipStream_t st, const KTime& kt) {
+    tlaunch(k_integrate<SEM, MAXS, FUSED>, integrate_grid<SEM, MAXS, FUSED>(), INT_THREADS, st,
+            kt.start, kt.stop, D, T, Wk, Pl, G, parity, R);
 }
 
 template <bool FUSED>
 static void integrate_mode(const BatchRef& D, const RayConst& R, const Table& T, const Work& Wk,
-                           const Pool& Pl, Globals* G, int parity, bool big, hipStream_t st) {
+                           const Pool& Pl, Globals* G, int parity, bool big, hipStream_t st,
+                           const KTime& kt) {
     // SEM 2 (VDBFusion at double precision) fuses like SEM 0; SEM 3 (Voxblox 1/z^2) never takes
     // the single walk (tsdf_capi.cpp)
     if (R.sem == 1) {
-        if (big) integrate_sem<1, MAX_BATCH, FUSED>(D, R, T, Wk, Pl, G, parity, st);
-        else integrate_sem<1, 64, FUSED>(D, R, T, Wk, Pl, G, parity, st);
+        if (big) integrate_sem<1, MAX_BATCH, FUSED>(D, R, T, Wk, Pl, G, parity, st, kt);
+        else integrate_sem<1, 64, FUSED>(D, R, T, Wk, Pl, G, parity, st, kt);
     } else if (R.sem == 3) {
         if constexpr (!FUSED) {
-            if (big) integrate_sem<3, MAX_BATCH, false>(D, R, T, Wk, Pl, G, parity, st);
-            else integrate_sem<3, 64, false>(D, R, T, Wk, Pl, G, parity, st);
+            if (big) integrate_sem<3, MAX_BATCH, false>(D, R, T, Wk, Pl, G, parity, st, kt);
+            else integrate_sem<3, 64, false>(D, R, T, Wk, Pl, G, parity, st, kt);
         }
     } else {
-        if (big) integrate_sem<0, MAX_BATCH, FUSED>(D, R, T, Wk, Pl, G, parity, st);
-        else integrate_sem<0, 64, FUSED>(D, R, T, Wk, Pl, G, parity, st);
+        if (big) integrate_sem<0, MAX_BATCH, FUSED>(D, R, T, Wk, Pl, G, parity, st, kt);
+        else integrate_sem<0, 64, FUSED>(D, R, T, Wk, Pl, G, parity, st, kt);
     }
 }
 
 hipError_t launch_integrate(const BatchRef& D, const RayConst& R, const Table& T, const Work& Wk,
                             const Pool& Pl, Globals* G, int parity, bool fused, bool big,
-                            hipStream_t st) {
-    if (fused) integrate_mode<true>(D, R, T, Wk, Pl, G, parity, big, st);
-    else integrate_mode<false>(D, R, T, Wk, Pl, G, parity, big, st);
+                            hipStream_t st, const KTime& kt) {
+    if (fused) integrate_mode<true>(D, R, T, Wk, Pl, G, parity, big, st, kt);
+    else integrate_mode<false>(D, R, T, Wk, Pl, G, parity, big, st, kt);
     return hipGetLastError();
 }
 

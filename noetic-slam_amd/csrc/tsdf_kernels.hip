@@ -460,6 +460,29 @@ hipError_t launch_sector_flags(const float* d_xyz, const BatchRef& D, const RayC
 }
 
 // ------------------------------------------------------------------------------------------------
+// Size order: k_integrate hands its workgroups bricks in list order (grid stride), and bricks hold
+// from a few to ~40 k samples, so a random order leaves the kernel waiting on the workgroups that
+// drew several large bricks.  A counting sort by size class (floor(log2(samples)), largest class
+// first) deals the large bricks out first and evenly (greedy largest-first).  Order inside a class
+// is whatever the atomics give: each brick is fused independently, so the field does not depend
+// on it.  k_compact builds the sorted list as it writes the records: k_compact_sum counts the
+// (table slice, size class) histogram, k_compact_scan turns it into first positions, and
+// k_compact_write ranks each record in its (slice, class) with one global atomic (a separate
+// three-launch k_order remains for the ablation build TSDF_SEPARATE_ORDER).
+
+constexpr int ORD_THREADS = 256;
+constexpr int ORD_BLOCKS = 64;  // slices: of the active list (k_order), of the table's chunks (k_compact)
+constexpr int ORD_CLASSES = 32;
+
+__device__ __forceinline__ uint32_t size_class(uint32_t n) {
+    return (uint32_t)__clz(max(n, 1u));  // 31 - floor(log2 n): large bricks -> small index
+}
+// the slice of table chunk c of nch (k_compact's size order)
+__device__ __forceinline__ uint32_t ord_chunk_slice(uint32_t c, uint32_t nch) {
+    return (uint32_t)(((uint64_t)c * ORD_BLOCKS) / nch);
+}
+
+// ------------------------------------------------------------------------------------------------
 // k_compact: per active brick — record segment, new pool slot, per-scan cell prefix
 
 constexpr int CMP_THREADS = 256;
@@ -545,6 +568,10 @@ __global__ __launch_bounds__(CMP_THREADS) void k_compact_sum(uint32_t n_scans, T
         s_acc[0] = 0u;
         s_acc[1] = 0u;
     }
+#ifndef TSDF_SEPARATE_ORDER
+    __shared__ uint32_t s_cls[ORD_CLASSES];  // the chunk's bricks per size class
+    if (threadIdx.x < ORD_CLASSES) s_cls[threadIdx.x] = 0u;
+#endif
     const uint32_t nh = compact_list(T, blockIdx.x * CMP_CHUNK, s_h, s_w, false);
     const uint32_t nq = row_groups<FUSED>(n_scans);  // whole uint4 groups (see cell_stride)
     const uint32_t grp = threadIdx.x / CMP_GROUP, li = threadIdx.x % CMP_GROUP;
@@ -552,7 +579,14 @@ __global__ __launch_bounds__(CMP_THREADS) void k_compact_sum(uint32_t n_scans, T
     for (uint32_t k = grp; k < nh; k += CMP_THREADS / CMP_GROUP) {
         const uint32_t h = s_h[k];
         const uint4* cp = cell_row<FUSED>(T, h);
-        for (uint32_t q = li; q < nq; q += CMP_GROUP) samples += group_count<FUSED>(cp[q]);
+        uint32_t sum = 0;
+        for (uint32_t q = li; q < nq; q += CMP_GROUP) sum += group_count<FUSED>(cp[q]);
+        samples += sum;
+#ifndef TSDF_SEPARATE_ORDER
+#pragma unroll
+        for (int d = CMP_GROUP / 2; d >= 1; d >>= 1) sum += __shfl_xor(sum, d, CMP_GROUP);
+        if (li == 0) atomicAdd(&s_cls[size_class(sum)], 1u);
+#endif
         if (li == 0 && T.slots[h] == UNASSIGNED) nnew++;
     }
     samples = wave_sum<uint32_t>(samples);
@@ -563,6 +597,12 @@ __global__ __launch_bounds__(CMP_THREADS) void k_compact_sum(uint32_t n_scans, T
     }
     __syncthreads();
     if (threadIdx.x == 0) Wk.cagg[blockIdx.x] = make_uint4(nh, s_acc[0], s_acc[1], 0u);
+#ifndef TSDF_SEPARATE_ORDER
+    // the chunk's slice histogram (zeroed again by k_compact_scan once read)
+    if (threadIdx.x < ORD_CLASSES && s_cls[threadIdx.x])
+        atomicAdd(&Wk.ord_hist[ord_chunk_slice(blockIdx.x, gridDim.x) * ORD_CLASSES + threadIdx.x],
+                  s_cls[threadIdx.x]);
+#endif
 }
 
 __global__ __launch_bounds__(CMP_SCAN_THREADS) void k_compact_scan(uint32_t nch, Work Wk,
@@ -593,6 +633,35 @@ __global__ __launch_bounds__(CMP_SCAN_THREADS) void k_compact_scan(uint32_t nch,
         }
         __syncthreads();
     }
+#ifndef TSDF_SEPARATE_ORDER
+    // size order: (slice, class) first positions = the records of larger classes + class k's
+    // records in the slices before (k_order_scan's rule); the histogram is zeroed for the next batch
+    {
+        __shared__ uint32_t s_tot[ORD_CLASSES], s_cbase[ORD_CLASSES];
+        const int t = threadIdx.x;
+        if (t < ORD_CLASSES) {
+            uint32_t sum = 0;
+            for (int b = 0; b < ORD_BLOCKS; b++) sum += Wk.ord_hist[b * ORD_CLASSES + t];
+            s_tot[t] = sum;
+        }
+        __syncthreads();
+        if (t < 64) {
+            const uint32_t v = t < ORD_CLASSES ? s_tot[t] : 0u;
+            const uint32_t incl = wave_incl_scan(v);
+            if (t < ORD_CLASSES) s_cbase[t] = incl - v;
+        }
+        __syncthreads();
+        if (t < ORD_CLASSES) {
+            uint32_t run = s_cbase[t];
+            for (int b = 0; b < ORD_BLOCKS; b++) {
+                const uint32_t v = Wk.ord_hist[b * ORD_CLASSES + t];
+                Wk.ord_hist[ORD_BLOCKS * ORD_CLASSES + b * ORD_CLASSES + t] = run;
+                Wk.ord_hist[b * ORD_CLASSES + t] = 0u;
+                run += v;
+            }
+        }
+    }
+#endif
     if (threadIdx.x == 0) {
         C->n_active = s_carry[0];
         C->cursor = s_carry[1];
@@ -655,8 +724,14 @@ __global__ __launch_bounds__(CMP_THREADS) void k_compact_write(uint32_t n_scans,
                 T.slots[h] = slot;
             }
             // k_integrate's whole per-brick header in one record
-            if (base.x + k < Wk.max_active)
-                Wk.active[base.x + k] = make_uint4(h, slot, base.y + ec, n[j]);
+            const uint4 rec = make_uint4(h, slot, base.y + ec, n[j]);
+            if (base.x + k < Wk.max_active) Wk.active[base.x + k] = rec;
+#ifndef TSDF_SEPARATE_ORDER
+            const uint32_t op = atomicAdd(&Wk.ord_hist[ORD_BLOCKS * ORD_CLASSES +
+                                                       ord_chunk_slice(blockIdx.x, gridDim.x) * ORD_CLASSES +
+                                                       size_class(n[j])], 1u);
+            if (op < Wk.max_active) Wk.active_ord[op] = rec;
+#endif
             s_n[k] = base.y + ec;
         }
         ec += n[j];
@@ -1116,48 +1191,29 @@ static int grid_for(uint64_t items, int per_block, int cap) {
 // One batch is k_count -> k_compact -> k_place -> k_integrate -> k_finish on one stream; the host
 // (tsdf_capi.cpp) interleaves the cross-batch waits between them.
 hipError_t launch_count(const float* d_xyz, const BatchRef& D, const RayConst& R, const Table& T,
-                        const Work& Wk, Globals* G, int parity, hipStream_t st) {
+                        const Work& Wk, Globals* G, int parity, hipStream_t st, const KTime& kt) {
     // sem 3 (Voxblox 1/z^2) counts with Walk<1>: the weight only matters where it is stored
-    if (R.sem == 1 || R.sem == 3) k_count<1><<<D.n_blocks, CNT_THREADS, 0, st>>>(d_xyz, D, R, T, Wk, G, parity);
-    else if (R.sem == 2) k_count<2><<<D.n_blocks, CNT_THREADS, 0, st>>>(d_xyz, D, R, T, Wk, G, parity);
-    else k_count<0><<<D.n_blocks, CNT_THREADS, 0, st>>>(d_xyz, D, R, T, Wk, G, parity);
+    auto k = R.sem == 1 || R.sem == 3 ? k_count<1> : R.sem == 2 ? k_count<2> : k_count<0>;
+    tlaunch(k, D.n_blocks, CNT_THREADS, st, kt.start, kt.stop, d_xyz, D, R, T, Wk, G, parity);
     return hipGetLastError();
 }
 
 hipError_t launch_compact(const BatchRef& D, const Table& T, const Work& Wk, Globals* G,
-                          int parity, bool fused, hipStream_t st) {
+                          int parity, bool fused, hipStream_t st, const KTime& kt) {
     const uint32_t nch = (uint32_t)compact_chunks(T.mask + 1);
-    if (fused) k_compact_sum<true><<<nch, CMP_THREADS, 0, st>>>(D.n_scans, T, Wk);
-    else k_compact_sum<false><<<nch, CMP_THREADS, 0, st>>>(D.n_scans, T, Wk);
+    tlaunch(fused ? k_compact_sum<true> : k_compact_sum<false>, nch, CMP_THREADS, st, kt.start,
+            nullptr, D.n_scans, T, Wk);
     k_compact_scan<<<1, CMP_SCAN_THREADS, 0, st>>>(nch, Wk, G, parity, fused ? 1 : 0);
-    if (fused) k_compact_write<true><<<nch, CMP_THREADS, 0, st>>>(D.n_scans, nch, T, Wk, G, parity);
-    else k_compact_write<false><<<nch, CMP_THREADS, 0, st>>>(D.n_scans, nch, T, Wk, G, parity);
+    tlaunch(fused ? k_compact_write<true> : k_compact_write<false>, nch, CMP_THREADS, st, nullptr,
+            kt.stop, D.n_scans, nch, T, Wk, G, parity);
     return hipGetLastError();
 }
 
 hipError_t launch_place(const float* d_xyz, const BatchRef& D, const RayConst& R, const Table& T,
-                        const Work& Wk, Globals* G, int parity, hipStream_t st) {
-    if (R.sem == 1) k_place<1><<<2 * D.n_blocks, PLC_THREADS, 0, st>>>(d_xyz, D, R, T, Wk, G, parity);
-    else if (R.sem == 3) k_place<3><<<2 * D.n_blocks, PLC_THREADS, 0, st>>>(d_xyz, D, R, T, Wk, G, parity);
-    else if (R.sem == 2) k_place<2><<<2 * D.n_blocks, PLC_THREADS, 0, st>>>(d_xyz, D, R, T, Wk, G, parity);
-    else k_place<0><<<2 * D.n_blocks, PLC_THREADS, 0, st>>>(d_xyz, D, R, T, Wk, G, parity);
+                        const Work& Wk, Globals* G, int parity, hipStream_t st, const KTime& kt) {
+    auto k = R.sem == 1 ? k_place<1> : R.sem == 3 ? k_place<3> : R.sem == 2 ? k_place<2> : k_place<0>;
+    tlaunch(k, 2 * D.n_blocks, PLC_THREADS, st, kt.start, kt.stop, d_xyz, D, R, T, Wk, G, parity);
     return hipGetLastError();
-}
-
-// ------------------------------------------------------------------------------------------------
-// k_order: k_integrate hands its workgroups bricks in list order (grid stride), and bricks hold
-// from a few to ~40 k samples, so a random order leaves the kernel waiting on the workgroups that
-// drew several large bricks.  A counting sort by size class (floor(log2(samples)), largest class
-// first) deals the large bricks out first and evenly (greedy largest-first).  Order inside a class
-// is whatever the atomics give: each brick is fused independently, so the field does not depend
-// on it.
-
-constexpr int ORD_THREADS = 256;
-constexpr int ORD_BLOCKS = 64;  // each takes a contiguous slice of the active list
-constexpr int ORD_CLASSES = 32;
-
-__device__ __forceinline__ uint32_t size_class(uint32_t n) {
-    return (uint32_t)__clz(max(n, 1u));  // 31 - floor(log2 n): large bricks -> small index
 }
 
 __device__ __forceinline__ void ord_slice(uint32_t n_active, uint32_t b, uint32_t& i0,

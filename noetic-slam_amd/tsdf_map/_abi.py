@@ -16,7 +16,7 @@ STATUS_NAMES = {
     TSDF_EHIP: "TSDF_EHIP", TSDF_ENODEV: "TSDF_ENODEV", TSDF_EOVERFLOW: "TSDF_EOVERFLOW",
 }
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 TILE_WORDS = 1028  # TSDF_TILE_WORDS: u32 words of one border-brick tile
 MAX_WORLD = 64
 SEM_VDBFUSION = 0
@@ -129,6 +129,7 @@ SIGNATURES = {
     "tsdf_get_stats": (C.c_int, [P, C.POINTER(TsdfStats)]),
     "tsdf_reset_stats": (C.c_int, [P]),
     "tsdf_set_profiling": (C.c_int, [P, C.c_int32]),
+    "tsdf_set_profiling_period": (C.c_int, [P, C.c_uint32, C.c_uint32]),
     "tsdf_set_metrics_log": (C.c_int, [P, C.c_char_p]),
     "tsdf_select_sector": (C.c_int, [FP, C.c_uint64, D3, C.c_double, C.c_uint32, C.c_uint32, FP,
                                      U64P]),

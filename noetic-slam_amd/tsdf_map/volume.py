@@ -367,6 +367,12 @@ class HipTSDFVolume(TSDFVolume):
     def set_profiling(self, on=True):
         self._check(self._lib.tsdf_set_profiling(self._ctx, 1 if on else 0), "set_profiling")
 
+    def set_profiling_period(self, every=_abi.KERNEL_KINDS, period=1):
+        """Time the kinds in `every` on every batch, the others on every period-th batch."""
+        mask = sum(1 << _abi.KERNEL_KINDS.index(k) for k in every)
+        self._check(self._lib.tsdf_set_profiling_period(self._ctx, mask, int(period)),
+                    "set_profiling_period")
+
     def set_metrics_log(self, path):
         """One JSON line per finished GPU batch appended to `path` (None: stop)."""
         self._check(self._lib.tsdf_set_metrics_log(

@@ -896,6 +896,11 @@ int tsdf_set_profiling(tsdf_ctx* c, int32_t on) {
     return c ? TSDF_OK : TSDF_EINVAL;
 }
 
+int tsdf_set_profiling_period(tsdf_ctx* c, uint32_t every_mask, uint32_t period) {
+    (void)every_mask;
+    return c && period ? TSDF_OK : TSDF_EINVAL;
+}
+
 int tsdf_set_metrics_log(tsdf_ctx* c, const char* path) {
     if (!c) return TSDF_EINVAL;
     return path ? set_err(c, TSDF_EINVAL, "the oracle writes no metrics log") : TSDF_OK;
