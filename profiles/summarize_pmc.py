@@ -40,8 +40,9 @@ def main(root):
     traffic = {"bytes_per_launch": {}, "fetch_bytes_raw": {}, "write_bytes": {},
                "note": "per dispatch means of rocprofv3 --pmc passes (profiles/collect_pmc.sh); "
                        "bytes_per_launch = 2 * FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE "
-                       "correction per MI355X_MICROARCH.md; uncalibrated for the 8-byte and "
-                       "gather accesses of these kernels, so an estimate)"}
+                       "correction per MI355X_MICROARCH.md, calibrated on this box's counters "
+                       "for 4/8/12/16-B contiguous reads (exact) and random 4-B gathers (128 B, "
+                       "one L2 line, per gather): profiles/r03/calib/calib.json)"}
     for kname, d in out.items():
         if "FETCH_SIZE" in d and "WRITE_SIZE" in d and not kname.startswith("k_fill"):
             f, w = d["FETCH_SIZE"] * 1024.0, d["WRITE_SIZE"] * 1024.0
