@@ -246,8 +246,12 @@ struct tsdf_ctx {
     // (tsdf_params.walk) and the band's walk fits nstep register slots per ray
     bool fused = false;
     int nstep = 0;
-    // batches of at most small_ns scans take k_integrate_small (TSDF_SMALL_NS; 0: never)
-    int small_ns = 8;
+    // batches of at most small_ns scans take k_integrate_small (TSDF_SMALL_NS; 0: never; measured
+    // break-even with k_integrate at 6-7 scans)
+    int small_ns = 6;
+    // batches of at most count_wide k_count blocks (fewer than the chip's CUs) run k_count with
+    // 1024-lane workgroups (TSDF_COUNT_WIDE; 0: never)
+    uint32_t count_wide = 256;
     // host-pointer path: pinned double buffer per scan; the pending batch's points are staged in
     // stage2[batch parity]
     float* h_stage[2] = {nullptr, nullptr};
@@ -415,7 +419,8 @@ static int launch(tsdf_ctx* c, const float* d_xyz, BatchDesc& D) {
         if (tm && c->fused) tm->begin(k_front, st);
         if (c->R.sec_on) HIPCHK(c, launch_sector_flags(d_xyz, B, c->R, W, c->G, par, st));
         if (c->fused) HIPCHK(c, launch_walk(d_xyz, B, c->R, T, W, c->G, par, c->nstep, st));
-        else HIPCHK(c, launch_count(d_xyz, B, c->R, T, W, c->G, par, st, kt(KIND_COUNT)));
+        else HIPCHK(c, launch_count(d_xyz, B, c->R, T, W, c->G, par, st, kt(KIND_COUNT),
+                                    !c->R.sec_on && D.n_blocks <= c->count_wide));
         if (tm && c->fused) tm->next(k_front, KIND_COMPACT, st);
         HIPCHK(c, launch_compact(B, T, W, c->G, par, c->fused, st, kt(KIND_COMPACT)));
 #if defined(TSDF_SEPARATE_ORDER) && !defined(TSDF_NO_ORDER)
@@ -1125,6 +1130,7 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
     }
     HIPCHK(c, hipMalloc(&c->G, sizeof(Globals)));
     if (const char* e = std::getenv("TSDF_SMALL_NS")) c->small_ns = std::max(0, std::min(8, std::atoi(e)));
+    if (const char* e = std::getenv("TSDF_COUNT_WIDE")) c->count_wide = (uint32_t)std::max(0, std::atoi(e));
     {
         // host staging threads: 3 workers + the caller (TSDF_PACK_THREADS overrides; 1 = none)
         int nt = 4;

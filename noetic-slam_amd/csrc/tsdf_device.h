@@ -272,9 +272,13 @@ struct KernelTimer {
 };
 
 hipError_t launch_count(const float* d_xyz, const BatchRef& D, const RayConst& R, const Table& T,
-                        const Work& Wk, Globals* G, int parity, hipStream_t st, const KTime& kt = {});
+                        const Work& Wk, Globals* G, int parity, hipStream_t st, const KTime& kt = {},
+                        bool wide = false);
 // table chunks of k_compact (Work::cagg holds two uint4 per chunk)
-constexpr uint32_t CMP_CHUNK = 1024;
+#ifndef TSDF_CMP_CHUNK
+#define TSDF_CMP_CHUNK 1024
+#endif
+constexpr uint32_t CMP_CHUNK = TSDF_CMP_CHUNK;
 inline uint64_t compact_chunks(uint64_t cap) { return (cap + CMP_CHUNK - 1) / CMP_CHUNK; }
 // Sector sharding (n_sectors > 1): which k_count blocks hold a ray of this GPU's sector; the walk
 // kernels' other workgroups leave after one load.

@@ -552,14 +552,22 @@ __global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchRef D, Table T, 
 //   accumulate scan t's samples (one contiguous segment) into dense per-voxel LDS cells
 //   (int64 fixed-point sum, count / weight sum) with LDS atomics, then every lane fuses its 8
 //   voxels' cells with the same arithmetic as k_integrate's chains and clears them.
-// No barrier (wave-private LDS), no k_order (the list is taken in table order), four bricks per
-// workgroup.  The field is bitwise k_integrate's (tests/test_gpu_parity.py small-batch cases).
+// No barrier (wave-private LDS), no size order (the list is taken in table order), four bricks per
+// workgroup.  Software-pipelined like k_integrate: while brick a is fused, brick a + G's cell row,
+// (S, W) and first SML_K x 64 samples (the record gives the segment, so they need not wait for the
+// cell row) are in flight to registers, and brick a + 2G's record is loading.
+// The field is bitwise k_integrate's (tests/test_gpu_parity.py::test_small_batch_kernel_bitwise).
 constexpr int SML_WAVES = 4;
+#ifndef TSDF_SML_K
+#define TSDF_SML_K 8
+#endif
+constexpr int SML_K = TSDF_SML_K;  // register-cached samples per lane
 template <int SEM>
 __global__ __launch_bounds__(SML_WAVES * 64) void k_integrate_small(BatchRef D, Table T, Work Wk,
                                                                    Pool Pl, Globals* G, int parity,
                                                                    RayConst R) {
     constexpr bool VB = SEM == 1 || SEM == 3;
+    constexpr int NW = SEM == 3 ? SML_K : 1;
     typedef typename std::conditional<VB, unsigned long long, uint32_t>::type CellB;
     __shared__ unsigned long long sA[SML_WAVES][BRICK_VOX];
     __shared__ CellB sB[SML_WAVES][BRICK_VOX];
@@ -576,44 +584,82 @@ __global__ __launch_bounds__(SML_WAVES * 64) void k_integrate_small(BatchRef D, 
         A[lane + 64 * k] = 0ull;
         Bc[lane + 64 * k] = 0;
     }
+    struct Regs {
+        uint32_t cell;     // lane t < ns: absolute position of the brick's scan-t samples
+        float s[8], w[8];  // voxels lane + 64 k
+        uint2 c[SML_K];    // samples lane + 64 j of the segment
+        float cw[NW];      // SEM 3: their weights
+    };
+    auto load = [&](const uint4& r, Regs& P) {
+        const uint32_t base = r.z, n = r.w;
+        const bool has = r.y < T.max_bricks;
+        P.cell = (uint32_t)lane < ns ? T.cell[(size_t)r.x * T.cell_stride + lane] : 0u;
+        const float* Sg = Pl.sdf + (size_t)(has ? r.y : 0) * BRICK_VOX;
+        const float* Wg = Pl.weight + (size_t)(has ? r.y : 0) * BRICK_VOX;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            P.s[k] = has ? Sg[lane + 64 * k] : R.bg;
+            P.w[k] = has ? Wg[lane + 64 * k] : 0.0f;
+        }
+#pragma unroll
+        for (int j = 0; j < SML_K; j++) {
+            const uint32_t i = lane + 64 * j;
+            const bool ok = i < n && base + i < Wk.max_smp;  // past max_smp: overflow (k_compact)
+            P.c[j] = ok ? Wk.smp[base + i] : make_uint2(0u, 0u);
+            if constexpr (SEM == 3) P.cw[j] = ok ? Wk.smw[base + i] : 0.0f;
+        }
+    };
+    auto add = [&](uint2 c, float wv_stored) {
+        const uint32_t l = c.y & 511u;
+        const float sv = __uint_as_float(c.x);
+        if constexpr (VB) {
+            float wv;
+            if constexpr (SEM == 3) wv = wv_stored;
+            else wv = vb_weight(R, 1.0f, sv);
+            atomicAdd(&A[l], (unsigned long long)(long long)((sv * wv) * 4294967296.0f));
+            atomicAdd(&Bc[l], (unsigned long long)(long long)(wv * 4294967296.0f));
+        } else {
+            (void)wv_stored;
+            atomicAdd(&A[l], (unsigned long long)(long long)(sv * 4294967296.0f));
+            atomicAdd(&Bc[l], 1u);
+        }
+    };
     uint32_t nvox = 0, ndirty = 0;
     const uint32_t stride = gridDim.x * SML_WAVES;
+    const uint4 zero4 = make_uint4(0u, 0u, 0u, 0u);
     uint32_t a = blockIdx.x * SML_WAVES + wid;
-    uint4 rec = a < n_active ? Wk.active[a] : make_uint4(0u, 0u, 0u, 0u);
+    uint4 rec = a < n_active ? Wk.active[a] : zero4;
+    uint4 rec_next = a + stride < n_active ? Wk.active[a + stride] : zero4;
+    Regs P;
+    if (a < n_active) load(rec, P);
     for (; a < n_active; a += stride) {
         const uint4 cur = rec;
-        if (a + stride < n_active) rec = Wk.active[a + stride];  // the next brick's record
+        const Regs B = P;
+        rec = rec_next;
+        if (a + stride < n_active) load(rec, P);                                  // brick a + G
+        if (a + 2 * stride < n_active) rec_next = Wk.active[a + 2 * stride];       // record of a + 2G
         const uint32_t h = cur.x, base = cur.z, n = cur.w;
         const bool has = cur.y < T.max_bricks;
         // lane t <= ns: start of scan t's samples relative to the segment (ns: the end)
-        const uint32_t cst = (uint32_t)lane < ns ? T.cell[(size_t)h * T.cell_stride + lane] - base : n;
-        const float* Sg = Pl.sdf + (size_t)(has ? cur.y : 0) * BRICK_VOX;
-        const float* Wg = Pl.weight + (size_t)(has ? cur.y : 0) * BRICK_VOX;
+        const uint32_t cst = (uint32_t)lane < ns ? B.cell - base : n;
         float s[8], w[8];
 #pragma unroll
         for (int k = 0; k < 8; k++) {
-            s[k] = has ? Sg[lane + 64 * k] : R.bg;
-            w[k] = has ? Wg[lane + 64 * k] : 0.0f;
+            s[k] = B.s[k];
+            w[k] = B.w[k];
         }
         uint32_t dirty = 0;
         for (uint32_t t = 0; t < ns; t++) {
             const uint32_t q0 = __shfl(cst, (int)t), q1 = __shfl(cst, (int)t + 1);
             if (q0 == q1) continue;  // uniform: no sample of scan t in this brick
-            for (uint32_t i = q0 + lane; i < q1; i += 64) {
-                if (base + i >= Wk.max_smp) continue;  // capacity overflow (reported by k_compact)
-                const uint2 c = Wk.smp[base + i];
-                const uint32_t l = c.y & 511u;
-                const float sv = __uint_as_float(c.x);
-                if constexpr (VB) {
-                    float wv;
-                    if constexpr (SEM == 3) wv = Wk.smw[base + i];
-                    else wv = vb_weight(R, 1.0f, sv);
-                    atomicAdd(&A[l], (unsigned long long)(long long)((sv * wv) * 4294967296.0f));
-                    atomicAdd(&Bc[l], (unsigned long long)(long long)(wv * 4294967296.0f));
-                } else {
-                    atomicAdd(&A[l], (unsigned long long)(long long)(sv * 4294967296.0f));
-                    atomicAdd(&Bc[l], 1u);
-                }
+#pragma unroll
+            for (int j = 0; j < SML_K; j++) {
+                const uint32_t i = lane + 64 * j;
+                if (i >= q0 && i < q1) add(B.c[j], B.cw[SEM == 3 ? j : 0]);
+            }
+            for (uint32_t i = max(q0, 64u * SML_K) + lane; i < q1; i += 64) {  // past the cache
+                if (base + i >= Wk.max_smp) continue;
+                add(Wk.smp[base + i], SEM == 3 ? Wk.smw[base + i] : 0.0f);
             }
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the cells complete
             __builtin_amdgcn_wave_barrier();

@@ -75,7 +75,9 @@ __device__ __forceinline__ int lds_insert(unsigned long long* s_key, uint64_t ke
 #endif
 constexpr int CNT_THREADS = TSDF_CNT_THREADS;
 
-template <int SEM>
+// NT: threads per workgroup (NT; 1024 for batches too small to fill the chip, one ray
+// per lane, so each SIMD holds four waves of one workgroup).
+template <int SEM, int NT = CNT_THREADS>
 // TSDF_SEM_VDBFUSION_F64: the fp32 filter's rare double branch would lift k_count to 93 VGPRs (5
 // waves per SIMD); the bound keeps the LDS-limited 6, spilling only inside that branch
 #ifndef TSDF_F64_COUNT_WAVES
@@ -84,14 +86,14 @@ template <int SEM>
 #ifndef TSDF_F64_PLACE_WAVES
 #define TSDF_F64_PLACE_WAVES 1
 #endif
-__global__ __launch_bounds__(CNT_THREADS, SEM == 2 ? TSDF_F64_COUNT_WAVES : 1) void k_count(const float* __restrict__ xyz, BatchRef D,
+__global__ __launch_bounds__(NT, SEM == 2 && NT == CNT_THREADS ? TSDF_F64_COUNT_WAVES : 1) void k_count(const float* __restrict__ xyz, BatchRef D,
                                                       RayConst R, Table T, Work Wk, Globals* G,
                                                       int parity) {
     __shared__ unsigned long long s_key[HCAP];
     __shared__ uint32_t s_cnt[HCAP];
-    __shared__ unsigned long long red[2][CNT_THREADS / 64];
-    __shared__ unsigned long long s_wsum[CNT_THREADS / 64];
-    __shared__ uint32_t s_wcnt[CNT_THREADS / 64];
+    __shared__ unsigned long long red[2][NT / 64];
+    __shared__ unsigned long long s_wsum[NT / 64];
+    __shared__ uint32_t s_wcnt[NT / 64];
 #ifndef TSDF_NO_PLAN
     __shared__ uint32_t s_bm[2][PLC_WORDS];  // per half: staging positions where a run starts
 #endif
@@ -107,12 +109,12 @@ __global__ __launch_bounds__(CNT_THREADS, SEM == 2 ? TSDF_F64_COUNT_WAVES : 1) v
     uint32_t t, r0, r1;
     block_range(D, bx, t, r0, r1);
     const float ox = D.s[t].ox, oy = D.s[t].oy, oz = D.s[t].oz;
-    for (int j = threadIdx.x; j < HCAP; j += CNT_THREADS) {
+    for (int j = threadIdx.x; j < HCAP; j += NT) {
         s_key[j] = EMPTY_KEY;
         s_cnt[j] = 0u;
     }
 #ifndef TSDF_NO_PLAN
-    for (int j = threadIdx.x; j < 2 * PLC_WORDS; j += CNT_THREADS) (&s_bm[0][0])[j] = 0u;
+    for (int j = threadIdx.x; j < 2 * PLC_WORDS; j += NT) (&s_bm[0][0])[j] = 0u;
 #endif
     __syncthreads();
     const uint32_t maxp = Wk.maxp;
@@ -142,7 +144,7 @@ __global__ __launch_bounds__(CNT_THREADS, SEM == 2 ? TSDF_F64_COUNT_WAVES : 1) v
         Wk.fb[f] = make_uint4(h, t, rk, 0u);
         return PAIR_FB | (cnt_in << PAIR_CNT_SHIFT) | f;
     };
-    for (uint32_t i = r0 + threadIdx.x; i < r1; i += CNT_THREADS) {
+    for (uint32_t i = r0 + threadIdx.x; i < r1; i += NT) {
         uint32_t* pc = Wk.pair + (size_t)i * maxp;
         uint32_t k = 0;
         typename Walk<SEM>::State r;
@@ -284,10 +286,10 @@ __global__ __launch_bounds__(CNT_THREADS, SEM == 2 ? TSDF_F64_COUNT_WAVES : 1) v
     // one global find-or-insert + one atomic per distinct brick of the workgroup: the cell
     // (brick, scan) count reserves the workgroup's ranks; `touched` (a plain store) lists the brick
     // for k_compact, which also derives the brick's total from its cells.  Each thread takes
-    // HCAP / CNT_THREADS consecutive slots; a block scan over their sample and run counts gives
+    // HCAP / NT consecutive slots; a block scan over their sample and run counts gives
     // every run its offset in the workgroup's sample order (k_place stages the samples in that
     // order) and its index in the workgroup's DENSE run list (slot order = sample order).
-    constexpr int SPT = HCAP / CNT_THREADS;
+    constexpr int SPT = HCAP / NT;
     // two dense run lists per workgroup, one per half (k_place workgroup 2 b + half)
     uint4* bt0 = Wk.blk + (size_t)bx * 2 * HCAP;
     uint4* bt1 = bt0 + HCAP;
@@ -311,7 +313,7 @@ __global__ __launch_bounds__(CNT_THREADS, SEM == 2 ? TSDF_F64_COUNT_WAVES : 1) v
         __syncthreads();
         unsigned long long ex = 0;
         uint32_t exc = 0, totc = 0;
-        for (int w = 0; w < CNT_THREADS / 64; w++) {
+        for (int w = 0; w < NT / 64; w++) {
             ex += w < wid ? s_wsum[w] : 0ull;
             exc += w < wid ? s_wcnt[w] : 0u;
             totc += s_wcnt[w];
@@ -320,13 +322,13 @@ __global__ __launch_bounds__(CNT_THREADS, SEM == 2 ? TSDF_F64_COUNT_WAVES : 1) v
         off1 = (uint32_t)(ex >> 32) + (i1 - n1s);
         idx0 = (exc & 0xFFFFu) + ((ic - c01) & 0xFFFFu);
         idx1 = (exc >> 16) + ((ic - c01) >> 16);
-        if (threadIdx.x == CNT_THREADS - 1) {
+        if (threadIdx.x == NT - 1) {
             Wk.blk_n[2 * bx] = totc & 0xFFFFu;
             Wk.blk_n[2 * bx + 1] = totc >> 16;
 #ifndef TSDF_NO_PLAN
             // each half's staged sample count: its samples, up to the staging capacity
             unsigned long long tot = 0;
-            for (int w = 0; w < CNT_THREADS / 64; w++) tot += s_wsum[w];
+            for (int w = 0; w < NT / 64; w++) tot += s_wsum[w];
             Wk.plan[(size_t)(2 * bx) * PLAN_STRIDE + PLAN_STRIDE - 1] =
                 min((uint32_t)tot, (uint32_t)PLC_STAGE);
             Wk.plan[(size_t)(2 * bx + 1) * PLAN_STRIDE + PLAN_STRIDE - 1] =
@@ -424,7 +426,7 @@ __global__ __launch_bounds__(CNT_THREADS, SEM == 2 ? TSDF_F64_COUNT_WAVES : 1) v
     if (threadIdx.x == 0) {
         v = 0;
         q = 0;
-        for (int w = 0; w < CNT_THREADS / 64; w++) { v += red[0][w]; q += red[1][w]; }
+        for (int w = 0; w < NT / 64; w++) { v += red[0][w]; q += red[1][w]; }
         if (v) atomicAdd(&C->n_rays[blockIdx.x & 7], v);  // -> G->tot_rays at k_finish
         if (q) atomicAdd(&C->n_pairs[blockIdx.x & 7], q);
     }
@@ -617,15 +619,33 @@ __global__ __launch_bounds__(CMP_SCAN_THREADS) void k_compact_scan(uint32_t nch,
         s_carry[2] = G->pool_count;
     }
     __syncthreads();
+    // the three prefixes (touched bricks, samples, new bricks) in one pass: per-wave DPP scans,
+    // the waves' totals through LDS (two barriers per 1024 chunks)
+    constexpr int NWS = CMP_SCAN_THREADS / 64;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     for (uint32_t b0 = 0; b0 < nch; b0 += CMP_SCAN_THREADS) {
         const uint32_t i = b0 + threadIdx.x;
         const uint4 a = i < nch ? Wk.cagg[i] : make_uint4(0u, 0u, 0u, 0u);
-        uint32_t ta, tc, tn;
-        const uint32_t ea = block_excl_scan<CMP_SCAN_THREADS>(a.x, s_w[0], &ta);
-        const uint32_t ec = block_excl_scan<CMP_SCAN_THREADS>(a.y, s_w[1], &tc);
-        const uint32_t en = block_excl_scan<CMP_SCAN_THREADS>(a.z, s_w[2], &tn);
-        if (i < nch) Wk.cagg[nch + i] = make_uint4(s_carry[0] + ea, s_carry[1] + ec, s_carry[2] + en, 0u);
+        const uint32_t ia = wave_incl_scan(a.x), ic = wave_incl_scan(a.y), in = wave_incl_scan(a.z);
+        if (lane == 63) {
+            s_w[0][wid] = ia;
+            s_w[1][wid] = ic;
+            s_w[2][wid] = in;
+        }
         __syncthreads();
+        uint32_t oa = s_carry[0], oc = s_carry[1], on = s_carry[2], ta = 0, tc = 0, tn = 0;
+#pragma unroll
+        for (int k = 0; k < NWS; k++) {
+            const uint32_t xa = s_w[0][k], xc = s_w[1][k], xn = s_w[2][k];
+            oa += k < wid ? xa : 0u;
+            oc += k < wid ? xc : 0u;
+            on += k < wid ? xn : 0u;
+            ta += xa;
+            tc += xc;
+            tn += xn;
+        }
+        if (i < nch) Wk.cagg[nch + i] = make_uint4(oa + ia - a.x, oc + ic - a.y, on + in - a.z, 0u);
+        __syncthreads();  // every thread read s_w and s_carry
         if (threadIdx.x == 0) {
             s_carry[0] += ta;
             s_carry[1] += tc;
@@ -635,30 +655,34 @@ __global__ __launch_bounds__(CMP_SCAN_THREADS) void k_compact_scan(uint32_t nch,
     }
 #ifndef TSDF_SEPARATE_ORDER
     // size order: (slice, class) first positions = the records of larger classes + class k's
-    // records in the slices before (k_order_scan's rule); the histogram is zeroed for the next batch
+    // records in the slices before (k_order_scan's rule); the histogram is zeroed for the next
+    // batch.  Wave w takes classes w and w + 16 with lane = slice (ORD_BLOCKS = 64): one DPP scan
+    // per class gives the slices' prefix, wave 0 the classes' bases.
+    static_assert(ORD_BLOCKS == 64 && ORD_CLASSES == 32 && CMP_SCAN_THREADS == 1024, "layout");
     {
         __shared__ uint32_t s_tot[ORD_CLASSES], s_cbase[ORD_CLASSES];
-        const int t = threadIdx.x;
-        if (t < ORD_CLASSES) {
-            uint32_t sum = 0;
-            for (int b = 0; b < ORD_BLOCKS; b++) sum += Wk.ord_hist[b * ORD_CLASSES + t];
-            s_tot[t] = sum;
+        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+        uint32_t v[2], ex[2];
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            const int cls = w + 16 * q;
+            v[q] = Wk.ord_hist[lane * ORD_CLASSES + cls];
+            const uint32_t incl = wave_incl_scan(v[q]);
+            ex[q] = incl - v[q];
+            if (lane == 63) s_tot[cls] = incl;
+            Wk.ord_hist[lane * ORD_CLASSES + cls] = 0u;
         }
         __syncthreads();
-        if (t < 64) {
-            const uint32_t v = t < ORD_CLASSES ? s_tot[t] : 0u;
-            const uint32_t incl = wave_incl_scan(v);
-            if (t < ORD_CLASSES) s_cbase[t] = incl - v;
+        if (w == 0) {
+            const uint32_t t = lane < ORD_CLASSES ? s_tot[lane] : 0u;
+            const uint32_t incl = wave_incl_scan(t);
+            if (lane < ORD_CLASSES) s_cbase[lane] = incl - t;
         }
         __syncthreads();
-        if (t < ORD_CLASSES) {
-            uint32_t run = s_cbase[t];
-            for (int b = 0; b < ORD_BLOCKS; b++) {
-                const uint32_t v = Wk.ord_hist[b * ORD_CLASSES + t];
-                Wk.ord_hist[ORD_BLOCKS * ORD_CLASSES + b * ORD_CLASSES + t] = run;
-                Wk.ord_hist[b * ORD_CLASSES + t] = 0u;
-                run += v;
-            }
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            const int cls = w + 16 * q;
+            Wk.ord_hist[ORD_BLOCKS * ORD_CLASSES + lane * ORD_CLASSES + cls] = s_cbase[cls] + ex[q];
         }
     }
 #endif
@@ -1191,10 +1215,16 @@ static int grid_for(uint64_t items, int per_block, int cap) {
 // One batch is k_count -> k_compact -> k_place -> k_integrate -> k_finish on one stream; the host
 // (tsdf_capi.cpp) interleaves the cross-batch waits between them.
 hipError_t launch_count(const float* d_xyz, const BatchRef& D, const RayConst& R, const Table& T,
-                        const Work& Wk, Globals* G, int parity, hipStream_t st, const KTime& kt) {
+                        const Work& Wk, Globals* G, int parity, hipStream_t st, const KTime& kt,
+                        bool wide) {
     // sem 3 (Voxblox 1/z^2) counts with Walk<1>: the weight only matters where it is stored
-    auto k = R.sem == 1 || R.sem == 3 ? k_count<1> : R.sem == 2 ? k_count<2> : k_count<0>;
-    tlaunch(k, D.n_blocks, CNT_THREADS, st, kt.start, kt.stop, d_xyz, D, R, T, Wk, G, parity);
+    if (wide) {  // a batch too small to fill the chip: 1024-lane workgroups
+        auto k = R.sem == 1 || R.sem == 3 ? k_count<1, 1024> : R.sem == 2 ? k_count<2, 1024> : k_count<0, 1024>;
+        tlaunch(k, D.n_blocks, 1024, st, kt.start, kt.stop, d_xyz, D, R, T, Wk, G, parity);
+    } else {
+        auto k = R.sem == 1 || R.sem == 3 ? k_count<1> : R.sem == 2 ? k_count<2> : k_count<0>;
+        tlaunch(k, D.n_blocks, CNT_THREADS, st, kt.start, kt.stop, d_xyz, D, R, T, Wk, G, parity);
+    }
     return hipGetLastError();
 }
 

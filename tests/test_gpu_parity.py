@@ -109,8 +109,10 @@ def test_batch_composition_is_invisible(sim):
 @pytest.mark.parametrize("semantics", ["vdbfusion", "vdbfusion_f64", "voxblox", "voxblox_z2"])
 def test_small_batch_kernel_bitwise(sim, monkeypatch, semantics):
     """Batches of <= 8 scans fuse in k_integrate_small (one wave per brick, dense LDS cells, no
-    k_order); TSDF_SMALL_NS=0 forces k_integrate.  Both equal the oracle bit for bit at 1, 3 and 8
-    scans per batch, on a full scan (long per-voxel runs of one scan) and with carving."""
+    size order) and, below 256 blocks, count in 1024-lane k_count workgroups; TSDF_SMALL_NS=0 and
+    TSDF_COUNT_WIDE=0 force k_integrate and the 256-lane k_count.  Both equal the oracle bit for bit
+    at 1, 3 and 8 scans per batch, on a full scan (long per-voxel runs of one scan) and with
+    carving."""
     from tsdf_map import bricks_to_voxels
     kw = dict(semantics="voxblox", use_const_weight=False) if semantics == "voxblox_z2" else \
         dict(semantics=semantics)
@@ -125,6 +127,7 @@ def test_small_batch_kernel_bitwise(sim, monkeypatch, semantics):
             got = {}
             for small in ("8", "0") if mb != 3 else ("8",):
                 monkeypatch.setenv("TSDF_SMALL_NS", small)
+                monkeypatch.setenv("TSDF_COUNT_WIDE", "256" if small != "0" else "0")
                 g = hip(max_batch=mb, **kw, **extra)
                 for p, org in scans:
                     g.integrate(p, org)
