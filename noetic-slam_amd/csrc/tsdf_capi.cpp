@@ -17,6 +17,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <numeric>
+#include <chrono>
 #include <condition_variable>
 #include <functional>
 #include <mutex>
@@ -33,6 +34,27 @@ static_assert(TSDF_MAX_BATCH == MAX_BATCH, "header and device batch limits diffe
 static_assert(TSDF_TILE_WORDS == TILE_WORDS && TSDF_MAX_WORLD == MAX_WORLD, "border tile layout differs");
 
 namespace {
+
+// Diagnostic host timing of launch() sections (TSDF_HOST_TIMING=1: averages printed at destroy).
+struct HostTiming {
+    bool on = std::getenv("TSDF_HOST_TIMING") != nullptr;
+    double acc[12] = {};
+    uint64_t n = 0;
+    std::chrono::steady_clock::time_point t;
+    void start() { if (on) t = std::chrono::steady_clock::now(); }
+    void lap(int k) {
+        if (!on) return;
+        const auto u = std::chrono::steady_clock::now();
+        acc[k] += std::chrono::duration<double, std::micro>(u - t).count();
+        t = u;
+    }
+    ~HostTiming() {
+        if (!on || !n) return;
+        std::fprintf(stderr, "host launch timing (us/batch over %llu):", (unsigned long long)n);
+        for (int k = 0; k < 12; k++) std::fprintf(stderr, " %d:%.2f", k, acc[k] / n);
+        std::fprintf(stderr, "\n");
+    }
+};
 
 struct EventTimer final : KernelTimer {
     struct Rec { int kind; uint64_t batch; hipEvent_t a, b; bool own_a; };
@@ -247,11 +269,11 @@ struct tsdf_ctx {
     bool fused = false;
     int nstep = 0;
     // batches of at most small_ns scans take k_integrate_small (TSDF_SMALL_NS; 0: never; measured
-    // break-even with k_integrate at 6-7 scans)
-    int small_ns = 6;
-    // batches of at most count_wide k_count blocks (fewer than the chip's CUs) run k_count with
-    // 1024-lane workgroups (TSDF_COUNT_WIDE; 0: never)
-    uint32_t count_wide = 256;
+    // break-even with k_integrate at 6 scans)
+    int small_ns = 5;
+    // batches of at most count_wide k_count blocks (about 4 full scans: too few workgroups of 256
+    // lanes to fill the chip) run k_count with 1024-lane workgroups (TSDF_COUNT_WIDE; 0: never)
+    uint32_t count_wide = 512;
     // host-pointer path: pinned double buffer per scan; the pending batch's points are staged in
     // stage2[batch parity]
     float* h_stage[2] = {nullptr, nullptr};
@@ -266,7 +288,10 @@ struct tsdf_ctx {
     uint32_t* cell2[2] = {nullptr, nullptr};  // u64 cells with the single walk
     float* stage2[2] = {nullptr, nullptr};
     hipEvent_t ev_main = nullptr;
-    hipEvent_t ev_compact[2] = {nullptr, nullptr}, ev_integ[2] = {nullptr, nullptr};
+    hipEvent_t ev_compact[2] = {nullptr, nullptr};
+    // the end of the last batch of each parity: the ring event of that batch's slot (one marker
+    // per batch; every marker in the stream costs the GPU a few microseconds)
+    hipEvent_t ev_integ[2] = {nullptr, nullptr};
     BatchDesc pend{};  // pending host scans (points in stage2[pend_stage])
     // Device staging ownership (independent of batch parity, which replays can shift): the pending
     // batch's buffer, and per buffer the last batch that read it (its id and completion event).
@@ -277,8 +302,13 @@ struct tsdf_ctx {
     // batch records for the kernels: a pinned host ring and its device twin (launch() copies a
     // batch's n_scans + 1 records into the next slot on the batch's stream)
     static constexpr int RING = 16;
+    HostTiming ht;
     ScanRec* h_ring = nullptr;
     ScanRec* d_ring = nullptr;
+    const ScanRec* d_ring_src = nullptr;  // h_ring as the device addresses it (k_upload)
+    // ring progress: k_upload of launch q stores q + 1 here once it has read its slot
+    unsigned long long* h_ring_done = nullptr;
+    unsigned long long* d_ring_done = nullptr;
     hipEvent_t ring_ev[RING] = {};
     uint64_t ring_next = 0;
     uint64_t batch_id = 0;
@@ -356,8 +386,33 @@ static int check_and_replay(tsdf_ctx* c);
 static int drain_all(tsdf_ctx* c);
 static int emit_metrics(tsdf_ctx* c);
 
+// Before launch seq rewrites its host ring slot: launch seq - RING (the slot's previous user) must
+// have read it (its k_upload raised the progress word to seq - RING + 1).  Waits like an event
+// synchronize (spin, then yield), and checks the batch streams for errors while it waits.
+static int ring_wait(tsdf_ctx* c, uint64_t seq) {
+    if (seq < (uint64_t)tsdf_ctx::RING) return TSDF_OK;
+    const unsigned long long need = seq - tsdf_ctx::RING + 1;
+    for (uint64_t i = 0;; i++) {
+        if (__atomic_load_n(c->h_ring_done, __ATOMIC_ACQUIRE) >= need) return TSDF_OK;
+        if (i < 64) continue;
+        std::this_thread::yield();
+        if ((i & 1023) == 0) {
+            bool idle = true;
+            for (int q = 0; q < 2; q++) {
+                const hipError_t e = hipStreamQuery(c->bst[q]);
+                if (e == hipErrorNotReady) idle = false;
+                else if (e != hipSuccess) HIPCHK(c, e);
+            }
+            if (idle && __atomic_load_n(c->h_ring_done, __ATOMIC_ACQUIRE) < need)
+                return fail(c, TSDF_EHIP, "scan-record ring: upload %llu never completed",
+                            (unsigned long long)(need - 1));
+        }
+    }
+}
+
 static int launch(tsdf_ctx* c, const float* d_xyz, BatchDesc& D) {
     if (D.n_scans == 0) return TSDF_OK;
+    c->ht.start();
     if (c->metrics && !c->in_replay && c->batch_id - c->metrics_next >= METRIC_RING - 8) {
         int rc = drain_all(c);  // the device ring of batch records would wrap
         if (!rc) rc = check_and_replay(c);
@@ -377,6 +432,7 @@ static int launch(tsdf_ctx* c, const float* d_xyz, BatchDesc& D) {
     if (D.n_blocks > c->max_blocks)
         return fail(c, TSDF_EINVAL, "batch needs %u workgroups > %u", D.n_blocks, c->max_blocks);
     const int par = (int)(c->batch_id & 1);
+    c->ht.lap(0);
 #ifndef TSDF_TWO_STREAM_SERIAL
     // serial batches share one stream (stream order replaces the cross-stream waits); pipelined
     // batches alternate between two
@@ -399,14 +455,29 @@ static int launch(tsdf_ctx* c, const float* d_xyz, BatchDesc& D) {
     if (c->batch_id > 0 && cross)  // pipelined: after the previous batch's compact; else after all of it
         HIPCHK(c, hipStreamWaitEvent(st, c->p.pipeline ? c->ev_compact[par ^ 1]
                                                        : c->ev_integ[par ^ 1], 0));
+    c->ht.lap(1);
     // the batch's scan records -> the device (a ring slot; the host slot is reused once its copy ran)
-    const int slot = (int)(c->ring_next++ % tsdf_ctx::RING);
-    HIPCHK(c, hipEventSynchronize(c->ring_ev[slot]));
+    const uint64_t seq = c->ring_next++;
+    const int slot = (int)(seq % tsdf_ctx::RING);
+    {
+        int rc = ring_wait(c, seq);
+        if (rc) return rc;
+    }
+    c->ht.lap(8);
     ScanRec* hs = c->h_ring + (size_t)slot * (MAX_BATCH + 1);
     ScanRec* ds = c->d_ring + (size_t)slot * (MAX_BATCH + 1);
     std::memcpy(hs, D.s, (D.n_scans + 1) * sizeof(ScanRec));
+    c->ht.lap(9);
+#ifdef TSDF_RING_MEMCPY
     HIPCHK(c, hipMemcpyAsync(ds, hs, (D.n_scans + 1) * sizeof(ScanRec), hipMemcpyHostToDevice, st));
-    HIPCHK(c, hipEventRecord(c->ring_ev[slot], st));
+#error "TSDF_RING_MEMCPY: the ring progress word is written by k_upload"
+#else
+    HIPCHK(c, launch_upload(c->d_ring_src + (size_t)slot * (MAX_BATCH + 1), ds,
+                            (uint32_t)((D.n_scans + 1) * sizeof(ScanRec)), c->d_ring_done, seq + 1,
+                            st));
+#endif
+    c->ht.lap(10);
+    c->ht.lap(2);
     const BatchRef B{D.n_scans, D.n_blocks, ds};
     // a small batch (a live node's 1-8 scans) fuses wave-per-brick, in table order (no k_order)
     const bool small = !c->fused && D.n_scans <= (uint32_t)c->small_ns;
@@ -421,8 +492,10 @@ static int launch(tsdf_ctx* c, const float* d_xyz, BatchDesc& D) {
         if (c->fused) HIPCHK(c, launch_walk(d_xyz, B, c->R, T, W, c->G, par, c->nstep, st));
         else HIPCHK(c, launch_count(d_xyz, B, c->R, T, W, c->G, par, st, kt(KIND_COUNT),
                                     !c->R.sec_on && D.n_blocks <= c->count_wide));
+        c->ht.lap(3);
         if (tm && c->fused) tm->next(k_front, KIND_COMPACT, st);
         HIPCHK(c, launch_compact(B, T, W, c->G, par, c->fused, st, kt(KIND_COMPACT)));
+        c->ht.lap(4);
 #if defined(TSDF_SEPARATE_ORDER) && !defined(TSDF_NO_ORDER)
         if (!small) HIPCHK(c, launch_order(W, c->G, par, st));
 #endif
@@ -432,6 +505,7 @@ static int launch(tsdf_ctx* c, const float* d_xyz, BatchDesc& D) {
         if (tm && c->fused) tm->next(KIND_COMPACT, k_back, st);
         if (c->fused) HIPCHK(c, launch_spans(B, c->R, T, W, c->G, par, c->nstep, st));
         else HIPCHK(c, launch_place(d_xyz, B, c->R, T, W, c->G, par, st, kt(KIND_PLACE)));
+        c->ht.lap(5);
         if (tm && c->fused) tm->end(k_back, st);
     }
     if (c->batch_id > 0 && cross) HIPCHK(c, hipStreamWaitEvent(st, c->ev_integ[par ^ 1], 0));
@@ -450,15 +524,21 @@ static int launch(tsdf_ctx* c, const float* d_xyz, BatchDesc& D) {
                                        kt(KIND_INTEGRATE)));
         }
         if (tm && c->fused) tm->end(KIND_INTEGRATE, st);
+        c->ht.lap(6);
     }
     HIPCHK(c, launch_finish(c->G, par, (uint32_t)c->batch_id, st));
-    HIPCHK(c, hipEventRecord(c->ev_integ[par], st));
+    if (cross) {  // pipelined: the other stream's next batches wait on this batch's end
+        HIPCHK(c, hipEventRecord(c->ring_ev[slot], st));
+        c->ev_integ[par] = c->ring_ev[slot];
+    }
     if (c->can_grow) c->log.push_back({c->batch_id, d_xyz, D});
     for (int k = 0; k < 2; k++)  // a host batch: its staging buffer's last reader
         if (d_xyz == c->stage2[k]) {
             c->stage_reader[k] = c->batch_id;
             HIPCHK(c, hipEventRecord(c->stage_ev[k], st));
         }
+    c->ht.lap(7);
+    c->ht.n++;
     c->batch_id++;
     c->n_batches++;
     c->n_scans += D.n_scans;
@@ -472,6 +552,14 @@ static int launch(tsdf_ctx* c, const float* d_xyz, BatchDesc& D) {
 
 // The context stream waits for every launched batch (read-outs, imports, sync).
 static int join(tsdf_ctx* c) {
+    if (c->batch_id == 0) return TSDF_OK;
+#ifndef TSDF_TWO_STREAM_SERIAL
+    if (!c->p.pipeline) {  // serial batches: one stream, no per-batch marker; one now
+        HIPCHK(c, hipEventRecord(c->ev_main, c->bst[0]));
+        HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_main, 0));
+        return TSDF_OK;
+    }
+#endif
     for (int q = 0; q < 2; q++)
         if (c->batch_id > (uint64_t)q) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_integ[q], 0));
     return TSDF_OK;
@@ -985,13 +1073,13 @@ void tsdf_destroy(tsdf_ctx* c) {
     for (int q = 0; q < 2; q++) {
         if (c->bst[q]) (void)hipStreamDestroy(c->bst[q]);
         if (c->ev_compact[q]) (void)hipEventDestroy(c->ev_compact[q]);
-        if (c->ev_integ[q]) (void)hipEventDestroy(c->ev_integ[q]);
         if (c->stage_ev[q]) (void)hipEventDestroy(c->stage_ev[q]);
     }
     if (c->ev_main) (void)hipEventDestroy(c->ev_main);
     for (int k = 0; k < tsdf_ctx::RING; k++)
         if (c->ring_ev[k]) (void)hipEventDestroy(c->ring_ev[k]);
     if (c->h_ring) (void)hipHostFree(c->h_ring);
+    if (c->h_ring_done) (void)hipHostFree(c->h_ring_done);
     if (c->d_ring) (void)hipFree(c->d_ring);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -1010,7 +1098,6 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
     for (int q = 0; q < 2; q++) {
         HIPCHK(c, hipStreamCreateWithFlags(&c->bst[q], hipStreamNonBlocking));
         HIPCHK(c, hipEventCreateWithFlags(&c->ev_compact[q], hipEventDisableTiming));
-        HIPCHK(c, hipEventCreateWithFlags(&c->ev_integ[q], hipEventDisableTiming));
         HIPCHK(c, hipEventCreateWithFlags(&c->stage_ev[q], hipEventDisableTiming));
     }
     HIPCHK(c, hipEventCreateWithFlags(&c->ev_main, hipEventDisableTiming));
@@ -1147,6 +1234,15 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
     HIPCHK(c, hipHostMalloc(&c->h_ring, tsdf_ctx::RING * (MAX_BATCH + 1) * sizeof(ScanRec),
                             hipHostMallocDefault));
     HIPCHK(c, hipMalloc(&c->d_ring, tsdf_ctx::RING * (MAX_BATCH + 1) * sizeof(ScanRec)));
+    {
+        void* dp = nullptr;
+        HIPCHK(c, hipHostGetDevicePointer(&dp, c->h_ring, 0));
+        c->d_ring_src = static_cast<const ScanRec*>(dp);
+        HIPCHK(c, hipHostMalloc(&c->h_ring_done, 64, hipHostMallocDefault));
+        *c->h_ring_done = 0;
+        HIPCHK(c, hipHostGetDevicePointer(&dp, c->h_ring_done, 0));
+        c->d_ring_done = static_cast<unsigned long long*>(dp);
+    }
     for (int k = 0; k < tsdf_ctx::RING; k++)
         HIPCHK(c, hipEventCreateWithFlags(&c->ring_ev[k], hipEventDisableTiming));
     HIPCHK(c, hipMemsetAsync(c->G, 0, sizeof(Globals), c->stream));

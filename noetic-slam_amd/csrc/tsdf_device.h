@@ -296,6 +296,10 @@ hipError_t launch_spans(const BatchRef& D, const RayConst& R, const Table& T, co
 hipError_t launch_place(const float* d_xyz, const BatchRef& D, const RayConst& R, const Table& T,
                         const Work& Wk, Globals* G, int parity, hipStream_t st, const KTime& kt = {});
 hipError_t launch_finish(Globals* G, int parity, uint32_t batch_id, hipStream_t st);
+// bytes (a multiple of 16) from device-accessible pinned host memory to device memory, then
+// *done = seq (done: device address of a pinned host word)
+hipError_t launch_upload(const void* host_src, void* dst, uint32_t bytes,
+                         unsigned long long* done, unsigned long long seq, hipStream_t st);
 // capacity growth: re-insert pool slots [0, n) of the new table from brick_keys
 hipError_t launch_rehash(const Table& T, uint32_t n, Globals* G, hipStream_t st);
 // Orders the batch's active bricks by size class, largest first (k_integrate's load balance).

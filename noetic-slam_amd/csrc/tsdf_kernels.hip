@@ -619,40 +619,55 @@ __global__ __launch_bounds__(CMP_SCAN_THREADS) void k_compact_scan(uint32_t nch,
         s_carry[2] = G->pool_count;
     }
     __syncthreads();
-    // the three prefixes (touched bricks, samples, new bricks) in one pass: per-wave DPP scans,
-    // the waves' totals through LDS (two barriers per 1024 chunks)
+    // the three prefixes (touched bricks, samples, new bricks) in one pass: thread t takes the
+    // chunks [t P, t P + P) (all loads issued at once), per-wave DPP scans of the threads' totals,
+    // the waves' totals through LDS
     constexpr int NWS = CMP_SCAN_THREADS / 64;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    for (uint32_t b0 = 0; b0 < nch; b0 += CMP_SCAN_THREADS) {
-        const uint32_t i = b0 + threadIdx.x;
-        const uint4 a = i < nch ? Wk.cagg[i] : make_uint4(0u, 0u, 0u, 0u);
-        const uint32_t ia = wave_incl_scan(a.x), ic = wave_incl_scan(a.y), in = wave_incl_scan(a.z);
-        if (lane == 63) {
-            s_w[0][wid] = ia;
-            s_w[1][wid] = ic;
-            s_w[2][wid] = in;
-        }
-        __syncthreads();
-        uint32_t oa = s_carry[0], oc = s_carry[1], on = s_carry[2], ta = 0, tc = 0, tn = 0;
-#pragma unroll
-        for (int k = 0; k < NWS; k++) {
-            const uint32_t xa = s_w[0][k], xc = s_w[1][k], xn = s_w[2][k];
-            oa += k < wid ? xa : 0u;
-            oc += k < wid ? xc : 0u;
-            on += k < wid ? xn : 0u;
-            ta += xa;
-            tc += xc;
-            tn += xn;
-        }
-        if (i < nch) Wk.cagg[nch + i] = make_uint4(oa + ia - a.x, oc + ic - a.y, on + in - a.z, 0u);
-        __syncthreads();  // every thread read s_w and s_carry
-        if (threadIdx.x == 0) {
-            s_carry[0] += ta;
-            s_carry[1] += tc;
-            s_carry[2] += tn;
-        }
-        __syncthreads();
+    const uint32_t P = (nch + CMP_SCAN_THREADS - 1) / CMP_SCAN_THREADS;
+    const uint32_t c0 = threadIdx.x * P;
+    uint32_t sa = 0, sc = 0, sn = 0;
+#pragma unroll 4
+    for (uint32_t q = 0; q < P; q++) {
+        const uint4 a = c0 + q < nch ? Wk.cagg[c0 + q] : make_uint4(0u, 0u, 0u, 0u);
+        sa += a.x;
+        sc += a.y;
+        sn += a.z;
     }
+    const uint32_t ia = wave_incl_scan(sa), ic = wave_incl_scan(sc), in = wave_incl_scan(sn);
+    if (lane == 63) {
+        s_w[0][wid] = ia;
+        s_w[1][wid] = ic;
+        s_w[2][wid] = in;
+    }
+    __syncthreads();
+    uint32_t oa = s_carry[0], oc = s_carry[1], on = s_carry[2], ta = 0, tc = 0, tn = 0;
+#pragma unroll
+    for (int k = 0; k < NWS; k++) {
+        const uint32_t xa = s_w[0][k], xc = s_w[1][k], xn = s_w[2][k];
+        oa += k < wid ? xa : 0u;
+        oc += k < wid ? xc : 0u;
+        on += k < wid ? xn : 0u;
+        ta += xa;
+        tc += xc;
+        tn += xn;
+    }
+    oa += ia - sa;
+    oc += ic - sc;
+    on += in - sn;
+    for (uint32_t q = 0; q < P && c0 + q < nch; q++) {  // re-read: L2-resident, and no registers held
+        const uint4 a = Wk.cagg[c0 + q];
+        Wk.cagg[nch + c0 + q] = make_uint4(oa, oc, on, 0u);
+        oa += a.x;
+        oc += a.y;
+        on += a.z;
+    }
+    if (threadIdx.x == 0) {
+        s_carry[0] += ta;
+        s_carry[1] += tc;
+        s_carry[2] += tn;
+    }
+    __syncthreads();
 #ifndef TSDF_SEPARATE_ORDER
     // size order: (slice, class) first positions = the records of larger classes + class k's
     // records in the slices before (k_order_scan's rule); the histogram is zeroed for the next
@@ -1366,6 +1381,26 @@ __global__ void k_finish(Globals* G, int parity, uint32_t batch_id) {
         dst[j] = src[j];
         src[j] = 0u;
     }
+}
+
+// A batch's scan records from the pinned host ring to the device ring: one small kernel reads them
+// over PCIe (zero-copy) instead of a copy command, then tells the host the ring slot is free by
+// storing the launch's sequence number to a pinned host word (a vector store at system scope).
+// The host waits on that word to reuse a slot, so a serial batch needs no event marker in the
+// stream: each marker left the GPU idle ~5 us (profiles/gap_trace.py).
+__global__ void k_upload(const uint4* __restrict__ src, uint4* __restrict__ dst, uint32_t n,
+                         unsigned long long* done, unsigned long long seq) {
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
+    __syncthreads();  // every read of the host slot is complete
+    if (threadIdx.x == 0)
+        __hip_atomic_fetch_max(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+hipError_t launch_upload(const void* host_src, void* dst, uint32_t bytes,
+                         unsigned long long* done, unsigned long long seq, hipStream_t st) {
+    k_upload<<<1, 256, 0, st>>>(static_cast<const uint4*>(host_src), static_cast<uint4*>(dst),
+                                bytes / 16, done, seq);
+    return hipGetLastError();
 }
 
 hipError_t launch_finish(Globals* G, int parity, uint32_t batch_id, hipStream_t st) {
