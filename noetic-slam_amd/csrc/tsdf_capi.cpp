@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <cmath>
 #include <cstdarg>
 #include <cstddef>
@@ -149,27 +150,46 @@ struct PackPool {
     std::vector<std::thread> th;
     std::mutex m;
     std::condition_variable go, done;
-    std::function<void(int)> job;
-    uint64_t gen = 0;
-    int busy = 0;
-    bool stop = false;
+    std::function<void(int)> job;  // stable while busy > 0
+    std::atomic<uint64_t> gen{0};
+    std::atomic<int> busy{0};
+    std::atomic<bool> stop{false};
+    // a worker (and a waiting caller) spins this long before sleeping: scans arrive back to back,
+    // and waking a sleeping thread costs tens of microseconds on a busy host
+    static constexpr double SPIN_US = 100.0;
+
+    static bool spin_until(const std::function<bool()>& ready) {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int i = 0;; i++) {
+            if (ready()) return true;
+            if ((i & 63) == 63 &&
+                std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0)
+                        .count() > SPIN_US)
+                return false;
+#if defined(__x86_64__)
+            __builtin_ia32_pause();
+#endif
+        }
+    }
 
     explicit PackPool(int workers) {
         for (int w = 0; w < workers; w++)
             th.emplace_back([this, w] {
                 uint64_t seen = 0;
                 for (;;) {
-                    std::function<void(int)> f;
-                    {
+                    auto fresh = [&] { return stop.load(std::memory_order_acquire) ||
+                                              gen.load(std::memory_order_acquire) != seen; };
+                    if (!spin_until(fresh)) {
                         std::unique_lock<std::mutex> l(m);
-                        go.wait(l, [&] { return stop || gen != seen; });
-                        if (stop) return;
-                        seen = gen;
-                        f = job;
+                        go.wait(l, fresh);
                     }
-                    f(w + 1);
-                    std::lock_guard<std::mutex> l(m);
-                    if (--busy == 0) done.notify_one();
+                    if (stop.load(std::memory_order_acquire)) return;
+                    seen = gen.load(std::memory_order_acquire);
+                    job(w + 1);
+                    if (busy.fetch_sub(1, std::memory_order_acq_rel) == 1) {
+                        std::lock_guard<std::mutex> l(m);
+                        done.notify_one();
+                    }
                 }
             });
     }
@@ -182,23 +202,21 @@ struct PackPool {
     }
     // the workers run f(base + 1) .. f(base + workers) while the caller goes on; wait() joins
     void start(const std::function<void(int)>& f, int base) {
-        {
-            std::lock_guard<std::mutex> l(m);
-            job = base ? std::function<void(int)>([f, base](int part) { f(base + part); }) : f;
-            busy = (int)th.size();
-            gen++;
-        }
+        job = base ? std::function<void(int)>([f, base](int part) { f(base + part); }) : f;
+        busy.store((int)th.size(), std::memory_order_release);
+        gen.fetch_add(1, std::memory_order_acq_rel);
+        { std::lock_guard<std::mutex> l(m); }  // a worker between its check and its sleep sees gen
         go.notify_all();
     }
     void wait() {
+        auto idle = [&] { return busy.load(std::memory_order_acquire) == 0; };
+        if (spin_until(idle)) return;
         std::unique_lock<std::mutex> l(m);
-        done.wait(l, [&] { return busy == 0; });
+        done.wait(l, idle);
     }
     ~PackPool() {
-        {
-            std::lock_guard<std::mutex> l(m);
-            stop = true;
-        }
+        stop.store(true, std::memory_order_release);
+        { std::lock_guard<std::mutex> l(m); }
         go.notify_all();
         for (auto& t : th) t.join();
     }
@@ -332,6 +350,7 @@ struct tsdf_ctx {
     // leads the split: cache-resident between its two passes
     std::vector<float> split_xyz;
     std::vector<int8_t> split_sec;
+    HostTiming split_ht;  // TSDF_HOST_TIMING: prep, classify, scatter, copies + queue (us/scan)
     uint64_t n_grows = 0, n_replayed = 0;
 };
 
@@ -1472,6 +1491,8 @@ int tsdf_integrate_sectors(tsdf_ctx* const* ctxs, uint32_t n_ctx, const void* pt
     }
     const ScanPose P = pose_of(pose);
     const float ox = (float)P.o[0], oy = (float)P.o[1];
+    HostTiming& ht = c0->split_ht;
+    ht.start();
     // room in every pending batch, and each context's free pinned buffer
     float* h[TSDF_MAX_WORLD];
     int hb[TSDF_MAX_WORLD];
@@ -1546,9 +1567,12 @@ int tsdf_integrate_sectors(tsdf_ctx* const* ctxs, uint32_t n_ctx, const void* pt
             int k = 0;
             if (sharded) {
                 const float a = pseudo_angle(v[0] - ox, v[1] - oy);
-                int c = 0;
-                for (uint32_t j = 0; j < n_ctx; j++) c += a >= u[j] ? 1 : 0;
-                k = a != a ? -1 : (int)((r0 + n_ctx + (uint32_t)c - 1u) % n_ctx);
+                uint32_t c = 0;
+                for (uint32_t j = 0; j < n_ctx; j++) c += a >= u[j] ? 1u : 0u;
+                uint32_t m = r0 + c + n_ctx - 1u;  // (r0 + c - 1) mod N without a division: m < 3N
+                m -= m >= n_ctx ? n_ctx : 0u;
+                m -= m >= n_ctx ? n_ctx : 0u;
+                k = a != a ? -1 : (int)m;
             }
             sec[i] = (int8_t)k;
             if (k >= 0) cl[k]++;
@@ -1566,7 +1590,9 @@ int tsdf_integrate_sectors(tsdf_ctx* const* ctxs, uint32_t n_ctx, const void* pt
             dst[k] += 3;
         }
     };
+    ht.lap(0);
     run_parts(classify);
+    ht.lap(1);
     std::vector<uint64_t> tot(n_ctx, 0);
     for (uint32_t k = 0; k < n_ctx; k++)
         for (int q = 0; q < parts; q++) {
@@ -1574,8 +1600,12 @@ int tsdf_integrate_sectors(tsdf_ctx* const* ctxs, uint32_t n_ctx, const void* pt
             tot[k] += cnt[(size_t)q * n_ctx + k];
         }
     run_parts(scatter);
-    // each context: its sector's points to its GPU, into its pending batch
-    for (uint32_t k = 0; k < n_ctx; k++) {
+    ht.lap(2);
+    // each context: its sector's points to its GPU, into its pending batch -- the contexts are
+    // independent, so the staging threads issue them side by side (the copy and launch API calls
+    // cost ~10 us each on the host)
+    int crc[TSDF_MAX_WORLD] = {};
+    auto push_ctx = [&](uint32_t k) -> int {
         tsdf_ctx* c = ctxs[k];
         HIPCHK(c, hipSetDevice(c->device));
         int rc = pend_stage_buffer(c);
@@ -1584,9 +1614,21 @@ int tsdf_integrate_sectors(tsdf_ctx* const* ctxs, uint32_t n_ctx, const void* pt
             HIPCHK(c, hipMemcpyAsync(c->stage2[c->pend_stage] + 3 * (uint64_t)c->pend.s[c->pend.n_scans].off,
                                      h[k], tot[k] * 12, hipMemcpyHostToDevice, c->stream));
         HIPCHK(c, hipEventRecord(c->stage_done[hb[k]], c->stream));
-        rc = pend_push(c, tot[k], P);
-        if (rc) return rc;
+        return pend_push(c, tot[k], P);
+    };
+    const int cparts = c0->pack && n_ctx > 1 ? std::min<int>(c0->pack->parts(), (int)n_ctx) : 1;
+    if (cparts > 1) {
+        c0->pack->run([&](int part) {
+            if (part >= cparts) return;
+            for (uint32_t k = (uint32_t)part; k < n_ctx; k += (uint32_t)cparts) crc[k] = push_ctx(k);
+        });
+    } else {
+        for (uint32_t k = 0; k < n_ctx; k++) crc[k] = push_ctx(k);
     }
+    for (uint32_t k = 0; k < n_ctx; k++)
+        if (crc[k]) return crc[k];
+    ht.lap(3);
+    ht.n++;
     return TSDF_OK;
 }
 
