@@ -81,8 +81,10 @@ typedef struct tsdf_params {
     uint32_t max_batch;    /* scans integrated per GPU batch, 1..TSDF_MAX_BATCH (default 32) */
     uint32_t pipeline;     /* 1: overlap consecutive batches on two streams (count / compact /
                               place of batch b+1 run beside batch b's place / integrate; same field,
-                              bit for bit); 0 (default): batches run one after another, so per-kernel
-                              timings (tsdf_stats.kernel_ms) are not shared with another batch */
+                              bit for bit); 2: only count / compact of batch b+1 beside batch b's
+                              integrate, place always alone; 0 (default): batches run one after
+                              another, so per-kernel timings (tsdf_stats.kernel_ms) are not shared
+                              with another batch */
     /* ABI v3: backend semantics */
     int32_t semantics;          /* TSDF_SEM_VDBFUSION (default), TSDF_SEM_VOXBLOX or
                                    TSDF_SEM_VDBFUSION_F64 */

@@ -519,7 +519,13 @@ static int launch(tsdf_ctx* c, const float* d_xyz, BatchDesc& D) {
         if (!small) HIPCHK(c, launch_order(W, c->G, par, st));
 #endif
     }
-    if (cross && c->p.pipeline) HIPCHK(c, hipEventRecord(c->ev_compact[par], st));  // batch b+1's wait
+    // pipeline 1: batch b+1's front end waits for this batch's compact (it may run beside this
+    // batch's place and integrate); pipeline 2: for its place, and this batch's place waits for
+    // batch b-1's end, so only k_count / k_compact of b+1 overlap k_integrate of b and k_place
+    // always runs alone
+    const bool lean = c->p.pipeline == 2;
+    if (cross && c->p.pipeline && !lean) HIPCHK(c, hipEventRecord(c->ev_compact[par], st));
+    if (lean && c->batch_id > 0) HIPCHK(c, hipStreamWaitEvent(st, c->ev_integ[par ^ 1], 0));
     if (D.n_blocks) {
         if (tm && c->fused) tm->next(KIND_COMPACT, k_back, st);
         if (c->fused) HIPCHK(c, launch_spans(B, c->R, T, W, c->G, par, c->nstep, st));
@@ -527,7 +533,8 @@ static int launch(tsdf_ctx* c, const float* d_xyz, BatchDesc& D) {
         c->ht.lap(5);
         if (tm && c->fused) tm->end(k_back, st);
     }
-    if (c->batch_id > 0 && cross) HIPCHK(c, hipStreamWaitEvent(st, c->ev_integ[par ^ 1], 0));
+    if (lean) HIPCHK(c, hipEventRecord(c->ev_compact[par], st));  // batch b+1's front-end wait
+    if (c->batch_id > 0 && cross && !lean) HIPCHK(c, hipStreamWaitEvent(st, c->ev_integ[par ^ 1], 0));
     if (D.n_blocks) {
         if (tm && c->fused) tm->begin(KIND_INTEGRATE, st);
         if (small) {

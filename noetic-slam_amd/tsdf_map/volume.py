@@ -96,7 +96,7 @@ class TSDFVolume:
         p.voxel_size = float(voxel_size)
         p.sdf_trunc = float(sdf_trunc)
         p.space_carving = 1 if space_carving else 0
-        p.pipeline = 1 if pipeline else 0
+        p.pipeline = int(pipeline) if not isinstance(pipeline, bool) else (1 if pipeline else 0)
         p.min_range = float(min_range)
         p.max_range = float(max_range)
         p.max_bricks = int(max_bricks)

@@ -149,7 +149,7 @@ def test_pipelined_and_64_scan_batches_bitwise(sim):
     for p, org in scans:
         o.integrate(p, org)
     ref = o.export_voxels()
-    for mb, pipe in ((2, True), (5, True), (64, False), (64, True)):
+    for mb, pipe in ((2, True), (5, True), (64, False), (64, True), (7, 2), (64, 2)):
         g = hip(max_batch=mb, pipeline=pipe)
         for k, (p, org) in enumerate(scans):
             g.integrate(p, org)

@@ -45,7 +45,7 @@ def test_full_c1_scan_from_64_bricks(scan0):
     assert st["n_rays_total"] == scan0[0].shape[0]  # replayed batches are counted once
 
 
-@pytest.mark.parametrize("pipeline", [False, True])
+@pytest.mark.parametrize("pipeline", [False, True, 2])
 @pytest.mark.parametrize("semantics", ["vdbfusion", "voxblox"])
 def test_host_path_sequence_grows(sim, pipeline, semantics):
     """Host-pointer scans in 2-scan batches: the staging checkpoint replays before overwriting."""
@@ -156,7 +156,7 @@ def test_sector_sample_list_grows(sim, walk):
     assert bitwise(g, o)
 
 
-@pytest.mark.parametrize("pipeline", [False, True])
+@pytest.mark.parametrize("pipeline", [False, True, 2])
 def test_metrics_drain_replay_keeps_staged_input(sim, tmp_path, pipeline):
     """the metrics-ring drain inside a launch can run a capacity replay while a host
     batch is already staged.  Hundreds of 1-scan batches with the metrics log on and a pool that

@@ -54,7 +54,7 @@ def test_full_c1_scan_single_walk_bitwise(scan0):
         assert sg[k] == st[k], k
 
 
-@pytest.mark.parametrize("mb,pipe", [(1, False), (7, True), (64, False), (64, True)])
+@pytest.mark.parametrize("mb,pipe", [(1, False), (7, True), (64, False), (64, True), (9, 2)])
 def test_sequences_both_front_ends(sim, mb, pipe):
     scans = [(decimate(p, 8), o) for p, o in (sim.scan(k) for k in range(70))]
     o = ora()
