@@ -72,6 +72,8 @@ def parse():
                          "scans per step): its time per step is one rank's; value = N x batch "
                          "scans / step time, the N-GPU throughput if every rank took as long "
                          "(rehearsal of the scaling runs on a one-GPU box)")
+    ap.add_argument("--rehearsal-sector", type=int, default=0, metavar="K",
+                    help="with --rank-rehearsal N: play rank K (sector K of N) instead of rank 0")
     ap.add_argument("--walk", default="two", choices=("two", "single"),
                     help="front end (tsdf_params.walk): two = k_count + k_place (default); single = "
                          "every ray walked once (k_walk + k_spans) when the band allows it")
@@ -177,7 +179,9 @@ def main():
                         max_bricks=args.max_bricks, device_id=local,
                         max_batch=min(scans_per_step, 512),  # one launch per step (all shards)
                         pipeline=args.pipeline, semantics=args.semantics,
-                        n_sectors=n_shards, sector=rank,  # this rank's azimuth sector of every scan
+                        n_sectors=n_shards,  # this rank's azimuth sector of every scan
+                        sector=(args.rehearsal_sector % n_shards if world == 1 and n_shards > 1
+                                else rank),
                         walk=args.walk)
 
     def run_step(i):
@@ -388,7 +392,8 @@ def main():
                     "scans_per_gpu_batch": args.batch, "pipelined_batches": args.pipeline,
                        "semantics": args.semantics,
                        "parallelism": ("azimuth-sector x%d" % world if world > 1 else
-                                       "rank-0 rehearsal of azimuth-sector x%d" % n_shards
+                                       "rank-%d rehearsal of azimuth-sector x%d" % (
+                                           args.rehearsal_sector % n_shards, n_shards)
                                        if n_shards > 1 else "single"),
                        "sector_split": "in-kernel (timed)" if n_shards > 1 else None,
                        "front_end": ("single walk (k_walk + k_spans)" if "walk" in kernel_ms_per_launch
