@@ -370,6 +370,18 @@ int tsdf_border_pack_device(tsdf_ctx* ctx, const uint64_t* d_all_keys, const uin
 int tsdf_border_merge_device(tsdf_ctx* ctx, const uint32_t* d_recv, const uint64_t* recv_counts,
                              uint32_t world);
 
+/* ---- ABI v7: several GPUs in ONE process (SURVEY §8b's num_gpus / device_ids) ----------------
+ * tsdf_create_sharded: n contexts, context k on device_ids[k] (NULL: device k) as azimuth sector k
+ * of n (p's n_sectors / sector / device_id are overridden), into out[0..n).  Feed them with
+ * tsdf_integrate_sectors (host clouds) or each with the full device scans; read out after
+ * tsdf_border_reduce_local, which runs the three steps above among the n contexts of this process:
+ * keys gathered on the host, each source's tiles copied to their owner's GPU with one peer copy
+ * per (source, owner) pair.  Synchronous; *bricks_moved (may be NULL) = tiles merged.  Contexts of
+ * different processes use the three device entry points with a collective instead. */
+int tsdf_create_sharded(const tsdf_params* p, uint32_t n, const int32_t* device_ids,
+                        tsdf_ctx** out);
+int tsdf_border_reduce_local(tsdf_ctx* const* ctxs, uint32_t n, uint64_t* bricks_moved);
+
 #ifdef __cplusplus
 }
 #endif

@@ -2274,4 +2274,127 @@ int tsdf_border_merge_device(tsdf_ctx* c, const uint32_t* d_recv, const uint64_t
     return tsdf_sync(c);
 }
 
+// ---- one process, several GPUs (SURVEY §8b's num_gpus / device_ids) ------------------------------
+
+int tsdf_create_sharded(const tsdf_params* p, uint32_t n, const int32_t* device_ids, tsdf_ctx** out) {
+    if (!p || !out || n == 0 || n > TSDF_MAX_WORLD) return TSDF_EINVAL;
+    for (uint32_t k = 0; k < n; k++) out[k] = nullptr;
+    for (uint32_t k = 0; k < n; k++) {
+        tsdf_params q = *p;
+        q.device_id = device_ids ? device_ids[k] : (int32_t)k;
+        q.n_sectors = n > 1 ? n : 0;
+        q.sector = k;
+        const int rc = tsdf_create(&q, &out[k]);
+        if (rc) {
+            for (uint32_t j = 0; j < k; j++) {
+                tsdf_destroy(out[j]);
+                out[j] = nullptr;
+            }
+            return rc;
+        }
+    }
+    return TSDF_OK;
+}
+
+// The border reduce of tsdf_brick_keys_device / tsdf_border_pack_device / tsdf_border_merge_device
+// among the contexts of one process: the keys meet on the host, and each source's tiles go to
+// their owner's GPU with one peer copy per (source, owner) pair (xGMI between GPUs; a device copy
+// when two contexts share a GPU).  Synchronous.
+int tsdf_border_reduce_local(tsdf_ctx* const* ctxs, uint32_t n, uint64_t* bricks_moved) {
+    if (!ctxs || n == 0 || n > TSDF_MAX_WORLD) return TSDF_EINVAL;
+    for (uint32_t k = 0; k < n; k++)
+        if (!ctxs[k]) return TSDF_EINVAL;
+    if (bricks_moved) *bricks_moved = 0;
+    if (n == 1) return TSDF_OK;
+    tsdf_ctx* c0 = ctxs[0];
+    std::vector<void*> dev_bufs;  // (device, pointer) freed at the end
+    std::vector<int> dev_of;
+    auto dalloc = [&](tsdf_ctx* c, size_t bytes, void** p) -> int {
+        HIPCHK(c, hipSetDevice(c->device));
+        HIPCHK(c, hipMalloc(p, std::max<size_t>(bytes, 16)));
+        dev_bufs.push_back(*p);
+        dev_of.push_back(c->device);
+        return TSDF_OK;
+    };
+    auto release = [&]() {
+        for (size_t i = 0; i < dev_bufs.size(); i++) {
+            (void)hipSetDevice(dev_of[i]);
+            (void)hipFree(dev_bufs[i]);
+        }
+    };
+    int rc = TSDF_OK;
+    // 1. every context's keys, gathered on the host
+    std::vector<uint64_t> counts(n, 0);
+    std::vector<std::vector<uint64_t>> hkeys(n);
+    for (uint32_t k = 0; k < n && !rc; k++) {
+        tsdf_ctx* c = ctxs[k];
+        uint64_t nb = 0;
+        rc = pool_bricks(c, &nb);
+        void* d = nullptr;
+        if (!rc) rc = dalloc(c, nb * 8, &d);
+        if (!rc) rc = tsdf_brick_keys_device(c, static_cast<uint64_t*>(d), nb, &counts[k]);
+        if (!rc) {
+            hkeys[k].resize(counts[k]);
+            if (counts[k] && hipMemcpy(hkeys[k].data(), d, counts[k] * 8, hipMemcpyDeviceToHost) != hipSuccess)
+                rc = fail(c, TSDF_EHIP, "border reduce: key read-back failed");
+        }
+    }
+    uint64_t stride = 1;
+    for (uint32_t k = 0; k < n; k++) stride = std::max(stride, counts[k]);
+    std::vector<uint64_t> all(stride * n, ~0ull);
+    for (uint32_t k = 0; k < n; k++) std::copy(hkeys[k].begin(), hkeys[k].end(), all.begin() + k * stride);
+    // 2. each context packs the bricks a lower rank owns
+    std::vector<uint32_t*> send(n, nullptr);
+    std::vector<std::vector<uint64_t>> sc(n, std::vector<uint64_t>(n, 0));
+    for (uint32_t k = 0; k < n && !rc; k++) {
+        tsdf_ctx* c = ctxs[k];
+        void *dk = nullptr, *ds = nullptr;
+        rc = dalloc(c, all.size() * 8, &dk);
+        if (!rc && hipMemcpy(dk, all.data(), all.size() * 8, hipMemcpyHostToDevice) != hipSuccess)
+            rc = fail(c, TSDF_EHIP, "border reduce: key upload failed");
+        if (!rc) rc = dalloc(c, counts[k] * TSDF_TILE_WORDS * 4, &ds);
+        if (!rc)
+            rc = tsdf_border_pack_device(c, static_cast<uint64_t*>(dk), counts.data(), stride, n, k,
+                                         static_cast<uint32_t*>(ds), counts[k], sc[k].data());
+        send[k] = static_cast<uint32_t*>(ds);
+    }
+    // 3. every owner d receives block d of every source, sources ascending; 4. merge
+    uint64_t moved = 0;
+    for (uint32_t d = 0; d < n && !rc; d++) {
+        tsdf_ctx* c = ctxs[d];
+        std::vector<uint64_t> rcnt(n, 0);
+        uint64_t total = 0;
+        for (uint32_t r = 0; r < n; r++) {
+            rcnt[r] = sc[r][d];
+            total += rcnt[r];
+        }
+        if (!total) continue;
+        void* dr = nullptr;
+        rc = dalloc(c, total * TSDF_TILE_WORDS * 4, &dr);
+        uint64_t row = 0;
+        for (uint32_t r = 0; r < n && !rc; r++) {
+            if (!rcnt[r]) continue;
+            uint64_t off = 0;
+            for (uint32_t q = 0; q < d; q++) off += sc[r][q];
+            const size_t bytes = rcnt[r] * TSDF_TILE_WORDS * 4;
+            uint32_t* dst = static_cast<uint32_t*>(dr) + row * TSDF_TILE_WORDS;
+            const uint32_t* src = send[r] + off * TSDF_TILE_WORDS;
+            const hipError_t e = ctxs[r]->device == c->device
+                                     ? hipMemcpy(dst, src, bytes, hipMemcpyDeviceToDevice)
+                                     : hipMemcpyPeer(dst, c->device, src, ctxs[r]->device, bytes);
+            if (e != hipSuccess) rc = fail(c, TSDF_EHIP, "border reduce: tile copy: %s", hipGetErrorString(e));
+            row += rcnt[r];
+        }
+        if (!rc) rc = tsdf_border_merge_device(c, static_cast<uint32_t*>(dr), rcnt.data(), n);
+        moved += total;
+    }
+    release();
+    if (rc) {  // the failing context holds the message; the first context gets a copy
+        for (uint32_t k = 1; k < n && c0->err.empty(); k++) c0->err = ctxs[k]->err;
+        return rc;
+    }
+    if (bricks_moved) *bricks_moved = moved;
+    return TSDF_OK;
+}
+
 }  // extern "C"

@@ -130,6 +130,9 @@ SIGNATURES = {
     "tsdf_reset_stats": (C.c_int, [P]),
     "tsdf_set_profiling": (C.c_int, [P, C.c_int32]),
     "tsdf_set_profiling_period": (C.c_int, [P, C.c_uint32, C.c_uint32]),
+    "tsdf_create_sharded": (C.c_int, [C.POINTER(TsdfParams), C.c_uint32, C.POINTER(C.c_int32),
+                                      C.POINTER(P)]),
+    "tsdf_border_reduce_local": (C.c_int, [C.POINTER(P), C.c_uint32, U64P]),
     "tsdf_set_metrics_log": (C.c_int, [P, C.c_char_p]),
     "tsdf_select_sector": (C.c_int, [FP, C.c_uint64, D3, C.c_double, C.c_uint32, C.c_uint32, FP,
                                      U64P]),

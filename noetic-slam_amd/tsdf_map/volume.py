@@ -83,15 +83,33 @@ class TSDFVolume:
     # into this memory): host memory for a CPU library, the context's GPU for libtsdf_hip.so
     tensor_device = "cpu"
 
-    def __init__(self, lib, voxel_size, sdf_trunc, space_carving=False, min_range=0.0,
-                 max_range=math.inf, max_bricks=1 << 20, max_points=1 << 18, device_id=0,
-                 max_batch=32, pipeline=False, semantics="vdbfusion", allow_clear=True,
-                 use_weight_dropoff=True, max_weight=10000.0, n_sectors=0, sector=0,
-                 sector_yaw0=0.0, max_bricks_hard=0, walk="two", use_const_weight=True):
+    def __init__(self, lib, voxel_size, sdf_trunc, space_carving=False, **kw):
         self._lib = lib
+        self._ctx = C.c_void_p()
+        p = self.make_params(lib, voxel_size, sdf_trunc, space_carving, **kw)
+        rc = lib.tsdf_create(C.byref(p), C.byref(self._ctx))
+        if rc != _abi.TSDF_OK:
+            self._ctx = C.c_void_p()
+            raise TsdfError(rc, "tsdf_create failed (voxel_size=%g sdf_trunc=%g)" %
+                            (voxel_size, sdf_trunc))
+        self._adopt(p)
+
+    def _adopt(self, p):
+        self.params = p
+        self.semantics = {v: k for k, v in _abi.SEMANTICS.items()}.get(p.semantics, "vdbfusion")
+        self.voxel_size = float(p.voxel_size)
+        self.sdf_trunc = float(p.sdf_trunc)
+        self.space_carving = bool(p.space_carving)
+
+    @staticmethod
+    def make_params(lib, voxel_size, sdf_trunc, space_carving=False, min_range=0.0,
+                    max_range=math.inf, max_bricks=1 << 20, max_points=1 << 18, device_id=0,
+                    max_batch=32, pipeline=False, semantics="vdbfusion", allow_clear=True,
+                    use_weight_dropoff=True, max_weight=10000.0, n_sectors=0, sector=0,
+                    sector_yaw0=0.0, max_bricks_hard=0, walk="two", use_const_weight=True):
+        """tsdf_params from the VDBFusion / Voxblox-style keyword arguments."""
         if semantics not in _abi.SEMANTICS:
             raise ValueError("semantics must be one of %s" % sorted(_abi.SEMANTICS))
-        self._ctx = C.c_void_p()
         p = _abi.default_params(lib)
         p.voxel_size = float(voxel_size)
         p.sdf_trunc = float(sdf_trunc)
@@ -116,16 +134,7 @@ class TSDFVolume:
         p.walk = {"two": _abi.WALK_TWO, "single": _abi.WALK_SINGLE}[walk]
         # Voxblox getVoxelWeight: 1 (use_const_weight) or 1 / z^2 of the sensor-frame depth
         p.depth_weight = 0 if use_const_weight else 1
-        self.params = p
-        self.semantics = semantics
-        rc = lib.tsdf_create(C.byref(p), C.byref(self._ctx))
-        if rc != _abi.TSDF_OK:
-            self._ctx = C.c_void_p()
-            raise TsdfError(rc, "tsdf_create failed (voxel_size=%g sdf_trunc=%g)" %
-                            (voxel_size, sdf_trunc))
-        self.voxel_size = float(voxel_size)
-        self.sdf_trunc = float(sdf_trunc)
-        self.space_carving = bool(space_carving)
+        return p
 
     # -- lifecycle ------------------------------------------------------------------------------
     def close(self):
@@ -329,6 +338,17 @@ def integrate_sectors(volumes, points, extrinsic):
     v0._check(rc, "integrate_sectors")
 
 
+def border_reduce_local(volumes):
+    """tsdf_border_reduce_local: the border-brick reduce among sector volumes of this process
+    (peer copies between their GPUs, no collective); returns the tiles merged."""
+    v0 = volumes[0]
+    ctxs = (C.c_void_p * len(volumes))(*[v._ctx.value for v in volumes])
+    moved = C.c_uint64()
+    v0._check(v0._lib.tsdf_border_reduce_local(ctxs, len(volumes), C.byref(moved)),
+              "border_reduce_local")
+    return moved.value
+
+
 def bricks_to_voxels(coords, sdf, weight):
     coords = np.asarray(coords, np.int64).reshape(-1, 3)
     s = np.asarray(sdf, np.float32).reshape(-1, 8, 8, 8)
@@ -346,6 +366,33 @@ class HipTSDFVolume(TSDFVolume):
     def __init__(self, voxel_size, sdf_trunc, space_carving=False, **kw):
         super().__init__(load_hip_library(), voxel_size, sdf_trunc, space_carving, **kw)
         self.tensor_device = "cuda:%d" % self.params.device_id
+
+    @classmethod
+    def sharded(cls, n, voxel_size, sdf_trunc, device_ids=None, **kw):
+        """tsdf_create_sharded: n volumes in this process, volume k on device_ids[k] (default k)
+        as azimuth sector k of n.  Feed them with `integrate_sectors`, reduce their border bricks
+        with `border_reduce_local`."""
+        lib = load_hip_library()
+        kw = {k: v for k, v in kw.items() if k not in ("n_sectors", "sector", "device_id")}
+        p = cls.make_params(lib, voxel_size, sdf_trunc, **kw)
+        ids = None if device_ids is None else (C.c_int32 * n)(*[int(d) for d in device_ids])
+        out = (C.c_void_p * n)()
+        rc = lib.tsdf_create_sharded(C.byref(p), int(n), ids, out)
+        if rc != _abi.TSDF_OK:
+            raise TsdfError(rc, "tsdf_create_sharded failed (n=%d)" % n)
+        vols = []
+        for k in range(n):
+            v = cls.__new__(cls)
+            v._lib = lib
+            v._ctx = C.c_void_p(out[k])
+            q = _abi.TsdfParams.from_buffer_copy(p)
+            q.device_id = int(device_ids[k]) if device_ids is not None else k
+            q.n_sectors = n if n > 1 else 0
+            q.sector = k
+            v._adopt(q)
+            v.tensor_device = "cuda:%d" % q.device_id
+            vols.append(v)
+        return vols
 
     def integrate_device(self, d_xyz_ptr, n, extrinsic):
         o = _origin_of(extrinsic)

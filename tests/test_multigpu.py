@@ -148,6 +148,35 @@ def test_border_reduce_matches_oracle_bitwise(sim):
     assert np.max(np.abs(ms - rs)) <= 1e-5
 
 
+def test_sharded_contexts_local_reduce_bitwise(sim):
+    """tsdf_create_sharded + tsdf_integrate_sectors + tsdf_border_reduce_local: one process
+    driving n sector contexts (here all on GPU 0; on a node, one per GPU, tiles between GPUs by
+    peer copy) gives every context the oracle's reduced field bit for bit, twice over."""
+    from tsdf_map import HipTSDFVolume, border_reduce_local, integrate_sectors
+    world, yaw0 = 4, 0.6
+    g = HipTSDFVolume.sharded(world, VS, TAU, device_ids=[0] * world, sector_yaw0=yaw0,
+                              max_bricks=1 << 18, max_batch=4)
+    assert [v.params.sector for v in g] == list(range(world))
+    assert all(v.params.n_sectors == world and v.params.device_id == 0 for v in g)
+    o = [ora(n_sectors=world, sector=r, sector_yaw0=yaw0) for r in range(world)]
+    moved = 0
+    for ks in ((0, 1, 2), (30,)):
+        for k in ks:
+            pts, org = sim.scan(k)
+            pts = np.ascontiguousarray(pts[::2])
+            integrate_sectors(g, pts, org)
+            for v in o:
+                v.integrate(pts, org)
+        moved += border_reduce_local(g)
+        splits = emulated_reduce_host(o)
+        assert sum(map(sum, splits)) > 100
+        for r in range(world):
+            assert voxels_equal_bitwise(g[r].export_voxels(), o[r].export_voxels()), (ks, r)
+    assert moved > 100
+    for v in g:
+        v.close()
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
