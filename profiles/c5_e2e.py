@@ -4,8 +4,9 @@
   synthetic DLIO bag (N world-frame dlio::Point clouds of the OS-1-128 1024x10 sensor + 100 Hz
   poses; no bag ships with the reference) -> tsdf_map.ingest.ingest_bag -> the GPU field at
   2 cm / 6 cm -> tsdf_extract_mesh, for both fusion rules:
-    vdbfusion  GPU field and mesh == the oracle's (scan-fused, bitwise); distance of the field from
-               the literal VDBFusion restatement (ORACLE_MODE_VDB_LITERAL)
+    vdbfusion_f64  GPU field and mesh == the oracle's (scan-fused, bitwise); distance of the field
+               from the literal VDBFusion restatement at upstream's precisions
+               (ORACLE_MODE_VDB_LITERAL: same voxels and weights expected)
     voxblox    GPU field and mesh == the oracle's scan-fused twin (bitwise); per-voxel diff against
                ORACLE_MODE_SEQUENTIAL (the literal per-sample Voxblox update in input order):
                max / p99.9 |dS| and the count over 0.1 tau (reported, not gated)
@@ -81,7 +82,7 @@ def main():
               "bag_bytes": os.path.getsize(bag), "bag_write_s": round(time.time() - tb, 1)}
     vb = dict(semantics="voxblox", space_carving=False, max_range=100.0, min_range=0.1,
               allow_clear=True, use_weight_dropoff=True)
-    for sem, kw in (("vdbfusion", {}), ("voxblox", vb)):
+    for sem, kw in (("vdbfusion_f64", dict(semantics="vdbfusion_f64")), ("voxblox", vb)):
         r = {}
         g = HipTSDFVolume(args.voxel, args.trunc, max_bricks=1 << 20, **kw)
         t = time.time()
@@ -95,6 +96,10 @@ def main():
         vg, _ = g.extract_triangle_mesh()
         r["gpu_mesh_s"] = round(time.time() - t, 3)
         r["triangles"] = int(vg.shape[0] // 3)
+        t = time.time()
+        vl, _ = g.extract_triangle_mesh(table="lorensen")
+        r["gpu_mesh_lorensen_s"] = round(time.time() - t, 3)
+        r["triangles_lorensen"] = int(vl.shape[0] // 3)
         gv = g.export_voxels()
         o = oracle.OracleTSDFVolume(args.voxel, args.trunc, threads=args.threads, **kw)
         t = time.time()
@@ -108,7 +113,7 @@ def main():
         vo, _ = o1.extract_triangle_mesh()
         r["mesh_bitwise"] = bool(vo.shape == vg.shape and np.array_equal(vo, vg))
         del o, o1
-        mode = oracle.MODE_VDB_LITERAL if sem == "vdbfusion" else oracle.MODE_SEQUENTIAL
+        mode = oracle.MODE_VDB_LITERAL if sem == "vdbfusion_f64" else oracle.MODE_SEQUENTIAL
         lit = oracle.OracleTSDFVolume(args.voxel, args.trunc, mode=mode, **kw)
         t = time.time()
         assert ingest.ingest_bag(lit, bag) == (args.scans, 0)
