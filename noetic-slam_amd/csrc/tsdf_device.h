@@ -50,11 +50,14 @@ constexpr int RPB = TSDF_RPB;          // rays per k_count / k_place block (one 
 constexpr int HCAP = TSDF_HCAP;        // LDS brick-hash slots per k_count block (~300-800 used)
 constexpr int LDS_PROBES = 64;         // probe limit before a pair takes the global fallback
 constexpr int MAX_IN_BRICK = 22;       // a line visits at most 8+8+8-2 voxels of an 8^3 brick
-// k_place's LDS staging: samples per workgroup (6 B each; 4 workgroups per CU), the bitmap words
-// of run starts, and the staging plan k_count hands over per half block (Work::plan: the bitmap
-// words, their exclusive popcount prefix as u16 pairs, then the staged sample count)
+// k_place's LDS staging: samples per workgroup (6 B each), the bitmap words of run starts, and the
+// staging plan k_count hands over per half block (Work::plan: the bitmap words, their exclusive
+// popcount prefix as u16 per word, then the staged sample count).  5600 samples hold nearly a whole
+// half block's samples (~4.8 k on average) at 50 KB of LDS, three workgroups per CU: fewer samples
+// go out as scattered 8-B stores, which cost more than the fourth workgroup per CU bought
+// (k_place 0.407 -> 0.390 ms against 3800 samples / four workgroups; 6000 no longer fits three)
 #ifndef TSDF_PLC_STAGE
-#define TSDF_PLC_STAGE 3800
+#define TSDF_PLC_STAGE 5600
 #endif
 constexpr int PLC_STAGE = TSDF_PLC_STAGE;
 constexpr int PLC_WORDS = (PLC_STAGE + 31) / 32;

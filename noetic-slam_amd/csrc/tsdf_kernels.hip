@@ -114,9 +114,7 @@ __global__ __launch_bounds__(NT, SEM == 2 && NT == CNT_THREADS ? TSDF_F64_COUNT_
     __shared__ unsigned long long red[2][NT / 64];
     __shared__ unsigned long long s_wsum[NT / 64];
     __shared__ uint32_t s_wcnt[NT / 64];
-#ifndef TSDF_NO_PLAN
     __shared__ uint32_t s_bm[2][PLC_WORDS];  // per half: staging positions where a run starts
-#endif
     Counters* C = &G->ctr[parity];  // zeroed by the previous batch of this parity (k_finish)
     // sector sharding: every GPU sees every scan, and a block of 1024 consecutive rays (~3 degrees
     // of azimuth) usually lies wholly in one sector; the workgroups take the blocks k_sector_flags
@@ -133,9 +131,7 @@ __global__ __launch_bounds__(NT, SEM == 2 && NT == CNT_THREADS ? TSDF_F64_COUNT_
         s_key[j] = EMPTY_KEY;
         s_cnt[j] = 0u;
     }
-#ifndef TSDF_NO_PLAN
     for (int j = threadIdx.x; j < 2 * PLC_WORDS; j += NT) (&s_bm[0][0])[j] = 0u;
-#endif
     __syncthreads();
     const uint32_t maxp = Wk.maxp;
     uint32_t valid = 0, npairs = 0;
@@ -345,7 +341,6 @@ __global__ __launch_bounds__(NT, SEM == 2 && NT == CNT_THREADS ? TSDF_F64_COUNT_
         if (threadIdx.x == NT - 1) {
             Wk.blk_n[2 * bx] = totc & 0xFFFFu;
             Wk.blk_n[2 * bx + 1] = totc >> 16;
-#ifndef TSDF_NO_PLAN
             // each half's staged sample count: its samples, up to the staging capacity
             unsigned long long tot = 0;
             for (int w = 0; w < NT / 64; w++) tot += s_wsum[w];
@@ -353,7 +348,6 @@ __global__ __launch_bounds__(NT, SEM == 2 && NT == CNT_THREADS ? TSDF_F64_COUNT_
                 min((uint32_t)tot, (uint32_t)PLC_STAGE);
             Wk.plan[(size_t)(2 * bx + 1) * PLAN_STRIDE + PLAN_STRIDE - 1] =
                 min((uint32_t)(tot >> 32), (uint32_t)PLC_STAGE);
-#endif
         }
     }
     // The thread's SPT slots go to the global table in three batched stages, so their round trips
@@ -402,41 +396,45 @@ __global__ __launch_bounds__(NT, SEM == 2 && NT == CNT_THREADS ? TSDF_F64_COUNT_
         }
         if (n0) {
             bt0[idx0++] = make_uint4(tx, rk, off0, n0 | ((uint32_t)slot << 16));
-#ifndef TSDF_NO_PLAN
             if (off0 < (uint32_t)PLC_STAGE) atomicOr(&s_bm[0][off0 >> 5], 1u << (off0 & 31));
-#endif
             off0 += n0;
         }
         if (n1) {
             bt1[idx1++] = make_uint4(tx, rk + n0, off1, n1 | ((uint32_t)slot << 16));
-#ifndef TSDF_NO_PLAN
             if (off1 < (uint32_t)PLC_STAGE) atomicOr(&s_bm[1][off1 >> 5], 1u << (off1 & 31));
-#endif
             off1 += n1;
         }
     }
-#ifndef TSDF_NO_PLAN
     // k_place's staging plan for each half: the run-start bitmap and its exclusive popcount
     // prefix per word (wave h writes half h's)
     __syncthreads();
     {
         const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
         if (wv < 2) {
+            // WPL consecutive bitmap words per lane; the prefix is one u16 per word
             constexpr int WPL = (PLC_WORDS + 63) / 64;
-            static_assert(WPL == 2, "two bitmap words per lane");
+            static_assert(WPL >= 1 && WPL <= 4, "bitmap words per lane");
             uint32_t* pl = Wk.plan + (size_t)(2 * bx + wv) * PLAN_STRIDE;
-            const int w0 = 2 * ln, w1 = 2 * ln + 1;
-            const uint32_t b0 = w0 < PLC_WORDS ? s_bm[wv][w0] : 0u;
-            const uint32_t b1 = w1 < PLC_WORDS ? s_bm[wv][w1] : 0u;
-            const uint32_t c0 = (uint32_t)__popc(b0), cs = c0 + (uint32_t)__popc(b1);
-            const uint32_t pre = wave_incl_scan(cs) - cs;
-            if (w0 < PLC_WORDS) pl[w0] = b0;
-            if (w1 < PLC_WORDS) pl[w1] = b1;
-            // the prefix of words w0, w1 as one u16 pair (little endian: w0 low)
-            if (w0 < PLC_WORDS) pl[PLC_WORDS + ln] = (pre & 0xFFFFu) | ((pre + c0) << 16);
+            uint16_t* pp = reinterpret_cast<uint16_t*>(pl + PLC_WORDS);
+            uint32_t b[WPL], cs = 0;
+#pragma unroll
+            for (int q = 0; q < WPL; q++) {
+                const int wd = WPL * ln + q;
+                b[q] = wd < PLC_WORDS ? s_bm[wv][wd] : 0u;
+                cs += (uint32_t)__popc(b[q]);
+            }
+            uint32_t pre = wave_incl_scan(cs) - cs;
+#pragma unroll
+            for (int q = 0; q < WPL; q++) {
+                const int wd = WPL * ln + q;
+                if (wd < PLC_WORDS) {
+                    pl[wd] = b[q];
+                    pp[wd] = (uint16_t)pre;
+                }
+                pre += (uint32_t)__popc(b[q]);
+            }
         }
     }
-#endif
     // block-reduce the stats, one atomic per block on a shard picked by block index
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     unsigned long long v = wave_sum<unsigned long long>(valid);
@@ -868,7 +866,7 @@ __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) v
     __shared__ float st_s[PLC_STAGE];      // staged samples
     __shared__ uint16_t st_l[PLC_STAGE];
     __shared__ float st_w[SEM == 3 ? PLC_STAGE : 1];  // Voxblox 1/z^2: the samples' weights
-#if defined(TSDF_NO_PLAN) || defined(TSDF_ABLATE_PL_EMPTY)
+#ifdef TSDF_ABLATE_PL_EMPTY
     __shared__ uint32_t s_nst;             // staged samples (end of the last staged run)
 #endif
 #ifdef TSDF_PLC_PHASE  // diagnostic build: thread 0's clock at the phase boundaries
@@ -911,7 +909,6 @@ __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) v
     const uint32_t nruns = Wk.blk_n[wb];
     static_assert(PLC_THREADS <= HCAP, "a lane's first list entry lies inside the list");
     const uint4 e0 = bt[threadIdx.x];
-#ifndef TSDF_NO_PLAN
     // k_count's staging plan: bitmap words, their prefix (u16 pairs) and the staged count
     const uint32_t* pl = Wk.plan + (size_t)wb * PLAN_STRIDE;
     static_assert(PLC_WORDS <= PLC_THREADS, "one bitmap word per lane");
@@ -919,51 +916,44 @@ __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) v
     const uint32_t plan_pre =
         threadIdx.x < (uint32_t)((PLC_WORDS + 1) / 2) ? pl[PLC_WORDS + threadIdx.x] : 0u;
     const uint32_t plan_nst = pl[PLAN_STRIDE - 1];
-#endif
     // a run's absolute sample position is its (brick, scan) cell (absolute after k_compact) + its
-    // rank
-    const uint32_t base0 = (threadIdx.x < nruns && e0.x != NO_PAIR)
-                               ? T.cell[(size_t)e0.x * T.cell_stride + t] + e0.y
+    // rank.  The gather is issued here; for short rays (maxp <= 4) its value is first needed after
+    // the walk (the copy-out, and the rare samples the staging cannot hold), so the walk hides it.
+    const bool late = maxp <= 4;
+    const uint32_t cell0 = (threadIdx.x < nruns && e0.x != NO_PAIR)
+                               ? T.cell[(size_t)e0.x * T.cell_stride + t]
                                : NO_PAIR;
     const float ox = D.s[t].ox, oy = D.s[t].oy, oz = D.s[t].oz;
     typename Walk<SEM>::State r;
     const bool ok = i < r1 && Walk<SEM>::init(R, D, t, px, py, pz, r);
     // sector sharding: a half block without a ray of this GPU's sector has no samples to place
     if (R.sec_on && !__syncthreads_or(ok)) return;
-#ifndef TSDF_NO_PLAN
     if (threadIdx.x < (uint32_t)PLC_WORDS) s_bits[threadIdx.x] = plan_bits;
     if (threadIdx.x < (uint32_t)((PLC_WORDS + 1) / 2))
         reinterpret_cast<uint32_t*>(s_wpre)[threadIdx.x] = plan_pre;
-#else
-    for (int j = threadIdx.x; j < PLC_WORDS; j += PLC_THREADS) s_bits[j] = 0u;
-    if (threadIdx.x == 0) s_nst = 0u;
-    __syncthreads();
-#endif
 #ifdef TSDF_PLC_PHASE
     if (threadIdx.x == 0) pt[1] = clock64();
 #endif
     // run table from the dense run list (k_count order = sample order); staged runs are a prefix
     // of the list, so a staged run's list index is its staging rank
-    auto fill = [&](uint32_t j, const uint4& e, uint32_t base) {
-        const uint32_t slot = e.w >> 16, n = e.w & 0xFFFFu;
-        s_base[slot] = base;
+    auto fill = [&](uint32_t j, const uint4& e) {
+        const uint32_t slot = e.w >> 16;
         // runs starting past the staging capacity are stored directly (0xFFFF: not staged)
         const bool stg = e.z < (uint32_t)PLC_STAGE;
         s_loff[slot] = stg ? (uint16_t)e.z : (uint16_t)0xFFFFu;
-        if (stg) {
-            s_ord[j] = (uint16_t)slot;
-#ifdef TSDF_NO_PLAN
-            atomicOr(&s_bits[e.z >> 5], 1u << (e.z & 31));
-            atomicMax(&s_nst, min(e.z + n, (uint32_t)PLC_STAGE));
-#else
-            (void)n;
-#endif
-        }
+        if (stg) s_ord[j] = (uint16_t)slot;
     };
-    if (threadIdx.x < nruns) fill(threadIdx.x, e0, base0);
+    auto run_base = [&](const uint4& e, uint32_t cell) {
+        return e.x != NO_PAIR ? cell + e.y : NO_PAIR;
+    };
+    if (threadIdx.x < nruns) {
+        fill(threadIdx.x, e0);
+        if (!late) s_base[e0.w >> 16] = run_base(e0, cell0);
+    }
     for (uint32_t j = threadIdx.x + PLC_THREADS; j < nruns; j += PLC_THREADS) {
         const uint4 e = bt[j];
-        fill(j, e, e.x != NO_PAIR ? T.cell[(size_t)e.x * T.cell_stride + t] + e.y : NO_PAIR);
+        fill(j, e);
+        if (!late) s_base[e.w >> 16] = run_base(e, e.x != NO_PAIR ? T.cell[(size_t)e.x * T.cell_stride + t] : 0u);
     }
     __syncthreads();
 #ifdef TSDF_PLC_PHASE
@@ -972,97 +962,78 @@ __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) v
 #ifdef TSDF_ABLATE_PL_PROLOGUE  // diagnostic build: the prologue (loads, run tables) only
     if (D.n_scans != 0xFFFFFFFFu) return;
 #endif
-#ifdef TSDF_NO_PLAN
-    if (threadIdx.x < 64) {  // exclusive prefix of run starts per bitmap word (one wave)
-        constexpr int WPL = (PLC_WORDS + 63) / 64;
-        uint32_t cnt[WPL], sum = 0;
-#pragma unroll
-        for (int q = 0; q < WPL; q++) {
-            const int wd = threadIdx.x * WPL + q;
-            cnt[q] = wd < PLC_WORDS ? (uint32_t)__popc(s_bits[wd]) : 0u;
-            sum += cnt[q];
-        }
-        const uint32_t incl = wave_incl_scan(sum);
-        uint32_t pre = incl - sum;
-#pragma unroll
-        for (int q = 0; q < WPL; q++) {
-            const int wd = threadIdx.x * WPL + q;
-            if (wd < PLC_WORDS) s_wpre[wd] = (uint16_t)pre;
-            pre += cnt[q];
-        }
-    }
-    __syncthreads();
-#endif
 #ifdef TSDF_PLC_PHASE
     if (threadIdx.x == 0) pt[3] = clock64();
 #endif
-#ifdef TSDF_ABLATE_PL_NOWALK
-    if (ok && r.px == 1e30f) {
-#else
-    if (ok) {
-#endif
-        // a pair code -> its samples' global position, staging position (lpos < PLC_STAGE), count
-        auto resolve = [&](uint32_t code, uint32_t& pos, uint32_t& lpos, uint32_t& cnt) {
-            pos = NO_PAIR;
-            lpos = NO_PAIR;
-            cnt = 0;
-            if (code == NO_PAIR || code == PAIR_DEAD) return;
-            cnt = (code >> PAIR_CNT_SHIFT) & 31u;
-            if (code & PAIR_FB) {
+    // a pair code -> its samples' global position (when `with_pos`: s_base is filled), staging
+    // position (lpos < PLC_STAGE), count
+    auto resolve = [&](uint32_t code, bool with_pos, uint32_t& pos, uint32_t& lpos, uint32_t& cnt) {
+        pos = NO_PAIR;
+        lpos = NO_PAIR;
+        cnt = 0;
+        if (code == NO_PAIR || code == PAIR_DEAD) return;
+        cnt = (code >> PAIR_CNT_SHIFT) & 31u;
+        if (code & PAIR_FB) {
+            if (with_pos) {
                 const uint4 f = Wk.fb[code & ((1u << PAIR_CNT_SHIFT) - 1u)];
                 pos = T.cell[(size_t)f.x * T.cell_stride + f.y] + f.z;
-            } else {
-                const uint32_t slot = (code >> PAIR_LID_SHIFT) & (HCAP - 1);
-                const uint32_t b = s_base[slot];
-                const uint32_t lr = code & ((1u << PAIR_LID_SHIFT) - 1u);
-                if (b != NO_PAIR) {
-                    pos = b + lr;
-                    const uint32_t lo = s_loff[slot];
-                    if (lo != 0xFFFFu) lpos = lo + lr;
-                }
             }
-        };
-        // Short rays (maxp <= 4): all of the ray's pairs are resolved up front, convergent across
-        // lanes; the walk then only selects the k-th.
-        const bool fast = maxp <= 4;
+        } else {
+            const uint32_t slot = (code >> PAIR_LID_SHIFT) & (HCAP - 1);
+            const uint32_t lr = code & ((1u << PAIR_LID_SHIFT) - 1u);
+            const uint32_t b = with_pos ? s_base[slot] : 0u;
+            if (b != NO_PAIR) {
+                if (with_pos) pos = b + lr;
+                const uint32_t lo = s_loff[slot];
+                if (lo != 0xFFFFu) lpos = lo + lr;
+            }
+        }
+    };
+    // Short rays (maxp <= 4): all of the ray's pairs are resolved up front, convergent across
+    // lanes; the walk then only selects the k-th.  Branch-free (lanes are at different steps of
+    // different pairs, so every data-dependent branch would run for the whole wave).
+    //   pass 0 (late: the bases are not known yet): the samples the staging holds go to LDS, and a
+    //          lane whose ray has others (past the staging, fallback pairs) notes it;
+    //   pass 1 (after the bases; only those lanes): the ray walks again and stores the others.
+    // Without `late` one pass does both, with the bases from the prologue.
+    bool ovf = false;
+    auto walk_short = [&](auto stage_c, auto direct_c) {
+        constexpr bool STAGE = decltype(stage_c)::value, DIRECT = decltype(direct_c)::value;
+        constexpr bool WITH_POS = DIRECT;
+        uint4 code = make_uint4(NO_PAIR, NO_PAIR, NO_PAIR, NO_PAIR);
+        if (maxp == 4) {
+            code = code4;
+        } else {
+            code.x = pc[0];
+            if (maxp > 1) code.y = pc[1];
+            if (maxp > 2) code.z = pc[2];
+        }
         // pair queue: global position P, and (staging position | count << 16) Q; a staging
         // position of 0xFFFF (>= PLC_STAGE) means not staged
         uint32_t P0 = NO_PAIR, P1 = NO_PAIR, P2 = NO_PAIR, P3 = NO_PAIR;
         uint32_t Q0 = 0xFFFFu, Q1 = 0xFFFFu, Q2 = 0xFFFFu, Q3 = 0xFFFFu;
         static_assert(PLC_STAGE < 0xFFFF, "staging positions are 16-bit");
-        if (fast) {
-            uint4 code = code4;
-            if (maxp < 4) {
-                code.x = pc[0];
-                if (maxp > 1) code.y = pc[1];
-                if (maxp > 2) code.z = pc[2];
-            }
-            auto resolve_q = [&](uint32_t c, uint32_t& P, uint32_t& Q) {
-                uint32_t lp, n;
-                resolve(c, P, lp, n);
-                Q = min(lp, 0xFFFFu) | (n << 16);
-            };
-            resolve_q(code.x, P0, Q0);
-            resolve_q(code.y, P1, Q1);
-            resolve_q(code.z, P2, Q2);
-            resolve_q(code.w, P3, Q3);
-        }
-        uint32_t cur = ~0u;  // brick code of the current pair
-        // current pair: global position, or staging position (lpos < PLC_STAGE)
-        uint32_t k = 0, pos = NO_PAIR, lpos = NO_PAIR, cnt = 0, w = 0;
-        if (fast) {
-            // Branch-free walk: lanes are at different steps of different pairs, so every
-            // data-dependent branch here would run for the whole wave; selects cost less.
-            uint32_t lq = 0xFFFFu;  // current pair's (staging position | count << 16)
-            auto walk = [&](auto chk) {
+        auto resolve_q = [&](uint32_t c, uint32_t& P, uint32_t& Q) {
+            uint32_t lp, n;
+            resolve(c, WITH_POS, P, lp, n);
+            Q = min(lp, 0xFFFFu) | (n << 16);
+        };
+        resolve_q(code.x, P0, Q0);
+        resolve_q(code.y, P1, Q1);
+        resolve_q(code.z, P2, Q2);
+        resolve_q(code.w, P3, Q3);
+        uint32_t cur = ~0u;          // brick code of the current pair
+        uint32_t pos = NO_PAIR, w = 0;
+        uint32_t lq = 0xFFFFu;       // current pair's (staging position | count << 16)
+        auto walk = [&](auto chk) {
             for (int it = 0; it < MAX_DDA_STEPS; it++) {
                 float s;
                 const bool g = Walk<SEM>::sample_sel(R, ox, oy, oz, r, s, decltype(chk)::value);
                 const uint32_t key = brick_code_of(r.vx, r.vy, r.vz);
                 const bool nb = g && key != cur;  // the ray's next pair, in k_count's order
                 cur = nb ? key : cur;
-                // take the head of the ray's pair queue (P0, L0, N0) and shift the queue: plain
-                // selects (a select on the pair index k compiles to branches)
+                // take the head of the ray's pair queue and shift the queue: plain selects (a
+                // select on the pair index k compiles to branches)
                 pos = nb ? P0 : pos;
                 lq = nb ? Q0 : lq;
                 P0 = nb ? P1 : P0;
@@ -1077,46 +1048,75 @@ __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) v
                 const uint32_t lpos = lq & 0xFFFFu, cnt = lq >> 16;
                 const bool st = g && w < cnt;
                 const uint32_t l = ((r.vz & 7) << 6) | ((r.vy & 7) << 3) | (r.vx & 7);
-                const bool stage = st && lpos + w < (uint32_t)PLC_STAGE;
-                if (stage) {
+                const bool staged = lpos + w < (uint32_t)PLC_STAGE;
+                if (STAGE && st && staged) {
                     st_s[lpos + w] = s;
                     st_l[lpos + w] = (uint16_t)l;
                     if constexpr (SEM == 3) st_w[lpos + w] = vb_weight(R, r.w0, s);
-                } else if (st && pos != NO_PAIR && pos + w < Wk.max_smp) {
-                    Wk.smp[pos + w] = make_uint2(__float_as_uint(s), (t << 9) | l);
-                    if constexpr (SEM == 3) Wk.smw[pos + w] = vb_weight(R, r.w0, s);
+                } else if (st && !staged) {
+                    if constexpr (DIRECT) {
+                        if (pos != NO_PAIR && pos + w < Wk.max_smp) {
+                            Wk.smp[pos + w] = make_uint2(__float_as_uint(s), (t << 9) | l);
+                            if constexpr (SEM == 3) Wk.smw[pos + w] = vb_weight(R, r.w0, s);
+                        }
+                    } else {
+                        ovf = true;
+                    }
                 }
                 w += g ? 1u : 0u;
                 if (!Walk<SEM>::step(r)) break;
             }
-            };
-            if (__all(Walk<SEM>::inside(R, r))) walk(std::false_type{});
-            else walk(std::true_type{});
-        } else
-        for (int it = 0; it < MAX_DDA_STEPS; it++) {
-            float s;
-            if (Walk<SEM>::sample(R, ox, oy, oz, r, s)) {
-                const uint32_t key = brick_code_of(r.vx, r.vy, r.vz);
-                if (key != cur) {  // the ray's next pair, in k_count's order
-                    cur = key;
-                    resolve(k < maxp ? pc[k] : NO_PAIR, pos, lpos, cnt);
-                    k++;
-                    w = 0;
-                }
-                if (w < cnt) {
-                    const uint32_t l = ((r.vz & 7) << 6) | ((r.vy & 7) << 3) | (r.vx & 7);
-                    if (lpos != NO_PAIR && lpos + w < (uint32_t)PLC_STAGE) {
-                        st_s[lpos + w] = s;
-                        st_l[lpos + w] = (uint16_t)l;
-                        if constexpr (SEM == 3) st_w[lpos + w] = vb_weight(R, r.w0, s);
-                    } else if (pos != NO_PAIR && pos + w < Wk.max_smp) {
-                        Wk.smp[pos + w] = make_uint2(__float_as_uint(s), (t << 9) | l);
-                        if constexpr (SEM == 3) Wk.smw[pos + w] = vb_weight(R, r.w0, s);
+        };
+        if (__all(Walk<SEM>::inside(R, r))) walk(std::false_type{});
+        else walk(std::true_type{});
+    };
+#ifdef TSDF_ABLATE_PL_NOWALK
+    if (ok && r.px == 1e30f) {
+#else
+    if (ok) {
+#endif
+        if (late) {
+            walk_short(std::true_type{}, std::false_type{});
+        } else {
+            uint32_t cur = ~0u;  // brick code of the current pair
+            uint32_t k = 0, pos = NO_PAIR, lpos = NO_PAIR, cnt = 0, w = 0;
+            for (int it = 0; it < MAX_DDA_STEPS; it++) {
+                float s;
+                if (Walk<SEM>::sample(R, ox, oy, oz, r, s)) {
+                    const uint32_t key = brick_code_of(r.vx, r.vy, r.vz);
+                    if (key != cur) {  // the ray's next pair, in k_count's order
+                        cur = key;
+                        resolve(k < maxp ? pc[k] : NO_PAIR, true, pos, lpos, cnt);
+                        k++;
+                        w = 0;
                     }
+                    if (w < cnt) {
+                        const uint32_t l = ((r.vz & 7) << 6) | ((r.vy & 7) << 3) | (r.vx & 7);
+                        if (lpos != NO_PAIR && lpos + w < (uint32_t)PLC_STAGE) {
+                            st_s[lpos + w] = s;
+                            st_l[lpos + w] = (uint16_t)l;
+                            if constexpr (SEM == 3) st_w[lpos + w] = vb_weight(R, r.w0, s);
+                        } else if (pos != NO_PAIR && pos + w < Wk.max_smp) {
+                            Wk.smp[pos + w] = make_uint2(__float_as_uint(s), (t << 9) | l);
+                            if constexpr (SEM == 3) Wk.smw[pos + w] = vb_weight(R, r.w0, s);
+                        }
+                    }
+                    w++;
                 }
-                w++;
+                if (!Walk<SEM>::step(r)) break;
             }
-            if (!Walk<SEM>::step(r)) break;
+        }
+    }
+    if (late) {
+        // the bases, now that the walk has covered the gather; then the second pass where needed
+        if (threadIdx.x < nruns) s_base[e0.w >> 16] = run_base(e0, cell0);
+        for (uint32_t j = threadIdx.x + PLC_THREADS; j < nruns; j += PLC_THREADS) {
+            const uint4 e = bt[j];
+            s_base[e.w >> 16] = run_base(e, e.x != NO_PAIR ? T.cell[(size_t)e.x * T.cell_stride + t] : 0u);
+        }
+        if (__syncthreads_or(ovf) && ovf) {
+            Walk<SEM>::init(R, D, t, px, py, pz, r);
+            walk_short(std::false_type{}, std::true_type{});
         }
     }
     __syncthreads();
@@ -1126,8 +1126,6 @@ __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) v
     // copy-out: one lane per staged sample; its run = the last run start at or before it
 #ifdef TSDF_ABLATE_PL_NOCOPY
     const uint32_t nst = 0;
-#elif defined(TSDF_NO_PLAN)
-    const uint32_t nst = s_nst;
 #else
     const uint32_t nst = plan_nst;
 #endif
