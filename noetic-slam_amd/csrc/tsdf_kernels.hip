@@ -1118,8 +1118,9 @@ __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) v
             Walk<SEM>::init(R, D, t, px, py, pz, r);
             walk_short(std::false_type{}, std::true_type{});
         }
+    } else {
+        __syncthreads();  // (late: the barrier above already published the staging and the bases)
     }
-    __syncthreads();
 #ifdef TSDF_PLC_PHASE
     if (threadIdx.x == 0) pt[4] = clock64();
 #endif
