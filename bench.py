@@ -308,7 +308,12 @@ def main():
         from tsdf_map.distributed import border_reduce
         dist.barrier()
         tm = time.perf_counter()
-        merge_info = border_reduce(vol, comm_device=cdev)
+        try:
+            merge_info = border_reduce(vol, comm_device=cdev)
+        except Exception as e:  # a read-out failure is reported in the line, not lost with it
+            merge_info = {"error": "%s: %s" % (type(e).__name__, e)}
+            print("border_reduce failed on rank %d: %s" % (rank, merge_info["error"]),
+                  file=sys.stderr)
         dist.barrier()
         merge_ms = (time.perf_counter() - tm) * 1e3
 
