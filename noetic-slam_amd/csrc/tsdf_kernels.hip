@@ -87,6 +87,25 @@ __device__ __forceinline__ int lds_insert(unsigned long long* s_key, uint64_t ke
     return -1;
 }
 
+// A workgroup-wide OR in one barrier: each wave publishes its vote in its own LDS slot
+// (__syncthreads_or takes three barriers: store, atomic OR, load).  Every lane of the workgroup
+// must call it; the slots may be reused after the next barrier.
+template <int NT>
+__device__ __forceinline__ bool block_any(bool p, uint32_t* s_vote) {
+#ifdef TSDF_SYNC_OR
+    (void)s_vote;
+    return __syncthreads_or(p);
+#else
+    const uint32_t w = __any(p) ? 1u : 0u;
+    if ((threadIdx.x & 63) == 0) s_vote[threadIdx.x >> 6] = w;
+    __syncthreads();
+    uint32_t r = 0;
+#pragma unroll
+    for (int k = 0; k < NT / 64; k++) r |= s_vote[k];
+    return r != 0;
+#endif
+}
+
 // ------------------------------------------------------------------------------------------------
 // k_count
 
@@ -866,6 +885,7 @@ __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) v
     __shared__ float st_s[PLC_STAGE];      // staged samples
     __shared__ uint16_t st_l[PLC_STAGE];
     __shared__ float st_w[SEM == 3 ? PLC_STAGE : 1];  // Voxblox 1/z^2: the samples' weights
+    __shared__ uint32_t s_vote[2][PLC_THREADS / 64];  // block_any: sector test, second pass
 #ifdef TSDF_ABLATE_PL_EMPTY
     __shared__ uint32_t s_nst;             // staged samples (end of the last staged run)
 #endif
@@ -927,7 +947,7 @@ __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) v
     typename Walk<SEM>::State r;
     const bool ok = i < r1 && Walk<SEM>::init(R, D, t, px, py, pz, r);
     // sector sharding: a half block without a ray of this GPU's sector has no samples to place
-    if (R.sec_on && !__syncthreads_or(ok)) return;
+    if (R.sec_on && !block_any<PLC_THREADS>(ok, s_vote[0])) return;
     if (threadIdx.x < (uint32_t)PLC_WORDS) s_bits[threadIdx.x] = plan_bits;
     if (threadIdx.x < (uint32_t)((PLC_WORDS + 1) / 2))
         reinterpret_cast<uint32_t*>(s_wpre)[threadIdx.x] = plan_pre;
@@ -1114,7 +1134,7 @@ __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) v
             const uint4 e = bt[j];
             s_base[e.w >> 16] = run_base(e, e.x != NO_PAIR ? T.cell[(size_t)e.x * T.cell_stride + t] : 0u);
         }
-        if (__syncthreads_or(ovf) && ovf) {
+        if (block_any<PLC_THREADS>(ovf, s_vote[1]) && ovf) {
             Walk<SEM>::init(R, D, t, px, py, pz, r);
             walk_short(std::false_type{}, std::true_type{});
         }
