@@ -1067,8 +1067,9 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
     c->R.bg = p->semantics == TSDF_SEM_VOXBLOX ? 0.0f : c->R.tau;
     c->R.tau_m_vs = c->R.tau - c->R.vs;
     sector_bounds(p->sector_yaw0, p->sector, p->n_sectors, c->R);
-    c->R.vs_d = (double)c->R.vs;  // VDBVolume keeps voxel_size as float
-    c->R.inv_s_d = 1.0 / c->R.vs_d;
+    const double vs_d = (double)c->R.vs;  // VDBVolume keeps voxel_size as float
+    c->R.hvs_d = vs_d * 0.5;               // exact
+    c->R.inv_s_d = 1.0 / vs_d;
     c->R.gate_d2 = gate_threshold(c->R.tau);
     {
         const double band = p->space_carving ? (p->max_range + p->sdf_trunc) / p->voxel_size

@@ -106,9 +106,11 @@ struct RayConst {
     // [sec_lo, sec_hi), or outside [sec_hi, sec_lo) when the sector wraps past 4 (sec_wrap)
     int sec_on, sec_wrap;
     float sec_lo, sec_hi;
-    // TSDF_SEM_VDBFUSION_F64: vs and 1/vs in double, and the gate's threshold on
-    // the squared distance behind the hit: (float)sqrt(d2) < tau  <=>  d2 < gate_d2
-    double vs_d, inv_s_d, gate_d2;
+    // TSDF_SEM_VDBFUSION_F64: vs / 2 and 1/vs in double, and the gate's threshold
+    // on the squared distance behind the hit: (float)sqrt(d2) < tau  <=>  d2 < gate_d2.  vs / 2 is
+    // GetVoxelCenter's half voxel, precomputed so the walk reads it as a scalar kernel argument
+    // (formed per voxel it cost a double multiply and two readfirstlanes at every DDA step)
+    double hvs_d, inv_s_d, gate_d2;
     // Voxblox 1/z^2 sample weights (tsdf_params.depth_weight; sem 3 internally, with per-sample
     // weights in Work::smw)
     int depth_w;

@@ -562,7 +562,7 @@ __device__ __forceinline__ void vdb_geom(const RayConst& R, const VdbState& r, d
     // the point's double conversions stay per voxel (hoisted they would hold 6 VGPRs)
     float px = r.px, py = r.py, pz = r.pz;
     asm volatile("" : "+v"(px), "+v"(py), "+v"(pz));
-    vdb_geom_at(uniform_f64(R.vs_d * 0.5), r.oxd, r.oyd, r.ozd, px, py, pz, r.vx, r.vy, r.vz, proj,
+    vdb_geom_at(R.hvs_d, r.oxd, r.oyd, r.ozd, px, py, pz, r.vx, r.vy, r.vz, proj,
                 d2);
 }
 
