@@ -559,9 +559,12 @@ __device__ __forceinline__ void vdb_geom_at(double hv, double ox, double oy, dou
 
 __device__ __forceinline__ void vdb_geom(const RayConst& R, const VdbState& r, double& proj,
                                          double& d2) {
-    // the point's double conversions stay per voxel (hoisted they would hold 6 VGPRs)
+    // the point's double conversions are loop-invariant: the compiler hoists them out of the walk
+    // (4 more VGPRs in k_place, whose occupancy LDS sets; 3 double conversions less per DDA step)
     float px = r.px, py = r.py, pz = r.pz;
+#ifdef TSDF_F64_PER_VOXEL_P
     asm volatile("" : "+v"(px), "+v"(py), "+v"(pz));
+#endif
     vdb_geom_at(R.hvs_d, r.oxd, r.oyd, r.ozd, px, py, pz, r.vx, r.vy, r.vz, proj,
                 d2);
 }
