@@ -1017,7 +1017,7 @@ __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) v
     //   pass 1 (after the bases; only those lanes): the ray walks again and stores the others.
     // Without `late` one pass does both, with the bases from the prologue.
     bool ovf = false;
-    auto walk_short = [&](auto stage_c, auto direct_c) {
+    auto walk_short = [&](auto stage_c, auto direct_c, typename Walk<SEM>::State& rs) {
         constexpr bool STAGE = decltype(stage_c)::value, DIRECT = decltype(direct_c)::value;
         constexpr bool WITH_POS = DIRECT;
         uint4 code = make_uint4(NO_PAIR, NO_PAIR, NO_PAIR, NO_PAIR);
@@ -1048,8 +1048,8 @@ __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) v
         auto walk = [&](auto chk) {
             for (int it = 0; it < MAX_DDA_STEPS; it++) {
                 float s;
-                const bool g = Walk<SEM>::sample_sel(R, ox, oy, oz, r, s, decltype(chk)::value);
-                const uint32_t key = brick_code_of(r.vx, r.vy, r.vz);
+                const bool g = Walk<SEM>::sample_sel(R, ox, oy, oz, rs, s, decltype(chk)::value);
+                const uint32_t key = brick_code_of(rs.vx, rs.vy, rs.vz);
                 const bool nb = g && key != cur;  // the ray's next pair, in k_count's order
                 cur = nb ? key : cur;
                 // take the head of the ray's pair queue and shift the queue: plain selects (a
@@ -1067,27 +1067,27 @@ __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) v
                 w = nb ? 0u : w;
                 const uint32_t lpos = lq & 0xFFFFu, cnt = lq >> 16;
                 const bool st = g && w < cnt;
-                const uint32_t l = ((r.vz & 7) << 6) | ((r.vy & 7) << 3) | (r.vx & 7);
+                const uint32_t l = ((rs.vz & 7) << 6) | ((rs.vy & 7) << 3) | (rs.vx & 7);
                 const bool staged = lpos + w < (uint32_t)PLC_STAGE;
                 if (STAGE && st && staged) {
                     st_s[lpos + w] = s;
                     st_l[lpos + w] = (uint16_t)l;
-                    if constexpr (SEM == 3) st_w[lpos + w] = vb_weight(R, r.w0, s);
+                    if constexpr (SEM == 3) st_w[lpos + w] = vb_weight(R, rs.w0, s);
                 } else if (st && !staged) {
                     if constexpr (DIRECT) {
                         if (pos != NO_PAIR && pos + w < Wk.max_smp) {
                             Wk.smp[pos + w] = make_uint2(__float_as_uint(s), (t << 9) | l);
-                            if constexpr (SEM == 3) Wk.smw[pos + w] = vb_weight(R, r.w0, s);
+                            if constexpr (SEM == 3) Wk.smw[pos + w] = vb_weight(R, rs.w0, s);
                         }
                     } else {
                         ovf = true;
                     }
                 }
                 w += g ? 1u : 0u;
-                if (!Walk<SEM>::step(r)) break;
+                if (!Walk<SEM>::step(rs)) break;
             }
         };
-        if (__all(Walk<SEM>::inside(R, r))) walk(std::false_type{});
+        if (__all(Walk<SEM>::inside(R, rs))) walk(std::false_type{});
         else walk(std::true_type{});
     };
 #ifdef TSDF_ABLATE_PL_NOWALK
@@ -1096,7 +1096,7 @@ __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) v
     if (ok) {
 #endif
         if (late) {
-            walk_short(std::true_type{}, std::false_type{});
+            walk_short(std::true_type{}, std::false_type{}, r);
         } else {
             uint32_t cur = ~0u;  // brick code of the current pair
             uint32_t k = 0, pos = NO_PAIR, lpos = NO_PAIR, cnt = 0, w = 0;
@@ -1135,8 +1135,11 @@ __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) v
             s_base[e.w >> 16] = run_base(e, e.x != NO_PAIR ? T.cell[(size_t)e.x * T.cell_stride + t] : 0u);
         }
         if (block_any<PLC_THREADS>(ovf, s_vote[1]) && ovf) {
-            Walk<SEM>::init(R, D, t, px, py, pz, r);
-            walk_short(std::false_type{}, std::true_type{});
+            // a fresh state: the first pass's is dead after its loop (kept, it would be carried
+            // out of that loop and cost register copies at every step)
+            typename Walk<SEM>::State r2;
+            Walk<SEM>::init(R, D, t, px, py, pz, r2);
+            walk_short(std::false_type{}, std::true_type{}, r2);
         }
     } else {
         __syncthreads();  // (late: the barrier above already published the staging and the bases)
