@@ -1050,6 +1050,10 @@ __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) v
                 float s;
                 const bool g = Walk<SEM>::sample_sel(R, ox, oy, oz, rs, s, decltype(chk)::value);
                 const uint32_t key = brick_code_of(rs.vx, rs.vy, rs.vz);
+                const uint32_t l = ((rs.vz & 7) << 6) | ((rs.vy & 7) << 3) | (rs.vx & 7);
+                // the next DDA step now, in the same basic block as the sample's double chain
+                // (after the staging branch the scheduler could not overlap the two)
+                const bool adv = Walk<SEM>::step_sel(rs);
                 const bool nb = g && key != cur;  // the ray's next pair, in k_count's order
                 cur = nb ? key : cur;
                 // take the head of the ray's pair queue and shift the queue: plain selects (a
@@ -1067,7 +1071,6 @@ __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) v
                 w = nb ? 0u : w;
                 const uint32_t lpos = lq & 0xFFFFu, cnt = lq >> 16;
                 const bool st = g && w < cnt;
-                const uint32_t l = ((rs.vz & 7) << 6) | ((rs.vy & 7) << 3) | (rs.vx & 7);
                 const bool staged = lpos + w < (uint32_t)PLC_STAGE;
                 if (STAGE && st && staged) {
                     st_s[lpos + w] = s;
@@ -1084,7 +1087,7 @@ __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) v
                     }
                 }
                 w += g ? 1u : 0u;
-                if (!Walk<SEM>::step(rs)) break;
+                if (!adv) break;
             }
         };
         if (__all(Walk<SEM>::inside(R, rs))) walk(std::false_type{});
