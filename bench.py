@@ -50,7 +50,11 @@ def parse():
                     help="also time the oracle on this many threads (0: off; the box's rules size "
                          "worker pools to one GPU's 16-core share, so the whole host is projected, "
                          "not run)")
-    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true",
+                    help="skip the CPU baseline and the parity check (both use the CPU oracle)")
+    ap.add_argument("--parity-steps", type=int, default=2,
+                    help="timed steps re-integrated by a fresh context and compared bit for bit "
+                         "with the CPU oracle after the timed region (0: off)")
     ap.add_argument("--pipeline", type=int, nargs="?", const=1, default=2, choices=(0, 1, 2),
                     help="tsdf_params.pipeline: 2 (default) overlaps batch b+1's k_count / "
                          "k_compact with batch b's k_integrate on a second HIP stream, k_place "
@@ -118,6 +122,49 @@ def launch_ranks(n, script=None, argv=None):
     return rc
 
 
+def bench_parity(args, steps, make_volume):
+    """The driver-timed workload under parity: a fresh context with the bench's settings integrates
+    the first `parity_steps` timed steps (the same resident TorchOusterSim tensors, the same
+    tsdf_integrate_batch_device calls), and its field is compared bit for bit (touched voxels,
+    weights, sdf bits) with the CPU oracle's on the same scans and semantics."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle
+
+    t0 = time.perf_counter()
+    sel = list(range(args.warmup, min(len(steps), args.warmup + args.parity_steps)))
+    g = make_volume()
+    for i in sel:
+        x, offs, org = steps[i]
+        g.integrate_batch_device(x.data_ptr(), offs, org)
+    gi, gs, gw = g.export_voxels()
+    g.close()
+    share = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    threads = max(1, min(args.cpu_threads, share or 1))
+    ov = oracle.OracleTSDFVolume(args.voxel, args.trunc, semantics=args.semantics, threads=threads)
+    n_scans = 0
+    for i in sel:
+        x, offs, org = steps[i]
+        xs = x.cpu().numpy()
+        for j in range(len(org)):
+            ov.integrate(xs[offs[j]:offs[j + 1]], org[j])
+            n_scans += 1
+    oi, os_, ow = ov.export_voxels()
+    same_set = gi.shape == oi.shape and bool(np.array_equal(gi, oi))
+    w_eq = same_set and bool(np.array_equal(gw.view(np.uint32), ow.view(np.uint32)))
+    s_eq = same_set and bool(np.array_equal(gs.view(np.uint32), os_.view(np.uint32)))
+    out = {"scans": n_scans, "voxels": int(gi.shape[0]), "oracle_voxels": int(oi.shape[0]),
+           "bitwise": bool(same_set and w_eq and s_eq), "same_voxels": same_set,
+           "weights_equal": w_eq, "sdf_bits_equal": s_eq,
+           "settings": "fresh context, semantics %s, pipeline %d, %d-scan device batches" % (
+               args.semantics, args.pipeline, args.batch),
+           "oracle": "oracle/tsdf_oracle.c scan-fused, %d threads" % threads,
+           "seconds": round(time.perf_counter() - t0, 2)}
+    if same_set and not (w_eq and s_eq):
+        out["sdf_mismatch_voxels"] = int(np.count_nonzero(gs.view(np.uint32) != os_.view(np.uint32)))
+        out["max_abs_dsdf"] = float(np.max(np.abs(gs - os_)))
+    return out
+
+
 def check_world(n_gpus, world):
     """The printed line's n_gpus must be the ranks that actually ran."""
     if n_gpus != world:
@@ -175,14 +222,17 @@ def main():
     t_gen = time.time() - t_gen
     max_pts = max(int(np.diff(o).max()) for _, o, _ in steps)
 
-    vol = HipTSDFVolume(args.voxel, args.trunc, max_points=max(max_pts, 1 << 17),
-                        max_bricks=args.max_bricks, device_id=local,
-                        max_batch=min(scans_per_step, 512),  # one launch per step (all shards)
-                        pipeline=args.pipeline, semantics=args.semantics,
-                        n_sectors=n_shards,  # this rank's azimuth sector of every scan
-                        sector=(args.rehearsal_sector % n_shards if world == 1 and n_shards > 1
-                                else rank),
-                        walk=args.walk)
+    def make_volume():
+        return HipTSDFVolume(args.voxel, args.trunc, max_points=max(max_pts, 1 << 17),
+                             max_bricks=args.max_bricks, device_id=local,
+                             max_batch=min(scans_per_step, 512),  # one launch per step (all shards)
+                             pipeline=args.pipeline, semantics=args.semantics,
+                             n_sectors=n_shards,  # this rank's azimuth sector of every scan
+                             sector=(args.rehearsal_sector % n_shards if world == 1 and n_shards > 1
+                                     else rank),
+                             walk=args.walk)
+
+    vol = make_volume()
 
     def run_step(i):
         x, offs, org = steps[i]
@@ -317,6 +367,13 @@ def main():
         dist.barrier()
         merge_ms = (time.perf_counter() - tm) * 1e3
 
+    # ---- parity of the timed workload: the first timed steps, integrated by a fresh context with
+    # the bench's exact settings (semantics, pipeline, batch size, device batch API), against the
+    # CPU oracle on the same scans (rank 0, N=1; after the timed region, never inside it) ---------
+    parity = None
+    if rank == 0 and world == 1 and n_shards == 1 and not args.no_cpu and args.parity_steps > 0:
+        parity = bench_parity(args, steps, make_volume)
+
     # ---- CPU baseline: the oracle on a bounded sample of the same workload (rank 0, N=1) --------
     # Two legs: the partitioned multi-threaded oracle on the box's CPU share (the
     # reported value) and the serial oracle (VDBFusion's serial Integrate loop), same scans.
@@ -404,6 +461,7 @@ def main():
                        "front_end": ("single walk (k_walk + k_spans)" if "walk" in kernel_ms_per_launch
                                      else "two walks (k_count + k_place)")},
             "roofline": roofline,
+            "parity": parity,
             "cpu_baseline": cpu,
             "path_ms_per_scan": round(path_ms_per_scan, 5),
             "kernel_ms_per_launch": {k: round(v, 5) for k, v in kernel_ms_per_launch.items()},

@@ -86,8 +86,9 @@ typedef struct tsdf_params {
                               another, so per-kernel timings (tsdf_stats.kernel_ms) are not shared
                               with another batch */
     /* ABI v3: backend semantics */
-    int32_t semantics;          /* TSDF_SEM_VDBFUSION (default), TSDF_SEM_VOXBLOX or
-                                   TSDF_SEM_VDBFUSION_F64 */
+    int32_t semantics;          /* TSDF_SEM_VDBFUSION_F64 (default since ABI v8: the mode that
+                                   matches VDBFusion's touched voxels and weights exactly),
+                                   TSDF_SEM_VDBFUSION (fp32 restatement) or TSDF_SEM_VOXBLOX */
     int32_t allow_clear;        /* Voxblox allow_clear: a ray longer than max_range becomes a
                                    clearing ray of length min(max(d - tau, 0), max_range) (default 1) */
     int32_t use_weight_dropoff; /* Voxblox use_weight_dropoff: w *= (tau + sdf) / (tau - voxel_size)
@@ -119,10 +120,16 @@ typedef struct tsdf_params {
     /* ABI v6: Voxblox's sample weight (TSDF_SEM_VOXBLOX only).  1 (tsdf_default_params; voxblox
      * TsdfIntegratorBase::Config use_const_weight = false, upstream's default): w = 1 / z^2, z the
      * point's depth along the sensor's z axis (|z| <= 1e-6: w = 0), the axis taken from the scan's
-     * pose (tsdf_integrate_pose; the plain integrate calls use the world z axis, an identity
-     * rotation); then the dropoff.  0: w = 1 (use_const_weight = true). */
+     * pose (tsdf_integrate_pose and the *_pose batch calls); then the dropoff.  Since ABI v8 the
+     * per-sample weight is capped at min(max_weight, TSDF_W0_CAP) (without a cap a point near the
+     * sensor plane, |z| ~ 1e-5, overflows the exact fixed-point sums), and scans given as a bare
+     * origin (tsdf_integrate, tsdf_integrate_device, tsdf_integrate_batch_device) carry no
+     * orientation and take w = 1.  0: w = 1 (use_const_weight = true). */
     int32_t depth_weight;
 } tsdf_params;
+
+/* cap of one sample's 1/z^2 weight (with max_weight, whichever is lower; ABI v8) */
+#define TSDF_W0_CAP 65536.0f
 
 #define TSDF_WALK_TWO 0
 #define TSDF_WALK_SINGLE 1

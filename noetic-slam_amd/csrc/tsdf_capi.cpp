@@ -976,7 +976,7 @@ void tsdf_default_params(tsdf_params* p) {
     p->device_id = 0;
     p->brick_side = TSDF_BRICK_SIDE;
     p->max_batch = 32;
-    p->semantics = TSDF_SEM_VDBFUSION;
+    p->semantics = TSDF_SEM_VDBFUSION_F64;  // ABI v8: the mode matching VDBFusion exactly
     p->allow_clear = 1;  // voxblox TsdfIntegratorBase::Config defaults
     p->use_weight_dropoff = 1;
     p->max_weight = 10000.0f;
@@ -1064,6 +1064,7 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
     c->R.allow_clear = p->allow_clear ? 1 : 0;
     c->R.dropoff = p->use_weight_dropoff ? 1 : 0;
     c->R.max_weight = p->max_weight;
+    c->R.w0_cap = p->max_weight > 0.0f && p->max_weight < TSDF_W0_CAP ? p->max_weight : TSDF_W0_CAP;
     c->R.bg = p->semantics == TSDF_SEM_VOXBLOX ? 0.0f : c->R.tau;
     c->R.tau_m_vs = c->R.tau - c->R.vs;
     sector_bounds(p->sector_yaw0, p->sector, p->n_sectors, c->R);
@@ -1257,8 +1258,10 @@ struct ScanPose {
     float z[3];
 };
 
+// An origin without an orientation: the zero axis tells the walk to use Voxblox's constant weight
+// (the 1/z^2 weight needs the sensor axis, which only the pose entry points carry)
 static ScanPose pose_of_origin(const double o[3]) {
-    return ScanPose{{o[0], o[1], o[2]}, {0.0f, 0.0f, 1.0f}};
+    return ScanPose{{o[0], o[1], o[2]}, {0.0f, 0.0f, 0.0f}};
 }
 
 // pose = (x, y, z, qx, qy, qz, qw): the z axis is the third column of the rotation of the

@@ -114,6 +114,7 @@ struct RayConst {
     // Voxblox 1/z^2 sample weights (tsdf_params.depth_weight; sem 3 internally, with per-sample
     // weights in Work::smw)
     int depth_w;
+    float w0_cap;  // cap of a sample's 1/z^2 weight: min(max_weight, 2^16) (TSDF_W0_CAP)
 };
 
 // fp32 pseudo-angle of (x, y) in [0, 4), monotone in atan2 (include/tsdf_hip.h tsdf_sector_of):

@@ -255,11 +255,17 @@ __device__ __forceinline__ bool vb_init(const RayConst& R, const BatchRef& D, ui
     vb_axis(sz * R.inv_vs, ez * R.inv_vs, r.vz, r.sz, r.tnz, r.tdz, steps);
     r.rem = min(steps, MAX_DDA_STEPS - 1);
     // TsdfIntegratorBase::getVoxelWeight: 1 / z^2 of the point's sensor-frame depth z (the scan's
-    // z axis dotted with p - o, Eigen's x + (y + z)); |z| <= kEpsilon (1e-6) gives 0
+    // z axis dotted with p - o, Eigen's x + (y + z)); |z| <= kEpsilon (1e-6) gives 0.  The weight
+    // is capped at R.w0_cap = min(max_weight, 2^16) so the int64 fixed-point sums cannot overflow
+    // (upstream's per-update max_weight cap bounds the fused weight the same way).  A scan without
+    // an orientation (origin-only entry points: zero axis) takes the constant weight 1.
     r.w0 = 1.0f;
     if (R.depth_w) {
-        const float z = fabsf(D.s[t].zx * dx + (D.s[t].zy * dy + D.s[t].zz * dz));
-        r.w0 = z > 1e-6f ? 1.0f / (z * z) : 0.0f;
+        const float zx = D.s[t].zx, zy = D.s[t].zy, zz = D.s[t].zz;
+        if (zx != 0.0f || zy != 0.0f || zz != 0.0f) {
+            const float z = fabsf(zx * dx + (zy * dy + zz * dz));
+            r.w0 = z > 1e-6f ? fminf(1.0f / (z * z), R.w0_cap) : 0.0f;
+        }
     }
     r.px = px;
     r.dx = dx;

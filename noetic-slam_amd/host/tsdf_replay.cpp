@@ -18,7 +18,7 @@
 // n_bricks * 512 f32 w.
 //
 // usage: tsdf_replay <in.scans> <out.bricks> [voxel_size sdf_trunc [semantics [max_batch]]]
-//   semantics: vdbfusion (default), vdbfusion_f64, voxblox (1/z^2 weight, upstream's default) or
+//   semantics: vdbfusion_f64 (the ABI default), vdbfusion (fp32), voxblox (1/z^2 weight, upstream's default) or
 //   voxblox_const (use_const_weight); max_batch: scans per GPU batch (the node's ~max_batch).
 // The time from the first integrate to the end of tsdf_sync is printed as the node-path rate.
 #include <chrono>
@@ -72,6 +72,7 @@ int main(int argc, char** argv) {
         if (sem == "voxblox" || sem == "voxblox_const") p.semantics = TSDF_SEM_VOXBLOX;
         if (sem == "voxblox_const") p.depth_weight = 0;
         if (sem == "vdbfusion_f64") p.semantics = TSDF_SEM_VDBFUSION_F64;
+        if (sem == "vdbfusion") p.semantics = TSDF_SEM_VDBFUSION;
     }
     if (argc >= 7) p.max_batch = (uint32_t)std::atoi(argv[6]);
     File in(argv[1], "rb");

@@ -85,7 +85,9 @@ class TsdfMapNode {
             p.depth_weight = const_w ? 0 : 1;
         } else if (sem == "vdbfusion_f64") {  // upstream's precisions
             p.semantics = TSDF_SEM_VDBFUSION_F64;
-        } else if (sem != "vdbfusion") {  // the fp32 restatement
+        } else if (sem == "vdbfusion") {  // the fp32 restatement
+            p.semantics = TSDF_SEM_VDBFUSION;
+        } else {
             ROS_FATAL("unknown semantics '%s' (vdbfusion_f64, vdbfusion, voxblox)", sem.c_str());
             ros::shutdown();
             return;

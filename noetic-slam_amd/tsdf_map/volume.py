@@ -104,9 +104,9 @@ class TSDFVolume:
     @staticmethod
     def make_params(lib, voxel_size, sdf_trunc, space_carving=False, min_range=0.0,
                     max_range=math.inf, max_bricks=1 << 20, max_points=1 << 18, device_id=0,
-                    max_batch=32, pipeline=False, semantics="vdbfusion", allow_clear=True,
+                    max_batch=32, pipeline=False, semantics="vdbfusion_f64", allow_clear=True,
                     use_weight_dropoff=True, max_weight=10000.0, n_sectors=0, sector=0,
-                    sector_yaw0=0.0, max_bricks_hard=0, walk="two", use_const_weight=True):
+                    sector_yaw0=0.0, max_bricks_hard=0, walk="two", use_const_weight=False):
         """tsdf_params from the VDBFusion / Voxblox-style keyword arguments."""
         if semantics not in _abi.SEMANTICS:
             raise ValueError("semantics must be one of %s" % sorted(_abi.SEMANTICS))

@@ -232,7 +232,7 @@ void tsdf_default_params(tsdf_params* p) {
     p->device_id = 0;
     p->brick_side = TSDF_BRICK_SIDE;
     p->max_batch = 32; /* accepted for ABI parity; the oracle integrates scan by scan */
-    p->semantics = TSDF_SEM_VDBFUSION;
+    p->semantics = TSDF_SEM_VDBFUSION_F64; /* ABI v8 default */
     p->allow_clear = 1;        /* voxblox TsdfIntegratorBase::Config defaults */
     p->use_weight_dropoff = 1;
     p->max_weight = 10000.0f;
@@ -258,7 +258,7 @@ int tsdf_create(const tsdf_params* params, tsdf_ctx** out) {
     c->inv_vs = 1.0f / c->vs;
     c->tau = (float)params->sdf_trunc;
     c->sem = params->semantics;
-    c->zax[0] = 0.0f; c->zax[1] = 0.0f; c->zax[2] = 1.0f;
+    c->zax[0] = 0.0f; c->zax[1] = 0.0f; c->zax[2] = 0.0f; /* no orientation: weight 1 */
     c->bg = c->sem == TSDF_SEM_VOXBLOX ? 0.0f : c->tau;
     c->mode = ORACLE_MODE_SCAN_FUSED;
     {
@@ -512,9 +512,13 @@ static int64_t walk_ray_vb(tsdf_ctx* c, float px, float py, float pz, float ox, 
     /* TsdfIntegratorBase::getVoxelWeight: use_const_weight -> 1; else 1 / z^2 of the point's
      * sensor-frame depth z = zaxis . (p - o) (Eigen's x + (y + z)), 0 for |z| <= kEpsilon 1e-6 */
     float w0 = 1.0f;
-    if (c->p.depth_weight) {
+    if (c->p.depth_weight && (c->zax[0] != 0.0f || c->zax[1] != 0.0f || c->zax[2] != 0.0f)) {
+        /* capped at min(max_weight, 2^16): the int64 fixed-point sums cannot overflow (the GPU
+         * library's RayConst::w0_cap); an origin-only scan (zero axis) keeps the weight 1 */
+        const float cap = c->p.max_weight > 0.0f && c->p.max_weight < TSDF_W0_CAP
+                              ? c->p.max_weight : TSDF_W0_CAP;
         const float z = fabsf(c->zax[0] * dx + (c->zax[1] * dy + c->zax[2] * dz));
-        w0 = z > 1e-6f ? 1.0f / (z * z) : 0.0f;
+        w0 = z > 1e-6f ? fminf(1.0f / (z * z), cap) : 0.0f;
     }
     float ex, ey, ez, sx, sy, sz;
     if (clearing) {
@@ -808,7 +812,7 @@ static int integrate_scan(tsdf_ctx* c, const void* pts, uint64_t n, uint32_t poi
 int tsdf_integrate(tsdf_ctx* c, const void* pts, uint64_t n, uint32_t point_step,
                    uint32_t xyz_offset, int32_t xyz_is_f64, const double origin[3]) {
     if (!c) return TSDF_EINVAL;
-    c->zax[0] = 0.0f; c->zax[1] = 0.0f; c->zax[2] = 1.0f;
+    c->zax[0] = 0.0f; c->zax[1] = 0.0f; c->zax[2] = 0.0f; /* no orientation: weight 1 */
     return integrate_scan(c, pts, n, point_step, xyz_offset, xyz_is_f64, origin);
 }
 

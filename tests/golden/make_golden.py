@@ -22,6 +22,7 @@ sys.path.insert(0, os.path.join(REPO, "oracle"))
 
 SCANS = (0, 1, 40)
 DECIMATE = 16
+SEMANTICS = "vdbfusion"  # the fp32 restatement (the golden file predates the ABI v8 default)
 VS, TAU = 0.05, 0.15
 
 
@@ -43,7 +44,7 @@ def main():
         pts.append(np.ascontiguousarray(p[::DECIMATE]))
         org.append(o)
     offs = np.cumsum([0] + [p.shape[0] for p in pts]).astype(np.int64)
-    v = oracle.OracleTSDFVolume(VS, TAU)
+    v = oracle.OracleTSDFVolume(VS, TAU, semantics=SEMANTICS)
     for p, o in zip(pts, org):
         v.integrate(p, o)
     ijk, s, w = v.export_voxels()

@@ -15,10 +15,15 @@ def _make_golden():
     return make_golden
 
 
+def make_golden_semantics():
+    return _make_golden().SEMANTICS
+
+
 def test_oracle_reproduces_golden():
     digest = _make_golden().digest
     z = np.load(os.path.join(GOLDEN, "golden_c1_decimated.npz"), allow_pickle=False)
-    v = oracle.OracleTSDFVolume(float(z["voxel_size"]), float(z["sdf_trunc"]))
+    v = oracle.OracleTSDFVolume(float(z["voxel_size"]), float(z["sdf_trunc"]),
+                                semantics=make_golden_semantics())
     offs = z["scan_offsets"]
     for s in range(len(offs) - 1):
         v.integrate(z["points"][offs[s]:offs[s + 1]], z["origins"][s])

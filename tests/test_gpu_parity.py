@@ -18,12 +18,31 @@ pytestmark = pytest.mark.gpu
 VS, TAU = 0.05, 0.15
 
 
+# Every case runs in both VDBFusion modes: the ABI default vdbfusion_f64 (upstream's precisions,
+# the bench's mode) and the fp32 restatement; a case that names its semantics keeps them.
+_SEM = {"default": "vdbfusion_f64"}
+
+
+def pytest_generate_tests(metafunc):
+    if "semantics" not in metafunc.fixturenames:
+        metafunc.parametrize("vdb_mode", ["vdbfusion_f64", "vdbfusion"], indirect=True)
+
+
+@pytest.fixture(autouse=True)
+def vdb_mode(request):
+    _SEM["default"] = getattr(request, "param", "vdbfusion_f64")
+    yield _SEM["default"]
+    _SEM["default"] = "vdbfusion_f64"
+
+
 def hip(**kw):
     from tsdf_map import HipTSDFVolume
+    kw.setdefault("semantics", _SEM["default"])
     return HipTSDFVolume(kw.pop("voxel_size", VS), kw.pop("sdf_trunc", TAU), **kw)
 
 
 def ora(**kw):
+    kw.setdefault("semantics", _SEM["default"])
     return oracle.OracleTSDFVolume(kw.pop("voxel_size", VS), kw.pop("sdf_trunc", TAU), **kw)
 
 
@@ -183,7 +202,7 @@ def test_golden_fixture(tmp_path):
     from conftest import GOLDEN
     import os
     z = np.load(os.path.join(GOLDEN, "golden_c1_decimated.npz"), allow_pickle=False)
-    g = hip(voxel_size=float(z["voxel_size"]), sdf_trunc=float(z["sdf_trunc"]))
+    g = hip(voxel_size=float(z["voxel_size"]), sdf_trunc=float(z["sdf_trunc"]), semantics="vdbfusion")
     offs = z["scan_offsets"]
     for s in range(len(offs) - 1):
         g.integrate(z["points"][offs[s]:offs[s + 1]], z["origins"][s])

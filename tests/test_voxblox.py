@@ -155,11 +155,19 @@ def test_sequential_vs_scan_fused_reported(sim):
     assert np.quantile(d, 0.999) <= 0.1 * TAU
 
 
-def test_vdbfusion_default_unchanged():
+def test_default_params():
+    """ABI v8 defaults: VDBFusion at upstream's precisions (the conforming mode), Voxblox's
+    config defaults (1/z^2 weight, dropoff, clearing, max_weight 1e4); the Python facade agrees."""
     from tsdf_map import _abi
-    p = _abi.default_params(oracle.load())
-    assert p.semantics == _abi.SEM_VDBFUSION and p.allow_clear == 1 and p.use_weight_dropoff == 1
-    assert p.max_weight == 10000.0
+    from tsdf_map.volume import TSDFVolume
+    lib = oracle.load()
+    p = _abi.default_params(lib)
+    assert p.semantics == _abi.SEM_VDBFUSION_F64 and p.allow_clear == 1 and p.use_weight_dropoff == 1
+    assert p.max_weight == 10000.0 and p.depth_weight == 1
+    q = TSDFVolume.make_params(lib, 0.05, 0.15)
+    for f in ("semantics", "allow_clear", "use_weight_dropoff", "max_weight", "depth_weight",
+              "pipeline", "space_carving"):
+        assert getattr(p, f) == getattr(q, f), f
 
 
 # -- GPU: bit-exact against the oracle's scan-fused Voxblox mode ---------------------------------
@@ -255,13 +263,44 @@ def test_depth_weight_is_inverse_z_squared(pitch):
     assert np.all(c.export_voxels()[2] == 1.0)
 
 
+IDENT = [0.0, 0.0, 0.0, 1.0]  # identity orientation (qx, qy, qz, qw): the sensor z axis = world z
+
+
 def test_depth_weight_tiny_z_gives_zero_weight():
     """|z| <= kEpsilon: weight 0, the samples are dropped (deviation 2)."""
     o = np.array([0.012, 0.013, 0.011])
     p = (o + [3.0, 0.4, 0.0]).astype(F)  # z = 0 along the world z axis
     vol = ora(use_const_weight=False)
-    vol.integrate(p[None], o)
+    vol.integrate(p[None], np.concatenate([o, IDENT]))
     assert vol.export_voxels()[0].shape[0] == 0
+
+
+def test_origin_only_scans_take_constant_weight():
+    """A bare origin carries no orientation: with the 1/z^2 weight on, such a scan fuses with
+    weight 1 (use_const_weight's field), not 1/(p.z - o.z)^2 of the world z axis (ABI v8)."""
+    o = np.array([0.012, 0.013, 0.011])
+    p = (o + [[3.0, 0.4, 0.0], [2.0, -1.0, 0.7]]).astype(F)
+    a = ora(use_const_weight=False)
+    a.integrate(p, o)
+    b = ora(use_const_weight=True)
+    b.integrate(p, o)
+    for x, y in zip(a.export_voxels(), b.export_voxels()):
+        assert np.array_equal(x, y)
+    assert a.export_voxels()[0].shape[0] > 0
+
+
+def test_depth_weight_is_capped():
+    """Points a hair off the sensor plane (|z| ~ 1e-5 m: 1/z^2 ~ 1e10) take the capped weight
+    min(max_weight, 2^16) per sample, so the exact int64 sums cannot overflow; the fused weight of
+    one such sample is the cap."""
+    o = np.array([0.0, 0.0, 0.0])
+    for mw, cap in ((10000.0, 10000.0), (1e9, 65536.0)):
+        pts = np.array([[3.0, 0.4, 1e-5], [3.0, 0.4, 2e-5]], F)
+        vol = ora(use_const_weight=False, use_weight_dropoff=False, max_weight=mw)
+        vol.integrate(pts[:1], np.concatenate([o, IDENT]))
+        ijk, s, w = vol.export_voxels()
+        assert ijk.shape[0] > 0 and np.all(w == np.float32(cap)), (mw, np.unique(w))
+        assert np.all(np.abs(s) <= 0.15 + 1e-6)
 
 
 def _posed_scans(sim, ks, decim):
