@@ -83,7 +83,7 @@ def parse():
                          "every ray walked once (k_walk + k_spans) when the band allows it")
     ap.add_argument("--no-profile", action="store_true",
                     help="do not record per-kernel HIP events in the timed region")
-    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_r03.json"),
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_r04.json"),
                     help="PMC-measured HBM bytes per launch (from a separate rocprofv3 --pmc run)")
     return ap.parse_args()
 
@@ -165,6 +165,54 @@ def bench_parity(args, steps, make_volume):
     return out
 
 
+def lib_sha16():
+    """First 16 hex digits of the sha256 of the loaded kernel library (the build the PMC traffic
+    file must have been measured on)."""
+    import hashlib
+    from tsdf_map._lib import HIP_LIB
+    p = os.environ.get("TSDF_HIP_LIB") or HIP_LIB
+    with open(p, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
+def read_traffic(path, kernel):
+    """roofline.traffic: PMC HBM bytes per launch of `kernel` from a separate rocprofv3 --pmc run
+    (profiles/collect_pmc.sh), only when that run measured THIS build of the library."""
+    try:
+        with open(path) as f:
+            tj = json.load(f)
+    except (OSError, ValueError):
+        return None, {"file": os.path.relpath(path, REPO), "error": "unreadable"}
+    cur = lib_sha16()
+    src = {"file": os.path.relpath(path, REPO), "lib_sha16": tj.get("lib_sha16"),
+           "this_build_sha16": cur, "matches_build": tj.get("lib_sha16") == cur}
+    if not src["matches_build"]:
+        return None, src  # stale: measured on another build of the kernels
+    return tj.get("bytes_per_launch", {}).get("k_" + kernel), src
+
+
+def serial_kernel_times(args, steps, make_volume):
+    """Every kernel's duration alone: a fresh context with pipeline 0 integrates the warmup steps,
+    then the timed steps with every launch of every kernel timed (dispatch timestamps).  Returns
+    ({kernel: mean ms per launch}, {kernel: launches})."""
+    v = make_volume(pipeline=0)
+    for i in range(args.warmup):
+        x, offs, org = steps[i]
+        v.integrate_batch_device(x.data_ptr(), offs, org)
+    v.sync()
+    v.reset_stats()
+    v.set_profiling(True)
+    for i in range(args.warmup, len(steps)):
+        x, offs, org = steps[i]
+        v.integrate_batch_device(x.data_ptr(), offs, org)
+    v.sync()
+    st = v.stats()
+    v.close()
+    n = st["kernel_launches"]
+    return ({k: st["kernel_ms"][k] / n[k] for k in st["kernel_ms"] if n[k] > 0},
+            {k: n[k] for k in n if n[k] > 0})
+
+
 def check_world(n_gpus, world):
     """The printed line's n_gpus must be the ranks that actually ran."""
     if n_gpus != world:
@@ -222,11 +270,12 @@ def main():
     t_gen = time.time() - t_gen
     max_pts = max(int(np.diff(o).max()) for _, o, _ in steps)
 
-    def make_volume():
+    def make_volume(pipeline=None):
         return HipTSDFVolume(args.voxel, args.trunc, max_points=max(max_pts, 1 << 17),
                              max_bricks=args.max_bricks, device_id=local,
                              max_batch=min(scans_per_step, 512),  # one launch per step (all shards)
-                             pipeline=args.pipeline, semantics=args.semantics,
+                             pipeline=args.pipeline if pipeline is None else pipeline,
+                             semantics=args.semantics,
                              n_sectors=n_shards,  # this rank's azimuth sector of every scan
                              sector=(args.rehearsal_sector % n_shards if world == 1 and n_shards > 1
                                      else rank),
@@ -238,38 +287,22 @@ def main():
         x, offs, org = steps[i]
         vol.integrate_batch_device(x.data_ptr(), offs, org)
 
-    # Kernel times: a timed launch records its dispatch timestamps, which costs the stream ~5 us.
-    # The warmup batches after the first time every kernel to find the dominant one; the timed
-    # region then times it on EVERY launch -- the roofline's avg_launch_ms -- and the others on
-    # every 8th batch (kernel_ms_per_launch).  Should a sampled kernel's mean come out higher, the
-    # roofline reports that kernel over its sampled launches (roofline.launches_timed says so).
+    # Kernel times.  The roofline kernel is ranked and timed ALONE: a serial leg
+    # (a fresh context with pipeline 0, the same steps; serial_kernel_times, after the timed
+    # region) times every kernel on every launch, where no kernel shares the GPU with another
+    # batch's.  The timed region itself samples every kernel on every 8th batch only (a timed
+    # launch costs the stream ~10 us): those are the pipelined durations (kernel_ms_per_launch),
+    # which under pipeline 1 / 2 include the other batch's kernels running beside them.
     for i in range(args.warmup):
-        if i == min(1, args.warmup - 1):  # rank on the warmup batches after the first (fresh map)
-            vol.sync()
-            vol.reset_stats()
-            if not args.no_profile:
-                vol.set_profiling(True)
         run_step(i)
     vol.sync()
     timing = None
-    # kernels whose launches never share the GPU with another batch's kernel: under --pipeline 2
-    # k_count and k_integrate of consecutive batches overlap each other (their event durations
-    # include the other), so the roofline's kernel is taken among the rest
-    alone = (("compact", "place", "walk", "spans") if args.pipeline == 2
-             else ("count", "compact", "place", "integrate", "walk", "spans"))
-    if not args.no_profile and args.warmup == 0:  # nothing to rank on: every kernel, every launch
+    if not args.no_profile:
         vol.set_profiling(True)
-        timing = {"every_launch": "all", "method": "dispatch timestamps (hipExtLaunchKernel "
-                                                   "start/stop events)"}
-    elif not args.no_profile:
-        wst = vol.stats()
-        wmean = {k: wst["kernel_ms"][k] / wst["kernel_launches"][k] for k in wst["kernel_ms"]
-                 if wst["kernel_launches"][k] > 0 and k in alone}
-        # the slowest kernel is timed on every launch (each timed launch costs the stream ~10 us)
-        every = [max(wmean, key=wmean.get)] if wmean else []
-        vol.set_profiling_period(every, PROFILE_PERIOD)
-        timing = {"every_launch": ["k_" + k for k in every], "others_every_nth_batch": PROFILE_PERIOD,
-                  "method": "dispatch timestamps (hipExtLaunchKernel start/stop events)"}
+        vol.set_profiling_period([], PROFILE_PERIOD)
+        timing = {"every_launch": [], "all_kernels_every_nth_batch": PROFILE_PERIOD,
+                  "method": "dispatch timestamps (hipExtLaunchKernel start/stop events)",
+                  "roofline_kernel_times": "serial leg (pipeline 0, every launch timed)"}
     vol.reset_stats()
 
     # ---- timed region ---------------------------------------------------------------------------
@@ -316,32 +349,27 @@ def main():
     roofline = None
     kernel_ms_per_launch = {k: (kms[k] / st["kernel_launches"][k]) for k in kms
                             if st["kernel_launches"][k] > 0}
-    kms = {k: kms[k] for k in kernel_ms_per_launch}
-    if not args.no_profile and sum(kms.values()) > 0:
-        cand = {k: v for k, v in kernel_ms_per_launch.items() if k in alone} or kernel_ms_per_launch
-        dom = max(cand, key=cand.get)
-        t_launch = kernel_ms_per_launch[dom] * 1e-3
+    serial = None
+    if not args.no_profile:
+        vol_serial_ms, serial_launches = serial_kernel_times(args, steps, make_volume)
+        serial = {k: round(v, 5) for k, v in vol_serial_ms.items()}
+        # the dominant kernel: the largest of the kernels' durations ALONE
+        dom = max(vol_serial_ms, key=vol_serial_ms.get)
+        t_launch = vol_serial_ms[dom] * 1e-3
         achieved = bytes_per_launch / t_launch / 1e9
-        traffic = None
-        if world == 1:  # the PMC profile is of the one-GPU workload (a rank's launch is smaller)
-            try:
-                with open(args.traffic_json) as f:
-                    traffic = json.load(f)["bytes_per_launch"].get("k_" + dom)
-            except (OSError, ValueError, KeyError):
-                traffic = None
+        traffic, traffic_src = read_traffic(args.traffic_json, dom) if world == 1 else (None, None)
         roofline = {"bound": "hbm", "kernel": "k_" + dom, "achieved": round(achieved, 2),
                     "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 5),
-                    "traffic": traffic,
+                    "traffic": traffic, "traffic_source": traffic_src,
                     "algorithmic_bytes_per_launch": round(bytes_per_launch),
                     "dedup_bytes_per_launch": round(dedup_bytes_per_launch),
                     "scans_per_launch": round(scans_per_launch, 2),
-                    "avg_launch_ms": round(kernel_ms_per_launch[dom], 5),
-                    "launches_timed": st["kernel_launches"][dom],
-                    "overlap": (None if args.pipeline == 0 else
-                                "pipeline 2: k_count and k_integrate of consecutive batches run "
-                                "beside each other (their durations include the overlap); the "
-                                "roofline kernel runs alone" if args.pipeline == 2 else
-                                "pipeline 1: every kernel may overlap the other batch's")}
+                    "avg_launch_ms": round(vol_serial_ms[dom], 5),
+                    "launches_timed": serial_launches[dom],
+                    "timed_in": "serial leg: a fresh context with pipeline 0 integrating the same "
+                                "warmup + timed steps, every launch of the timed steps timed, so "
+                                "every kernel's duration is its own (the headline runs pipeline %d)"
+                                % args.pipeline}
         # the whole path: the same algorithmic bytes over the step time (pipelined kernels overlap,
         # so their summed times would overstate it)
         path_ms = (sum(kernel_ms_per_launch.values()) if args.pipeline == 0
@@ -465,6 +493,7 @@ def main():
             "cpu_baseline": cpu,
             "path_ms_per_scan": round(path_ms_per_scan, 5),
             "kernel_ms_per_launch": {k: round(v, 5) for k, v in kernel_ms_per_launch.items()},
+            "serial_kernel_ms_per_launch": serial,
             "kernel_timing": timing,
             "uvox_per_scan": round(uvox_per_scan),
             "dirty_voxels_per_batch": round(st["n_dirty_total"] / n_batches),

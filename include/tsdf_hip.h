@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define TSDF_ABI_VERSION 7
+#define TSDF_ABI_VERSION 8
 #define TSDF_MAX_BATCH 512 /* scans per GPU batch (see tsdf_params.max_batch) */
 #define TSDF_BRICK_SIDE 8 /* voxels per brick edge: a brick is 8^3 = 512 voxels */
 
@@ -126,7 +126,29 @@ typedef struct tsdf_params {
      * origin (tsdf_integrate, tsdf_integrate_device, tsdf_integrate_batch_device) carry no
      * orientation and take w = 1.  0: w = 1 (use_const_weight = true). */
     int32_t depth_weight;
+    /* ABI v8: Voxblox's integrator (TSDF_SEM_VOXBLOX only; voxblox_ros TsdfServer `method`).
+     * TSDF_VB_SIMPLE (default): every point casts its own ray (SimpleTsdfIntegrator).
+     * TSDF_VB_MERGED: MergedTsdfIntegrator -- a scan's points are bundled by the voxel they fall in
+     * (getGridIndexFromPoint), each bundle's weighted mean point casts ONE ray carrying the summed
+     * point weights, and clearing points are bundled apart (one ray from each bundle's first
+     * point).  Bundles are formed in cloud order (voxblox integration_order_mode "sorted";
+     * DESIGN.md §2d states the deviations).  "fast" (FastTsdfIntegrator) is not offered: its ray
+     * early-exit depends on thread timing, so its field is not reproducible. */
+    int32_t voxblox_method;
+    /* ABI v8: how tsdf_integrate_sectors hands a host cloud to its n sector contexts.
+     * TSDF_SECTOR_INPUT_FANOUT (default): packed once, one H2D copy to the first context's GPU,
+     * then device-to-device (xGMI peer) copies to the others; every context's kernels drop the
+     * other sectors' rays.  TSDF_SECTOR_INPUT_H2D: packed once, each context copies the packed
+     * cloud over its own PCIe link.  TSDF_SECTOR_INPUT_SPLIT: classified and split on the host,
+     * each context receives only its sector's points (round 3's path).  Read from ctxs[0]. */
+    int32_t sector_input;
 } tsdf_params;
+
+#define TSDF_VB_SIMPLE 0
+#define TSDF_VB_MERGED 1
+#define TSDF_SECTOR_INPUT_FANOUT 0
+#define TSDF_SECTOR_INPUT_H2D 1
+#define TSDF_SECTOR_INPUT_SPLIT 2
 
 /* cap of one sample's 1/z^2 weight (with max_weight, whichever is lower; ABI v8) */
 #define TSDF_W0_CAP 65536.0f
@@ -159,6 +181,10 @@ typedef struct tsdf_stats {
     uint64_t n_grows;          /* capacity growths since create */
     uint64_t n_replayed;       /* batches re-run after a growth since create */
     uint64_t max_bricks;       /* current brick pool capacity */
+    /* ABI v8 */
+    uint64_t peer_mask;        /* contexts of tsdf_create_sharded: bit j set when context j's
+                                  device memory is directly reachable from this context's device
+                                  (the same device, or peer access enabled: xGMI); 0 otherwise */
 } tsdf_stats;
 
 /* kernel kinds reported in tsdf_stats.kernel_ms (profiling on) */
@@ -197,11 +223,13 @@ int tsdf_integrate_pose(tsdf_ctx* ctx, const void* pts, uint64_t n, uint32_t poi
 
 /* ABI v6: the live multi-GPU input path.  One host cloud for n_ctx contexts that
  * shard it by azimuth sector, one context per GPU: ctxs[k] was created with n_sectors = n_ctx,
- * sector = k and the same sector_yaw0 (n_ctx = 1: one unsharded context).  Every point is
- * classified once on the host (tsdf_sector_of's rule) and each context receives only its
- * sector's points, so a scan crosses PCIe once in total, split over the GPUs' links, instead of
- * once per GPU.  pose as in tsdf_integrate_pose.  Call from the one thread that uses these
- * contexts; each context's queue behaves as after tsdf_integrate_pose. */
+ * sector = k and the same sector_yaw0 (n_ctx = 1: one unsharded context).  ABI v8:
+ * ctxs[0]'s tsdf_params.sector_input picks the transfer: by default the cloud is packed once,
+ * crosses PCIe once to the first context's GPU and is copied device to device (xGMI) to the
+ * others, whose kernels drop the other sectors' rays; TSDF_SECTOR_INPUT_SPLIT classifies every
+ * point on the host (tsdf_sector_of's rule) and each context receives only its sector's points.
+ * The fields are the same bit for bit.  pose as in tsdf_integrate_pose.  Call from the one thread
+ * that uses these contexts; each context's queue behaves as after tsdf_integrate_pose. */
 int tsdf_integrate_sectors(tsdf_ctx* const* ctxs, uint32_t n_ctx, const void* pts, uint64_t n,
                            uint32_t point_step, uint32_t xyz_offset, int32_t xyz_is_f64,
                            const double pose[7]);
@@ -210,7 +238,10 @@ int tsdf_integrate_sectors(tsdf_ctx* const* ctxs, uint32_t n_ctx, const void* pt
  * points are copied (device to device) into the pending batch's staging before the call returns,
  * so d_xyz may be reused or freed at once; the scan joins the pending batch like a host scan (see
  * Batching).  (ABI v6; before, the scan launched at once and d_xyz had to stay valid until the next
- * tsdf_sync.) */
+ * tsdf_sync.)  The call blocks until that copy has run: when the scan opens a new pending batch,
+ * that includes waiting for the batch launched two batches earlier, the last reader of the
+ * staging buffer the copy overwrites.  Batches of device scans that need not block use
+ * tsdf_integrate_batch_device. */
 int tsdf_integrate_device(tsdf_ctx* ctx, const float* d_xyz, uint64_t n, const double origin[3]);
 
 /* n_scans scans in device memory, integrated in order, max_batch scans per GPU batch.  Scan s is
@@ -379,7 +410,10 @@ int tsdf_border_merge_device(tsdf_ctx* ctx, const uint32_t* d_recv, const uint64
 
 /* ---- ABI v7: several GPUs in ONE process (SURVEY §8b's num_gpus / device_ids) ----------------
  * tsdf_create_sharded: n contexts, context k on device_ids[k] (NULL: device k) as azimuth sector k
- * of n (p's n_sectors / sector / device_id are overridden), into out[0..n).  Feed them with
+ * of n (p's n_sectors / sector / device_id are overridden), into out[0..n).  ABI v8: peer access
+ * is enabled between every pair of distinct devices that supports it (hipDeviceEnablePeerAccess),
+ * so the input fan-out and the border reduce's tile copies run over xGMI; tsdf_stats.peer_mask
+ * reports which contexts each one reaches directly.  Feed them with
  * tsdf_integrate_sectors (host clouds) or each with the full device scans; read out after
  * tsdf_border_reduce_local, which runs the three steps above among the n contexts of this process:
  * keys gathered on the host, each source's tiles copied to their owner's GPU with one peer copy

@@ -7,7 +7,9 @@
 //                   min(rank, holders below it); per-destination row counts
 //   k_border_list   the bricks owned elsewhere get a row in their destination's group
 //   k_border_pack   one workgroup per row: the brick's 512 S and 512 W (+ key) go into the tile,
-//                   and the brick is reset to the background (its mass now travels)
+//                   and (reset) the brick is reset to the background (its mass now travels)
+//   k_border_reset  the same reset on its own: tsdf_border_reduce_local packs without resetting
+//                   and resets the sent bricks only after every merge succeeded
 //   k_border_merge  owner side, one workgroup per received tile, launched once per source rank in
 //                   ascending order: the tsdf_import_bricks rule (weighted mean, copy where W == 0)
 // Rows within a destination group are in atomic order: the owner merges each source's tiles of
@@ -69,7 +71,7 @@ __global__ __launch_bounds__(BRD_THREADS) void k_border_list(const uint32_t* __r
 // tile = [S 512][W 512][key lo, key hi, 0, 0]; 256 lanes move two voxels each as float2
 __global__ __launch_bounds__(BRD_THREADS) void k_border_pack(Table T, Pool Pl, float bg,
                                                              const uint32_t* __restrict__ rows,
-                                                             uint32_t* __restrict__ send) {
+                                                             uint32_t* __restrict__ send, int reset) {
     const uint32_t slot = rows[blockIdx.x];
     uint32_t* tile = send + (size_t)blockIdx.x * TILE_WORDS;
     float2* S = reinterpret_cast<float2*>(Pl.sdf + (size_t)slot * BRICK_VOX);
@@ -78,13 +80,24 @@ __global__ __launch_bounds__(BRD_THREADS) void k_border_pack(Table T, Pool Pl, f
     const float2 s = S[l], w = W[l];
     reinterpret_cast<float2*>(tile)[l] = s;
     reinterpret_cast<float2*>(tile + BRICK_VOX)[l] = w;
-    S[l] = make_float2(bg, bg);
-    W[l] = make_float2(0.0f, 0.0f);
+    if (reset) {
+        S[l] = make_float2(bg, bg);
+        W[l] = make_float2(0.0f, 0.0f);
+    }
     if (l == 0) {
         const uint64_t key = T.brick_keys[slot];
         reinterpret_cast<uint4*>(tile + 2 * BRICK_VOX)[0] =
             make_uint4((uint32_t)key, (uint32_t)(key >> 32), 0u, 0u);
     }
+}
+
+__global__ __launch_bounds__(BRD_THREADS) void k_border_reset(Pool Pl, float bg,
+                                                              const uint32_t* __restrict__ rows) {
+    const uint32_t slot = rows[blockIdx.x];
+    float2* S = reinterpret_cast<float2*>(Pl.sdf + (size_t)slot * BRICK_VOX);
+    float2* W = reinterpret_cast<float2*>(Pl.weight + (size_t)slot * BRICK_VOX);
+    S[threadIdx.x] = make_float2(bg, bg);
+    W[threadIdx.x] = make_float2(0.0f, 0.0f);
 }
 
 __global__ __launch_bounds__(BRD_THREADS) void k_border_merge(Table T, Pool Pl,
@@ -142,11 +155,19 @@ hipError_t launch_border_owner(const Table& T, uint32_t n_bricks, const uint64_t
 hipError_t launch_border_pack(const Table& T, const Pool& Pl, float bg, uint32_t n_bricks,
                               uint32_t rank, const uint32_t* d_owner, uint32_t* d_cursor,
                               uint32_t* d_rows, uint32_t n_rows, uint32_t* d_send,
-                              hipStream_t st) {
+                              bool reset, hipStream_t st) {
     if (!n_rows) return hipSuccess;
     k_border_list<<<grid_of(n_bricks), BRD_THREADS, 0, st>>>(d_owner, n_bricks, rank, d_cursor,
                                                              d_rows, n_rows);
-    k_border_pack<<<n_rows, BRD_THREADS, 0, st>>>(T, Pl, bg, d_rows, d_send);
+    k_border_pack<<<n_rows, BRD_THREADS, 0, st>>>(T, Pl, bg, d_rows, d_send, reset ? 1 : 0);
+    return hipGetLastError();
+}
+
+hipError_t launch_border_reset(const Pool& Pl, float bg, const uint32_t* d_rows, uint32_t n_rows,
+                               hipStream_t st) {
+    if (!n_rows) return hipSuccess;
+    static_assert(BRICK_VOX == 2 * BRD_THREADS, "two voxels per lane");
+    k_border_reset<<<n_rows, BRD_THREADS, 0, st>>>(Pl, bg, d_rows);
     return hipGetLastError();
 }
 

@@ -274,6 +274,14 @@ struct tsdf_ctx {
     std::vector<int8_t> split_sec;
     HostTiming split_ht;  // TSDF_HOST_TIMING: prep, classify, scatter, copies + queue (us/scan)
     uint64_t n_grows = 0, n_replayed = 0;
+    // Voxblox MergedTsdfIntegrator (tsdf_params.voxblox_method): the bundling pre-pass' buffers,
+    // one set per batch parity (tsdf_merged.hip)
+    bool merged = false;
+    MgBufs mg[2];
+    // tsdf_create_sharded: the contexts whose device memory this one reaches directly (peer access
+    // or the same device); tsdf_integrate_sectors' fan-out: its copy-done event (this device)
+    uint64_t peer_mask = 0;
+    hipEvent_t bc_ev = nullptr;
 };
 
 // Weight cap of the weighted-mean merges (import, border reduce): Voxblox's max_weight, else none
@@ -420,6 +428,15 @@ static int launch(tsdf_ctx* c, const float* d_xyz, BatchDesc& D) {
     c->ht.lap(10);
     c->ht.lap(2);
     const BatchRef B{D.n_scans, D.n_blocks, ds};
+    // MergedTsdfIntegrator: the batch's points bundled per (scan, voxel) first; the walk kernels
+    // then read one ray per bundle, in the slot of its first point (tsdf_merged.hip)
+    RayConst R = c->R;
+    const float* d_rays = d_xyz;
+    if (c->merged && D.n_blocks) {
+        HIPCHK(c, launch_mg_prepass(d_xyz, B, D.n_blocks, D.s[D.n_scans].off, c->R, c->mg[par], st));
+        d_rays = c->mg[par].xyz_out;
+        R.ray_w = c->mg[par].w_out;
+    }
     // a small batch (a live node's 1-8 scans) fuses wave-per-brick, in table order (no k_order)
     const bool small = !c->fused && D.n_scans <= (uint32_t)c->small_ns;
     const int k_front = c->fused ? KIND_WALK : KIND_COUNT;
@@ -429,9 +446,9 @@ static int launch(tsdf_ctx* c, const float* d_xyz, BatchDesc& D) {
     auto kt = [&](int kind) { return tm && !c->fused && tm->want(kind) ? tm->timing(kind) : KTime{}; };
     if (D.n_blocks) {
         if (tm && c->fused) tm->begin(k_front, st);
-        if (c->R.sec_on) HIPCHK(c, launch_sector_flags(d_xyz, B, c->R, W, c->G, par, st));
-        if (c->fused) HIPCHK(c, launch_walk(d_xyz, B, c->R, T, W, c->G, par, c->nstep, st));
-        else HIPCHK(c, launch_count(d_xyz, B, c->R, T, W, c->G, par, st, kt(KIND_COUNT),
+        if (c->R.sec_on) HIPCHK(c, launch_sector_flags(d_rays, B, R, W, c->G, par, st));
+        if (c->fused) HIPCHK(c, launch_walk(d_rays, B, R, T, W, c->G, par, c->nstep, st));
+        else HIPCHK(c, launch_count(d_rays, B, R, T, W, c->G, par, st, kt(KIND_COUNT),
                                     !c->R.sec_on && D.n_blocks <= c->count_wide));
         c->ht.lap(3);
         if (tm && c->fused) tm->next(k_front, KIND_COMPACT, st);
@@ -451,7 +468,7 @@ static int launch(tsdf_ctx* c, const float* d_xyz, BatchDesc& D) {
     if (D.n_blocks) {
         if (tm && c->fused) tm->next(KIND_COMPACT, k_back, st);
         if (c->fused) HIPCHK(c, launch_spans(B, c->R, T, W, c->G, par, c->nstep, st));
-        else HIPCHK(c, launch_place(d_xyz, B, c->R, T, W, c->G, par, st, kt(KIND_PLACE)));
+        else HIPCHK(c, launch_place(d_rays, B, R, T, W, c->G, par, st, kt(KIND_PLACE)));
         c->ht.lap(5);
         if (tm && c->fused) tm->end(k_back, st);
     }
@@ -713,7 +730,7 @@ static int grow_smp(tsdf_ctx* c) {
     float* fw[2] = {nullptr, nullptr};  // sem 3: the samples' weights
     hipError_t e = hipMalloc(&f[0], ns * sizeof(uint2));
     if (e == hipSuccess) e = hipMalloc(&f[1], ns * sizeof(uint2));
-    for (int q = 0; q < 2 && e == hipSuccess && c->R.depth_w; q++) e = hipMalloc(&fw[q], ns * sizeof(float));
+    for (int q = 0; q < 2 && e == hipSuccess && c->R.sem == 3; q++) e = hipMalloc(&fw[q], ns * sizeof(float));
     if (e != hipSuccess) {
         (void)hipGetLastError();
         for (auto q : f) if (q) (void)hipFree(q);
@@ -977,6 +994,8 @@ void tsdf_default_params(tsdf_params* p) {
     p->brick_side = TSDF_BRICK_SIDE;
     p->max_batch = 32;
     p->semantics = TSDF_SEM_VDBFUSION_F64;  // ABI v8: the mode matching VDBFusion exactly
+    p->voxblox_method = TSDF_VB_SIMPLE;
+    p->sector_input = TSDF_SECTOR_INPUT_FANOUT;
     p->allow_clear = 1;  // voxblox TsdfIntegratorBase::Config defaults
     p->use_weight_dropoff = 1;
     p->max_weight = 10000.0f;
@@ -1017,7 +1036,12 @@ void tsdf_destroy(tsdf_ctx* c) {
     for (int i = 0; i < 2; i++) {
         if (c->h_stage[i]) (void)hipHostFree(c->h_stage[i]);
         if (c->stage_done[i]) (void)hipEventDestroy(c->stage_done[i]);
+        MgBufs& M = c->mg[i];
+        for (void* q : {(void*)M.key, (void*)M.key2, (void*)M.idx, (void*)M.idx2, (void*)M.dw,
+                        (void*)M.sid, (void*)M.xyz_out, (void*)M.w_out, M.tmp})
+            if (q) (void)hipFree(q);
     }
+    if (c->bc_ev) (void)hipEventDestroy(c->bc_ev);
     for (int q = 0; q < 2; q++) {
         if (c->bst[q]) (void)hipStreamDestroy(c->bst[q]);
         if (c->ev_compact[q]) (void)hipEventDestroy(c->ev_compact[q]);
@@ -1060,7 +1084,10 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
     c->R.tau2_hi = (float)(((double)c->R.tau * (1.0 + 0x1p-20)) * ((double)c->R.tau * (1.0 + 0x1p-20)));
     // internal sem 3: Voxblox with the 1/z^2 weight (per-sample weights stored by k_place)
     c->R.depth_w = p->semantics == TSDF_SEM_VOXBLOX && p->depth_weight ? 1 : 0;
-    c->R.sem = c->R.depth_w ? 3 : p->semantics;
+    // MergedTsdfIntegrator: bundles carry summed weights, so per-sample weights too (sem 3)
+    c->merged = p->semantics == TSDF_SEM_VOXBLOX && p->voxblox_method == TSDF_VB_MERGED;
+    c->R.sem = c->R.depth_w || c->merged ? 3 : p->semantics;
+    c->R.ray_w = nullptr;  // set per launch to the pre-pass output (merged)
     c->R.allow_clear = p->allow_clear ? 1 : 0;
     c->R.dropoff = p->use_weight_dropoff ? 1 : 0;
     c->R.max_weight = p->max_weight;
@@ -1105,7 +1132,7 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
         const bool clearing = p->semantics == TSDF_SEM_VOXBLOX && p->allow_clear &&
                               std::isfinite(p->max_range);
         c->fused = p->walk == TSDF_WALK_SINGLE && !p->space_carving && !clearing && maxp <= 4 &&
-                   !c->R.depth_w &&
+                   c->R.sem != 3 &&
                    steps <= 32.0;
         c->nstep = steps <= 16.0 ? 16 : 32;
     }
@@ -1157,13 +1184,28 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
         HIPCHK(c, hipMalloc(&W.plan, (size_t)c->max_blocks * 2 * PLAN_STRIDE * sizeof(uint32_t)));
         HIPCHK(c, hipMalloc(&W.fb, (size_t)W.max_fb * sizeof(uint4)));
         HIPCHK(c, hipMalloc(&W.smp, (size_t)W.max_smp * sizeof(uint2)));
-        if (c->R.depth_w) HIPCHK(c, hipMalloc(&W.smw, (size_t)W.max_smp * sizeof(float)));
+        if (c->R.sem == 3) HIPCHK(c, hipMalloc(&W.smw, (size_t)W.max_smp * sizeof(float)));
         HIPCHK(c, hipMalloc(&W.spn, (size_t)W.max_spn * sizeof(uint32_t)));
         // (slice, size class) histogram, then first positions (k_compact; zero between batches)
         HIPCHK(c, hipMalloc(&W.ord_hist, 2 * 64 * 32 * sizeof(uint32_t)));
         HIPCHK(c, hipMemset(W.ord_hist, 0, 2 * 64 * 32 * sizeof(uint32_t)));
         HIPCHK(c, hipMalloc(&W.act, (size_t)c->max_blocks * sizeof(uint32_t)));
         HIPCHK(c, hipMalloc(&c->stage2[q], c->batch_points * 3 * sizeof(float)));
+        if (c->merged) {  // the bundling pre-pass: one set per parity, batch_points entries
+            MgBufs& M = c->mg[q];
+            const uint64_t n = c->batch_points;
+            M.cap = n;
+            M.tmp_bytes = mg_sort_scratch(n);
+            HIPCHK(c, hipMalloc(&M.key, n * 8));
+            HIPCHK(c, hipMalloc(&M.key2, n * 8));
+            HIPCHK(c, hipMalloc(&M.idx, n * 4));
+            HIPCHK(c, hipMalloc(&M.idx2, n * 4));
+            HIPCHK(c, hipMalloc(&M.dw, n * sizeof(float4)));
+            HIPCHK(c, hipMalloc(&M.sid, n * 2));
+            HIPCHK(c, hipMalloc(&M.xyz_out, n * 12));
+            HIPCHK(c, hipMalloc(&M.w_out, n * 4));
+            HIPCHK(c, hipMalloc(&M.tmp, std::max<size_t>(M.tmp_bytes, 16)));
+        }
     }
     HIPCHK(c, hipMalloc(&c->G, sizeof(Globals)));
     if (const char* e = std::getenv("TSDF_SMALL_NS")) c->small_ns = std::max(0, std::min(8, std::atoi(e)));
@@ -1236,6 +1278,8 @@ int tsdf_create(const tsdf_params* p, tsdf_ctx** out) {
         (p->semantics != TSDF_SEM_VDBFUSION && p->semantics != TSDF_SEM_VOXBLOX &&
          p->semantics != TSDF_SEM_VDBFUSION_F64) ||
         (p->semantics == TSDF_SEM_VOXBLOX && !(p->max_weight > 0.0f)) ||
+        (p->voxblox_method != TSDF_VB_SIMPLE && p->voxblox_method != TSDF_VB_MERGED) ||
+        p->sector_input < TSDF_SECTOR_INPUT_FANOUT || p->sector_input > TSDF_SECTOR_INPUT_SPLIT ||
         (p->n_sectors > 1 && p->sector >= p->n_sectors) || !std::isfinite(p->sector_yaw0) ||
         (p->max_bricks_hard && p->max_bricks_hard < p->max_bricks))
         return TSDF_EINVAL;
@@ -1395,6 +1439,99 @@ int tsdf_integrate(tsdf_ctx* c, const void* pts, uint64_t n, uint32_t point_step
     return integrate_impl(c, pts, n, point_step, xyz_offset, xyz_is_f64, pose_of_origin(origin));
 }
 
+}  // extern "C"
+
+// tsdf_integrate_sectors without a host split (tsdf_params.sector_input FANOUT / H2D): the cloud
+// is packed ONCE into ctxs[0]'s pinned buffer h[0] (on every context's staging threads), and every
+// context receives all of it -- its kernels drop the other sectors' rays (R.sec_on), so the fields
+// are those of the split, bit for bit.
+//   FANOUT: one H2D copy into ctxs[0]'s staging, then ctxs[k] copies that region device to device
+//           (hipMemcpyPeerAsync: xGMI with peer access, tsdf_create_sharded) into its own staging,
+//           after ctxs[0]'s copy (an event); ctxs[0]'s stream then waits for those copies, so its
+//           staging region is not rewritten (and h[0] not reused) before they ran.
+//   H2D:    every context copies h[0] over its own PCIe link; ctxs[0]'s stream waits for them all
+//           before it records h[0]'s reuse event.
+static int sectors_broadcast(tsdf_ctx* const* ctxs, uint32_t n_ctx, const void* pts, uint64_t n,
+                             uint32_t point_step, uint32_t xyz_offset, int32_t xyz_is_f64,
+                             const ScanPose& P, float* const* h, const int* hb, bool fanout) {
+    tsdf_ctx* c0 = ctxs[0];
+    float* hx = h[0];
+    const char* base = static_cast<const char*>(pts);
+    auto pack = [&](uint64_t i0, uint64_t i1) {
+        if (!xyz_is_f64 && point_step == 12 && xyz_offset == 0) {
+            std::memcpy(hx + 3 * i0, base + 12 * i0, (i1 - i0) * 12);
+            return;
+        }
+        for (uint64_t i = i0; i < i1; i++) {
+            const char* q = base + i * point_step + xyz_offset;
+            if (xyz_is_f64) {
+                double d[3];
+                std::memcpy(d, q, sizeof d);
+                hx[3 * i] = (float)d[0];
+                hx[3 * i + 1] = (float)d[1];
+                hx[3 * i + 2] = (float)d[2];
+            } else {
+                std::memcpy(hx + 3 * i, q, 12);
+            }
+        }
+    };
+    // every context's staging threads pack a share of the points
+    int pbase[TSDF_MAX_WORLD + 1];
+    pbase[0] = 0;
+    for (uint32_t k = 0; k < n_ctx; k++)
+        pbase[k + 1] = pbase[k] + (ctxs[k]->pack ? ctxs[k]->pack->parts() - (k ? 1 : 0) : (k ? 0 : 1));
+    const int parts = n >= (1u << 15) ? pbase[n_ctx] : 1;
+    auto part = [&](int q) { pack(n * (uint64_t)q / parts, n * (uint64_t)(q + 1) / parts); };
+    if (parts == 1) {
+        part(0);
+    } else {
+        for (uint32_t k = 1; k < n_ctx; k++)
+            if (ctxs[k]->pack) ctxs[k]->pack->start(part, pbase[k] - 1);
+        if (c0->pack) c0->pack->run(part);
+        else part(0);
+        for (uint32_t k = 1; k < n_ctx; k++)
+            if (ctxs[k]->pack) ctxs[k]->pack->wait();
+    }
+    // the copies: ctxs[0] first (FANOUT reads its staging region)
+    float* dst0 = nullptr;
+    for (uint32_t k = 0; k < n_ctx; k++) {
+        tsdf_ctx* c = ctxs[k];
+        HIPCHK(c, hipSetDevice(c->device));
+        int rc = pend_stage_buffer(c);
+        if (rc) return rc;
+        float* dst = c->stage2[c->pend_stage] + 3 * (uint64_t)c->pend.s[c->pend.n_scans].off;
+        if (k == 0) {
+            dst0 = dst;
+            if (n) HIPCHK(c, hipMemcpyAsync(dst, hx, n * 12, hipMemcpyHostToDevice, c->stream));
+            if (fanout && n_ctx > 1) {
+                if (!c->bc_ev) HIPCHK(c, hipEventCreateWithFlags(&c->bc_ev, hipEventDisableTiming));
+                HIPCHK(c, hipEventRecord(c->bc_ev, c->stream));
+            }
+        } else if (n) {
+            if (fanout) {
+                HIPCHK(c, hipStreamWaitEvent(c->stream, c0->bc_ev, 0));
+                HIPCHK(c, c->device == c0->device
+                              ? hipMemcpyAsync(dst, dst0, n * 12, hipMemcpyDeviceToDevice, c->stream)
+                              : hipMemcpyPeerAsync(dst, c->device, dst0, c0->device, n * 12, c->stream));
+            } else {
+                HIPCHK(c, hipMemcpyAsync(dst, hx, n * 12, hipMemcpyHostToDevice, c->stream));
+            }
+            // ctxs[0] must not rewrite its staging region or h[0] before this copy ran
+            if (!c->bc_ev) HIPCHK(c, hipEventCreateWithFlags(&c->bc_ev, hipEventDisableTiming));
+            HIPCHK(c, hipEventRecord(c->bc_ev, c->stream));
+        }
+        if (k) HIPCHK(c, hipEventRecord(c->stage_done[hb[k]], c->stream));
+        rc = pend_push(c, n, P);
+        if (rc) return rc;
+    }
+    HIPCHK(c0, hipSetDevice(c0->device));
+    for (uint32_t k = 1; k < n_ctx && n; k++) HIPCHK(c0, hipStreamWaitEvent(c0->stream, ctxs[k]->bc_ev, 0));
+    HIPCHK(c0, hipEventRecord(c0->stage_done[hb[0]], c0->stream));
+    return TSDF_OK;
+}
+
+extern "C" {
+
 // One host cloud for N sector-sharded contexts (the live N-GPU input path): every
 // point is classified once (the kernels' in_sector rule on each context's bounds) and packed into
 // its context's pinned staging; each context then copies only its sector's points to its GPU, so a
@@ -1438,6 +1575,18 @@ int tsdf_integrate_sectors(tsdf_ctx* const* ctxs, uint32_t n_ctx, const void* pt
         c->stage_cur ^= 1;
         HIPCHK(c, hipEventSynchronize(c->stage_done[hb[k]]));
         h[k] = c->h_stage[hb[k]];
+    }
+    int mode = n_ctx > 1 ? c0->p.sector_input : TSDF_SECTOR_INPUT_SPLIT;
+    // MergedTsdfIntegrator bundles the whole scan's points before the sector filter: a host split
+    // would bundle each sector's points apart
+    if (mode == TSDF_SECTOR_INPUT_SPLIT && n_ctx > 1 && c0->merged) mode = TSDF_SECTOR_INPUT_FANOUT;
+    if (mode == TSDF_SECTOR_INPUT_FANOUT || mode == TSDF_SECTOR_INPUT_H2D) {
+        const int rc = sectors_broadcast(ctxs, n_ctx, pts, n, point_step, xyz_offset, xyz_is_f64,
+                                         P, h, hb, mode == TSDF_SECTOR_INPUT_FANOUT);
+        if (rc) return rc;
+        ht.lap(3);
+        ht.n++;
+        return TSDF_OK;
     }
     // Two passes over point chunks, on the staging threads of ALL the contexts (each GPU's host
     // share): (1) read the records once, pack xyz into c0's scratch and classify each point,
@@ -2000,6 +2149,7 @@ int tsdf_get_stats(tsdf_ctx* c, tsdf_stats* out) {
     out->n_grows = c->n_grows;
     out->n_replayed = c->n_replayed;
     out->max_bricks = c->T.max_bricks;
+    out->peer_mask = c->peer_mask;
     if (c->batch_id) {
         const Counters& L = g.last;
         out->n_active_last = L.n_active;
@@ -2120,10 +2270,17 @@ int tsdf_brick_keys_device(tsdf_ctx* c, uint64_t* d_keys, uint64_t cap, uint64_t
     return TSDF_OK;
 }
 
-int tsdf_border_pack_device(tsdf_ctx* c, const uint64_t* d_all_keys, const uint64_t* counts,
+}  // extern "C"
+
+// tsdf_border_pack_device with the reset optional: keep_rows (not null) receives the device list
+// of the packed bricks' pool slots (caller frees it; null when nothing was packed) and their count,
+// so the caller can reset them later (launch_border_reset)
+static int border_pack_impl(tsdf_ctx* c, const uint64_t* d_all_keys, const uint64_t* counts,
                             uint64_t stride, uint32_t world, uint32_t rank, uint32_t* d_send,
-                            uint64_t cap_rows, uint64_t* send_counts) {
-    if (!c) return TSDF_EINVAL;
+                            uint64_t cap_rows, uint64_t* send_counts, bool reset,
+                            uint32_t** keep_rows, uint64_t* kept) {
+    if (keep_rows) *keep_rows = nullptr;
+    if (kept) *kept = 0;
     if (!counts || !send_counts || world == 0 || world > TSDF_MAX_WORLD || rank >= world)
         return fail(c, TSDF_EINVAL, "bad world/rank or null counts");
     WorldCounts wc{};
@@ -2169,13 +2326,29 @@ int tsdf_border_pack_device(tsdf_ctx* c, const uint64_t* d_all_keys, const uint6
                                c->stream);
         if (e == hipSuccess)
             e = launch_border_pack(c->T, c->Pl, c->R.bg, (uint32_t)nb, rank, d_owner,
-                                   d_aux + MAX_WORLD, d_rows, (uint32_t)rows, d_send, c->stream);
+                                   d_aux + MAX_WORLD, d_rows, (uint32_t)rows, d_send, reset,
+                                   c->stream);
         if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    }
+    if (e == hipSuccess && keep_rows && d_rows) {  // handed to the caller
+        *keep_rows = d_rows;
+        *kept = rows;
+        d_rows = nullptr;
     }
     for (void* q : {(void*)d_owner, (void*)d_aux, (void*)d_rows})
         if (q) (void)hipFree(q);
     if (e != hipSuccess) return fail(c, TSDF_EHIP, "border pack: %s", hipGetErrorString(e));
     return TSDF_OK;
+}
+
+extern "C" {
+
+int tsdf_border_pack_device(tsdf_ctx* c, const uint64_t* d_all_keys, const uint64_t* counts,
+                            uint64_t stride, uint32_t world, uint32_t rank, uint32_t* d_send,
+                            uint64_t cap_rows, uint64_t* send_counts) {
+    if (!c) return TSDF_EINVAL;
+    return border_pack_impl(c, d_all_keys, counts, stride, world, rank, d_send, cap_rows,
+                            send_counts, true, nullptr, nullptr);
 }
 
 int tsdf_border_merge_device(tsdf_ctx* c, const uint32_t* d_recv, const uint64_t* recv_counts,
@@ -2217,6 +2390,24 @@ int tsdf_create_sharded(const tsdf_params* p, uint32_t n, const int32_t* device_
                 out[j] = nullptr;
             }
             return rc;
+        }
+    }
+    // peer access between every pair of distinct devices that supports it, so the input fan-out
+    // (tsdf_integrate_sectors) and the border reduce's tile copies go GPU to GPU over xGMI
+    for (uint32_t k = 0; k < n; k++) {
+        tsdf_ctx* c = out[k];
+        for (uint32_t j = 0; j < n; j++) {
+            const int dk = c->device, dj = out[j]->device;
+            if (dk == dj) {
+                c->peer_mask |= 1ull << j;
+                continue;
+            }
+            int can = 0;
+            if (hipDeviceCanAccessPeer(&can, dk, dj) != hipSuccess || !can) continue;
+            if (hipSetDevice(dk) != hipSuccess) continue;
+            const hipError_t e = hipDeviceEnablePeerAccess(dj, 0);
+            if (e == hipSuccess || e == hipErrorPeerAccessAlreadyEnabled) c->peer_mask |= 1ull << j;
+            (void)hipGetLastError();  // an already-enabled pair leaves its error code behind
         }
     }
     return TSDF_OK;
@@ -2269,8 +2460,12 @@ int tsdf_border_reduce_local(tsdf_ctx* const* ctxs, uint32_t n, uint64_t* bricks
     for (uint32_t k = 0; k < n; k++) stride = std::max(stride, counts[k]);
     std::vector<uint64_t> all(stride * n, ~0ull);
     for (uint32_t k = 0; k < n; k++) std::copy(hkeys[k].begin(), hkeys[k].end(), all.begin() + k * stride);
-    // 2. each context packs the bricks a lower rank owns
+    // 2. each context packs the bricks a lower rank owns, WITHOUT resetting them: the sources
+    // keep their mass until every merge has succeeded (step 5), so a failed copy or merge loses
+    // nothing
     std::vector<uint32_t*> send(n, nullptr);
+    std::vector<uint32_t*> sent_rows(n, nullptr);
+    std::vector<uint64_t> n_sent(n, 0);
     std::vector<std::vector<uint64_t>> sc(n, std::vector<uint64_t>(n, 0));
     for (uint32_t k = 0; k < n && !rc; k++) {
         tsdf_ctx* c = ctxs[k];
@@ -2280,8 +2475,13 @@ int tsdf_border_reduce_local(tsdf_ctx* const* ctxs, uint32_t n, uint64_t* bricks
             rc = fail(c, TSDF_EHIP, "border reduce: key upload failed");
         if (!rc) rc = dalloc(c, counts[k] * TSDF_TILE_WORDS * 4, &ds);
         if (!rc)
-            rc = tsdf_border_pack_device(c, static_cast<uint64_t*>(dk), counts.data(), stride, n, k,
-                                         static_cast<uint32_t*>(ds), counts[k], sc[k].data());
+            rc = border_pack_impl(c, static_cast<uint64_t*>(dk), counts.data(), stride, n, k,
+                                  static_cast<uint32_t*>(ds), counts[k], sc[k].data(), false,
+                                  &sent_rows[k], &n_sent[k]);
+        if (sent_rows[k]) {  // freed with the other buffers
+            dev_bufs.push_back(sent_rows[k]);
+            dev_of.push_back(c->device);
+        }
         send[k] = static_cast<uint32_t*>(ds);
     }
     // 3. every owner d receives block d of every source, sources ascending; 4. merge
@@ -2313,6 +2513,16 @@ int tsdf_border_reduce_local(tsdf_ctx* const* ctxs, uint32_t n, uint64_t* bricks
         }
         if (!rc) rc = tsdf_border_merge_device(c, static_cast<uint32_t*>(dr), rcnt.data(), n);
         moved += total;
+    }
+    // 5. every merge succeeded: the sent bricks' mass now lives at their owners, reset the sources
+    for (uint32_t k = 0; k < n && !rc; k++) {
+        if (!n_sent[k]) continue;
+        tsdf_ctx* c = ctxs[k];
+        hipError_t e = hipSetDevice(c->device);
+        if (e == hipSuccess)
+            e = launch_border_reset(c->Pl, c->R.bg, sent_rows[k], (uint32_t)n_sent[k], c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        if (e != hipSuccess) rc = fail(c, TSDF_EHIP, "border reduce: reset: %s", hipGetErrorString(e));
     }
     release();
     if (rc) {  // the failing context holds the message; the first context gets a copy

@@ -115,6 +115,10 @@ struct RayConst {
     // weights in Work::smw)
     int depth_w;
     float w0_cap;  // cap of a sample's 1/z^2 weight: min(max_weight, 2^16) (TSDF_W0_CAP)
+    // Voxblox MergedTsdfIntegrator (tsdf_params.voxblox_method; sem 3): per ray slot of the
+    // batch, its bundle's weight (< 0: a clearing bundle; 0: no bundle ray in this slot), set per
+    // launch to the bundling pre-pass's output (tsdf_merged.hip); null otherwise
+    const float* ray_w;
 };
 
 // fp32 pseudo-angle of (x, y) in [0, 4), monotone in atan2 (include/tsdf_hip.h tsdf_sector_of):
@@ -332,14 +336,35 @@ struct WorldCounts { uint64_t n[MAX_WORLD]; };
 hipError_t launch_border_owner(const Table& T, uint32_t n_bricks, const uint64_t* d_all_keys,
                                const WorldCounts& counts, uint64_t stride, uint32_t rank,
                                uint32_t* d_owner, uint32_t* d_dest_n, hipStream_t st);
-// rows of the bricks owned elsewhere (cursor[r] = first row of destination r), tiles packed and the
-// bricks reset to the background
+// rows of the bricks owned elsewhere (cursor[r] = first row of destination r), tiles packed and,
+// with reset, the bricks reset to the background
 hipError_t launch_border_pack(const Table& T, const Pool& Pl, float bg, uint32_t n_bricks,
                               uint32_t rank, const uint32_t* d_owner, uint32_t* d_cursor,
-                              uint32_t* d_rows, uint32_t n_rows, uint32_t* d_send, hipStream_t st);
+                              uint32_t* d_rows, uint32_t n_rows, uint32_t* d_send, bool reset,
+                              hipStream_t st);
+// the bricks of rows[0, n_rows) reset to the background (after a pack without reset)
+hipError_t launch_border_reset(const Pool& Pl, float bg, const uint32_t* d_rows, uint32_t n_rows,
+                               hipStream_t st);
 // max_w: the merged weight's cap (Voxblox max_weight; +inf for VDBFusion)
 hipError_t launch_border_merge(const Table& T, const Pool& Pl, const uint32_t* d_recv,
                                uint64_t n_rows, Globals* G, float max_w, hipStream_t st);
+// Voxblox MergedTsdfIntegrator's bundling pre-pass (tsdf_merged.hip): per batch, the points of
+// every scan bundled by voxel; xyz_out / w_out hold one ray per bundle at its first point's slot
+// (other slots: NaN point, weight 0), so the batch keeps its ray layout and block counts
+struct MgBufs {
+    uint64_t *key = nullptr, *key2 = nullptr;
+    uint32_t *idx = nullptr, *idx2 = nullptr;
+    float4* dw = nullptr;     // p - o and the point's getVoxelWeight
+    uint16_t* sid = nullptr;  // the point's scan in the batch
+    float* xyz_out = nullptr;
+    float* w_out = nullptr;
+    void* tmp = nullptr;      // radix-sort scratch
+    size_t tmp_bytes = 0;
+    uint64_t cap = 0;         // points
+};
+size_t mg_sort_scratch(uint64_t n_points);
+hipError_t launch_mg_prepass(const float* d_xyz, const BatchRef& B, uint32_t n_blocks,
+                             uint64_t n_points, const RayConst& R, MgBufs& M, hipStream_t st);
 // Ouster packets (tsdf_ouster.hip)
 struct OsField {
     uint32_t nbytes;  // little-endian source bytes (0: the profile has no such field)

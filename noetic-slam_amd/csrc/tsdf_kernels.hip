@@ -37,20 +37,6 @@ namespace tsdf {
 // ------------------------------------------------------------------------------------------------
 // shared helpers of the batch kernels
 
-// Scan and ray range of k_count / k_place workgroup b (uniform: scalar loads of the descriptor).
-__device__ __forceinline__ void block_range(const BatchRef& D, uint32_t b, uint32_t& t,
-                                            uint32_t& r0, uint32_t& r1) {
-    uint32_t lo = 0, hi = D.n_scans;  // blk[lo] <= b < blk[hi]
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (D.s[mid].blk <= b) lo = mid;
-        else hi = mid;
-    }
-    t = lo;
-    r0 = D.s[t].off + (b - D.s[t].blk) * RPB;
-    r1 = min(D.s[t + 1].off, r0 + RPB);
-}
-
 // XCD-aware block order: the hardware deals workgroup p to XCD p % 8, so consecutive blocks --
 // adjacent azimuth wedges of a scan -- would land on different XCDs, and a brick on a wedge border
 // would have its cell row fetched into two L2s.  Within every aligned group of 8 G workgroups,
@@ -183,7 +169,7 @@ __global__ __launch_bounds__(NT, SEM == 2 && NT == CNT_THREADS ? TSDF_F64_COUNT_
         uint32_t* pc = Wk.pair + (size_t)i * maxp;
         uint32_t k = 0;
         typename Walk<SEM>::State r;
-        const bool ok = Walk<SEM>::init(R, D, t, xyz[3 * (size_t)i], xyz[3 * (size_t)i + 1],
+        const bool ok = Walk<SEM>::init(R, D, t, i, xyz[3 * (size_t)i], xyz[3 * (size_t)i + 1],
                                         xyz[3 * (size_t)i + 2], r);
         valid += ok ? 1u : 0u;
         // One pair per distinct brick; a line visits a brick in one contiguous run of DDA voxels,
@@ -945,7 +931,7 @@ __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) v
                                : NO_PAIR;
     const float ox = D.s[t].ox, oy = D.s[t].oy, oz = D.s[t].oz;
     typename Walk<SEM>::State r;
-    const bool ok = i < r1 && Walk<SEM>::init(R, D, t, px, py, pz, r);
+    const bool ok = i < r1 && Walk<SEM>::init(R, D, t, i, px, py, pz, r);
     // sector sharding: a half block without a ray of this GPU's sector has no samples to place
     if (R.sec_on && !block_any<PLC_THREADS>(ok, s_vote[0])) return;
     if (threadIdx.x < (uint32_t)PLC_WORDS) s_bits[threadIdx.x] = plan_bits;
@@ -1141,7 +1127,7 @@ __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) v
             // a fresh state: the first pass's is dead after its loop (kept, it would be carried
             // out of that loop and cost register copies at every step)
             typename Walk<SEM>::State r2;
-            Walk<SEM>::init(R, D, t, px, py, pz, r2);
+            Walk<SEM>::init(R, D, t, i, px, py, pz, r2);
             walk_short(std::false_type{}, std::true_type{}, r2);
         }
     } else {

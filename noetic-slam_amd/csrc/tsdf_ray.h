@@ -187,6 +187,21 @@ __device__ __forceinline__ bool ray_step_sel(RayState& r) {
 // Voxblox ray model (TSDF_SEM_VOXBLOX; the bit-exact twin of oracle/tsdf_oracle.c walk_ray_vb,
 // which restates voxblox SimpleTsdfIntegrator / RayCaster / updateTsdfVoxel — DESIGN.md §2b)
 
+// Scan and ray range of k_count / k_place workgroup b, and of the merged pre-pass' k_mg_keys
+// (uniform: scalar loads of the descriptor).
+__device__ __forceinline__ void block_range(const BatchRef& D, uint32_t b, uint32_t& t,
+                                            uint32_t& r0, uint32_t& r1) {
+    uint32_t lo = 0, hi = D.n_scans;  // blk[lo] <= b < blk[hi]
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (D.s[mid].blk <= b) lo = mid;
+        else hi = mid;
+    }
+    t = lo;
+    r0 = D.s[t].off + (b - D.s[t].blk) * RPB;
+    r1 = min(D.s[t + 1].off, r0 + RPB);
+}
+
 constexpr float VB_MIN_WEIGHT = 1.0f / 65536.0f;  // lighter samples are dropped whole
 
 struct VbState {
@@ -214,16 +229,27 @@ __device__ __forceinline__ void vb_axis(float ss, float es, int& v, int& st, flo
 }
 
 // isPointValid + RayCaster setup; false when the ray is dropped.
+// Ray slot i of the batch (R.ray_w: MergedTsdfIntegrator bundles, see RayConst).
 __device__ __forceinline__ bool vb_init(const RayConst& R, const BatchRef& D, uint32_t t,
-                                        float px, float py, float pz, VbState& r) {
+                                        uint32_t i, float px, float py, float pz, VbState& r) {
     const float ox = D.s[t].ox, oy = D.s[t].oy, oz = D.s[t].oz;
     const float dx = px - ox, dy = py - oy, dz = pz - oz;
     if (!in_sector(R, dx, dy)) return false;  // another GPU's azimuth sector
     const float depth = __builtin_sqrtf(dx * dx + (dy * dy + dz * dz));
     if (!(depth > 0.0f)) return false;
-    if (depth < R.min_range) return false;
-    const bool clearing = depth > R.max_range;
-    if (clearing && !R.allow_clear) return false;
+    bool clearing;
+    float bw = 0.0f;
+    if (R.ray_w) {
+        // a bundle's ray: integrateVoxel passes the clearing flag and the summed weight, the ray's
+        // length is not tested again
+        bw = R.ray_w[i];
+        if (bw == 0.0f) return false;
+        clearing = bw < 0.0f;
+    } else {
+        if (depth < R.min_range) return false;
+        clearing = depth > R.max_range;
+        if (clearing && !R.allow_clear) return false;
+    }
     const float ux = dx / depth, uy = dy / depth, uz = dz / depth;
     float ex, ey, ez, sx, sy, sz;
     if (clearing) {
@@ -260,7 +286,9 @@ __device__ __forceinline__ bool vb_init(const RayConst& R, const BatchRef& D, ui
     // (upstream's per-update max_weight cap bounds the fused weight the same way).  A scan without
     // an orientation (origin-only entry points: zero axis) takes the constant weight 1.
     r.w0 = 1.0f;
-    if (R.depth_w) {
+    if (R.ray_w) {
+        r.w0 = fabsf(bw);
+    } else if (R.depth_w) {
         const float zx = D.s[t].zx, zy = D.s[t].zy, zz = D.s[t].zz;
         if (zx != 0.0f || zy != 0.0f || zz != 0.0f) {
             const float z = fabsf(zx * dx + (zy * dy + zz * dz));
@@ -344,7 +372,8 @@ template <>
 struct Walk<0> {  // TSDF_SEM_VDBFUSION
     typedef RayState State;
     __device__ static __forceinline__ bool init(const RayConst& R, const BatchRef& D, uint32_t t,
-                                                float px, float py, float pz, State& r) {
+                                                uint32_t i, float px, float py, float pz, State& r) {
+        (void)i;
         return ray_init(R, D.s[t].ox, D.s[t].oy, D.s[t].oz, px, py, pz, r);
     }
     __device__ static __forceinline__ bool gate(const RayConst& R, float ox, float oy, float oz,
@@ -377,8 +406,8 @@ template <>
 struct Walk<1> {  // TSDF_SEM_VOXBLOX
     typedef VbState State;
     __device__ static __forceinline__ bool init(const RayConst& R, const BatchRef& D, uint32_t t,
-                                                float px, float py, float pz, State& r) {
-        return vb_init(R, D, t, px, py, pz, r);
+                                                uint32_t i, float px, float py, float pz, State& r) {
+        return vb_init(R, D, t, i, px, py, pz, r);
     }
     __device__ static __forceinline__ bool gate(const RayConst& R, float ox, float oy, float oz,
                                                 const State& r, bool check = true) {
@@ -617,7 +646,8 @@ template <>
 struct Walk<2> {  // TSDF_SEM_VDBFUSION_F64
     typedef VdbState State;
     __device__ static __forceinline__ bool init(const RayConst& R, const BatchRef& D, uint32_t t,
-                                                float px, float py, float pz, State& r) {
+                                                uint32_t i, float px, float py, float pz, State& r) {
+        (void)i;
         return vdb_init(R, D, t, px, py, pz, r);
     }
     // k_count: the verdict alone ((float)sqrt(d2) < tau, i.e. -dist > -tau, is d2 < gate_d2)

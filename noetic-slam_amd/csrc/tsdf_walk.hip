@@ -103,7 +103,7 @@ __global__ __launch_bounds__(WLK_THREADS) void k_walk(const float* __restrict__ 
     }
     const float ox = D.s[t].ox, oy = D.s[t].oy, oz = D.s[t].oz;
     typename Walk<SEM>::State r{};
-    const bool ok = i < r1 && Walk<SEM>::init(R, D, t, px, py, pz, r);
+    const bool ok = i < r1 && Walk<SEM>::init(R, D, t, i, px, py, pz, r);
     const int bx0 = r.vx >> 3, by0 = r.vy >> 3, bz0 = r.vz >> 3;  // the ray's first brick
     // One register slot per DDA step: sv = the sample, mv = voxel | pair << 9 | rank in the pair
     // << 11 | valid << 16 (0: no sample at this step).

@@ -16,7 +16,7 @@ STATUS_NAMES = {
     TSDF_EHIP: "TSDF_EHIP", TSDF_ENODEV: "TSDF_ENODEV", TSDF_EOVERFLOW: "TSDF_EOVERFLOW",
 }
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 TILE_WORDS = 1028  # TSDF_TILE_WORDS: u32 words of one border-brick tile
 MAX_WORLD = 64
 SEM_VDBFUSION = 0
@@ -30,6 +30,8 @@ KERNEL_KINDS = ("count", "compact", "place", "integrate", "walk", "spans")
 WALK_TWO = 0     # tsdf_params.walk: k_count + k_place (default)
 WALK_SINGLE = 1  # k_walk + k_spans when the band allows it
 MC_TABLES = {"generated": 0, "lorensen": 1}  # TSDF_MC_GENERATED, TSDF_MC_LORENSEN
+VB_METHODS = {"simple": 0, "merged": 1}  # tsdf_params.voxblox_method (TSDF_VB_*)
+SECTOR_INPUTS = {"fanout": 0, "h2d": 1, "split": 2}  # tsdf_params.sector_input
 
 
 class TsdfParams(C.Structure):
@@ -61,6 +63,9 @@ class TsdfParams(C.Structure):
         ("walk", C.c_int32),
         # ABI v6
         ("depth_weight", C.c_int32),
+        # ABI v8
+        ("voxblox_method", C.c_int32),
+        ("sector_input", C.c_int32),
     ]
 
 
@@ -82,6 +87,8 @@ class TsdfStats(C.Structure):
         ("n_grows", C.c_uint64),
         ("n_replayed", C.c_uint64),
         ("max_bricks", C.c_uint64),
+        # ABI v8
+        ("peer_mask", C.c_uint64),
     ]
 
     def as_dict(self):
@@ -179,9 +186,10 @@ def default_params(lib=None, **kw):
         p.min_range, p.max_range = 0.0, math.inf
         p.max_bricks, p.max_points, p.max_pairs = 1 << 20, 1 << 18, 0
         p.device_id, p.brick_side, p.max_batch = 0, BRICK_SIDE, 32
-        p.semantics, p.allow_clear, p.use_weight_dropoff, p.max_weight = SEM_VDBFUSION, 1, 1, 1e4
+        p.semantics, p.allow_clear, p.use_weight_dropoff, p.max_weight = SEM_VDBFUSION_F64, 1, 1, 1e4
         p.n_sectors, p.sector, p.sector_yaw0, p.max_bricks_hard = 0, 0, 0.0, 0
         p.walk = WALK_TWO
+        p.depth_weight, p.voxblox_method, p.sector_input = 1, 0, 0
     for k, v in kw.items():
         if not hasattr(p, k):
             raise TypeError("unknown tsdf_params field %r" % k)

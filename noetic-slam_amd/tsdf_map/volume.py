@@ -106,7 +106,8 @@ class TSDFVolume:
                     max_range=math.inf, max_bricks=1 << 20, max_points=1 << 18, device_id=0,
                     max_batch=32, pipeline=False, semantics="vdbfusion_f64", allow_clear=True,
                     use_weight_dropoff=True, max_weight=10000.0, n_sectors=0, sector=0,
-                    sector_yaw0=0.0, max_bricks_hard=0, walk="two", use_const_weight=False):
+                    sector_yaw0=0.0, max_bricks_hard=0, walk="two", use_const_weight=False,
+                    method="simple", sector_input="fanout"):
         """tsdf_params from the VDBFusion / Voxblox-style keyword arguments."""
         if semantics not in _abi.SEMANTICS:
             raise ValueError("semantics must be one of %s" % sorted(_abi.SEMANTICS))
@@ -134,6 +135,12 @@ class TSDFVolume:
         p.walk = {"two": _abi.WALK_TWO, "single": _abi.WALK_SINGLE}[walk]
         # Voxblox getVoxelWeight: 1 (use_const_weight) or 1 / z^2 of the sensor-frame depth
         p.depth_weight = 0 if use_const_weight else 1
+        # Voxblox's integrator (voxblox_ros `method`): "simple" or "merged" (ABI v8)
+        if method not in _abi.VB_METHODS:
+            raise ValueError("method must be one of %s" % sorted(_abi.VB_METHODS))
+        p.voxblox_method = _abi.VB_METHODS[method]
+        # tsdf_integrate_sectors' transfer (ABI v8): "fanout", "h2d" or "split"
+        p.sector_input = _abi.SECTOR_INPUTS[sector_input]
         return p
 
     # -- lifecycle ------------------------------------------------------------------------------

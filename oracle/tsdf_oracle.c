@@ -90,6 +90,9 @@ struct tsdf_ctx {
      * n_thr partitions by brick hash, each a full context of its own (sub[p]); tab is then only a
      * read-out snapshot, rebuilt from the partitions when mt_dirty */
     int n_thr, mt_dirty;
+    /* Voxblox MergedTsdfIntegrator (voxblox_method == TSDF_VB_MERGED): while mg_on, the "points"
+     * walked are the scan's bundled rays, 16-B records (x, y, z, w) with w < 0 for a clearing ray */
+    int mg_on;
     struct tsdf_ctx** sub;
     struct mt_bucket* bk; /* n_thr x n_thr: samples of ray-thread t for partition p at [t n_thr + p] */
 };
@@ -237,6 +240,8 @@ void tsdf_default_params(tsdf_params* p) {
     p->use_weight_dropoff = 1;
     p->max_weight = 10000.0f;
     p->depth_weight = 1; /* voxblox use_const_weight = false (upstream's default) */
+    p->voxblox_method = TSDF_VB_SIMPLE;
+    p->sector_input = TSDF_SECTOR_INPUT_FANOUT;
 }
 
 int tsdf_abi_version(void) { return TSDF_ABI_VERSION; }
@@ -248,6 +253,9 @@ int tsdf_create(const tsdf_params* params, tsdf_ctx** out) {
         (params->semantics != TSDF_SEM_VDBFUSION && params->semantics != TSDF_SEM_VOXBLOX &&
          params->semantics != TSDF_SEM_VDBFUSION_F64) ||
         (params->semantics == TSDF_SEM_VOXBLOX && !(params->max_weight > 0.0f)) ||
+        (params->voxblox_method != TSDF_VB_SIMPLE && params->voxblox_method != TSDF_VB_MERGED) ||
+        (params->sector_input < TSDF_SECTOR_INPUT_FANOUT ||
+         params->sector_input > TSDF_SECTOR_INPUT_SPLIT) ||
         (params->n_sectors > 1 && params->sector >= params->n_sectors) ||
         !isfinite(params->sector_yaw0))
         return TSDF_EINVAL;
@@ -494,25 +502,34 @@ static int64_t walk_ray_vdb(tsdf_ctx* c, const double p[3], const double o[3], v
  * All fp32, -ffp-contract=off, the GPU's op order (tsdf_ray.h vb_*). */
 #define VB_MIN_WEIGHT (1.0f / 65536.0f)
 
+/* bw: 0 for a point's own ray (SimpleTsdfIntegrator); else a MergedTsdfIntegrator bundle's ray,
+ * weight |bw|, a clearing ray when bw < 0: integrateVoxel hands the RayCaster the clearing flag and
+ * updateTsdfVoxel the bundle's summed point weight, without re-testing the ray's length */
 static int64_t walk_ray_vb(tsdf_ctx* c, float px, float py, float pz, float ox, float oy,
-                           float oz, visit_fn visit, void* user) {
+                           float oz, float bw, visit_fn visit, void* user) {
     const float vs = c->vs, inv_vs = c->inv_vs, tau = c->tau;
     const float dx = px - ox, dy = py - oy, dz = pz - oz;
     if (!ctx_in_sector(c, dx, dy)) return -1; /* another GPU's azimuth sector */
     /* Eigen's fixed-size-3 reductions (squaredNorm, dot) associate as x + (y + z) */
     const float depth = sqrtf(dx * dx + (dy * dy + dz * dz));
     if (!(depth > 0.0f)) return -1;
-    if (depth < (float)c->p.min_range) return -1;
     int clearing = 0;
-    if (depth > (float)c->p.max_range) {
-        if (!c->p.allow_clear) return -1;
-        clearing = 1;
+    if (bw != 0.0f) {
+        clearing = bw < 0.0f;
+    } else {
+        if (depth < (float)c->p.min_range) return -1;
+        if (depth > (float)c->p.max_range) {
+            if (!c->p.allow_clear) return -1;
+            clearing = 1;
+        }
     }
     const float ux = dx / depth, uy = dy / depth, uz = dz / depth;
     /* TsdfIntegratorBase::getVoxelWeight: use_const_weight -> 1; else 1 / z^2 of the point's
      * sensor-frame depth z = zaxis . (p - o) (Eigen's x + (y + z)), 0 for |z| <= kEpsilon 1e-6 */
     float w0 = 1.0f;
-    if (c->p.depth_weight && (c->zax[0] != 0.0f || c->zax[1] != 0.0f || c->zax[2] != 0.0f)) {
+    if (bw != 0.0f) {
+        w0 = fabsf(bw);
+    } else if (c->p.depth_weight && (c->zax[0] != 0.0f || c->zax[1] != 0.0f || c->zax[2] != 0.0f)) {
         /* capped at min(max_weight, 2^16): the int64 fixed-point sums cannot overflow (the GPU
          * library's RayConst::w0_cap); an origin-only scan (zero axis) keeps the weight 1 */
         const float cap = c->p.max_weight > 0.0f && c->p.max_weight < TSDF_W0_CAP
@@ -709,9 +726,10 @@ static void* mt_walk(void* arg) {
     mt_job* j = (mt_job*)arg;
     tsdf_ctx* c = j->c;
     for (uint64_t i = j->i0; i < j->i1 && !j->fail; i++) {
-        float px, py, pz;
+        float px, py, pz, bw = 0.0f;
         const char* q = j->base + i * j->point_step + j->xyz_offset;
         mt_point(q, j->xyz_is_f64, &px, &py, &pz);
+        if (c->mg_on) memcpy(&bw, q + 12, sizeof bw);
         int64_t r;
         if (c->sem == TSDF_SEM_VDBFUSION_F64) {
             double pd[3] = {px, py, pz};
@@ -719,7 +737,7 @@ static void* mt_walk(void* arg) {
             r = walk_ray_vdb(c, pd, j->origin, visit_bucket, j);
         } else {
             r = c->sem == TSDF_SEM_VOXBLOX
-                    ? walk_ray_vb(c, px, py, pz, j->ox, j->oy, j->oz, visit_bucket, j)
+                    ? walk_ray_vb(c, px, py, pz, j->ox, j->oy, j->oz, bw, visit_bucket, j)
                     : walk_ray(c, px, py, pz, j->ox, j->oy, j->oz, visit_bucket, j);
         }
         if (r >= 0) j->rays++;
@@ -806,6 +824,129 @@ int tsdf_oracle_set_threads(tsdf_ctx* c, int n) {
     return TSDF_OK;
 }
 
+
+/* ---- Voxblox MergedTsdfIntegrator: the bundling pre-pass (tsdf_params.voxblox_method) ----------
+ *
+ * voxblox (ethz-asl/voxblox, unpinned; not in /root/reference -- SURVEY §8a9), restated:
+ *   bundleRays:     for every point (index order: integration_order_mode "sorted"):
+ *                   isPointValid (as walk_ray_vb: d = |p - o|, < min_range dropped, > max_range a
+ *                   clearing point if allow_clear, else dropped); its voxel
+ *                   getGridIndexFromPoint(p, 1/vs) = floor(p / vs + kCoordinateEpsilon) goes to
+ *                   clear_map or voxel_map, each voxel keeping its points in visiting order
+ *   integrateVoxel: per map entry: merged = 0, W = 0; for each point: w = getVoxelWeight (1 or
+ *                   1/z^2, walk_ray_vb's w0); w < kEpsilon (1e-6) -> skipped;
+ *                   merged = (merged W + (p - o) w) / (W + w) per component; W += w;
+ *                   a clearing entry stops after its first kept point.  Then ONE ray from o to
+ *                   o + merged, clearing as its map, carrying the weight W (updateTsdfVoxel's
+ *                   `weight`; the dropoff multiplies it per voxel)
+ *   enable_anti_grazing = false (voxblox's default): no ray skips voxels of other bundles.
+ * Stated deviations: the merge runs on p - o in the world frame (upstream on the
+ * sensor-frame point_C, rotated back: equal in exact arithmetic); bundles are formed in cloud
+ * order (upstream's default "mixed" order visits a bundle's points in another fixed order, which
+ * only changes the rounding of the running mean); voxel indices beyond +-2^20 drop the point; a
+ * bundle's weight is capped at TSDF_MG_W_CAP (2^20) so the exact fixed-point sums cannot overflow;
+ * the bundles' rays update the field in the order of their first points, through the same
+ * scan-fused fuse as SimpleTsdfIntegrator (deviation 4). */
+#define MG_W_CAP 1048576.0f
+#define MG_VOX_LIM (1 << 20)
+
+typedef struct { uint64_t key; uint32_t i; } mg_ent;
+
+static int cmp_mg(const void* a, const void* b) {
+    const mg_ent* x = (const mg_ent*)a;
+    const mg_ent* y = (const mg_ent*)b;
+    if (x->key != y->key) return x->key < y->key ? -1 : 1;
+    return x->i < y->i ? -1 : (x->i > y->i);
+}
+
+/* the scan's bundled rays as 16-B records (x, y, z, w), w < 0: clearing; *nb of them */
+static float* mg_bundle(tsdf_ctx* c, const char* base, uint64_t n, uint32_t point_step,
+                        uint32_t xyz_offset, int32_t xyz_is_f64, float ox, float oy, float oz,
+                        uint64_t* nb) {
+    mg_ent* e = (mg_ent*)malloc((n ? n : 1) * sizeof(mg_ent));
+    float* w = (float*)malloc((n ? n : 1) * sizeof(float));
+    float* d = (float*)malloc((n ? n : 1) * 3 * sizeof(float));
+    float* out = (float*)malloc((n ? n : 1) * 4 * sizeof(float));
+    *nb = 0;
+    if (!e || !w || !d || !out) {
+        free(e); free(w); free(d); free(out);
+        return NULL;
+    }
+    const int have_axis = c->zax[0] != 0.0f || c->zax[1] != 0.0f || c->zax[2] != 0.0f;
+    const float cap = c->p.max_weight > 0.0f && c->p.max_weight < TSDF_W0_CAP ? c->p.max_weight
+                                                                            : TSDF_W0_CAP;
+    uint64_t m = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        float p[3];
+        mt_point(base + i * point_step + xyz_offset, xyz_is_f64, &p[0], &p[1], &p[2]);
+        const float dx = p[0] - ox, dy = p[1] - oy, dz = p[2] - oz;
+        const float depth = sqrtf(dx * dx + (dy * dy + dz * dz));
+        if (!(depth > 0.0f) || depth < (float)c->p.min_range) continue;
+        int clearing = 0;
+        if (depth > (float)c->p.max_range) {
+            if (!c->p.allow_clear) continue;
+            clearing = 1;
+        }
+        int32_t v[3];
+        int ok = 1;
+        for (int a = 0; a < 3; a++) {
+            const float f = floorf(p[a] * c->inv_vs + 1e-6f);
+            ok &= f > -(float)MG_VOX_LIM && f < (float)MG_VOX_LIM;
+            v[a] = ok ? (int32_t)f : 0;
+        }
+        if (!ok) continue;
+        float pw = 1.0f;
+        if (c->p.depth_weight && have_axis) {
+            const float z = fabsf(c->zax[0] * dx + (c->zax[1] * dy + c->zax[2] * dz));
+            pw = z > 1e-6f ? fminf(1.0f / (z * z), cap) : 0.0f;
+        }
+        w[i] = pw;
+        d[3 * i] = dx; d[3 * i + 1] = dy; d[3 * i + 2] = dz;
+        /* key: clearing bit, then the biased 21-bit axes (z, y, x), as the GPU pre-pass */
+        e[m].key = ((uint64_t)clearing << 63) | ((uint64_t)(uint32_t)(v[2] + MG_VOX_LIM) << 42) |
+                   ((uint64_t)(uint32_t)(v[1] + MG_VOX_LIM) << 21) | (uint64_t)(uint32_t)(v[0] + MG_VOX_LIM);
+        e[m].i = (uint32_t)i;
+        m++;
+    }
+    qsort(e, m, sizeof(mg_ent), cmp_mg);
+    /* bundles in the order of their first points */
+    uint64_t nr = 0;
+    for (uint64_t j = 0; j < m;) {
+        uint64_t q = j;
+        const int clearing = (int)(e[j].key >> 63);
+        float mx = 0.0f, my = 0.0f, mz = 0.0f, mw = 0.0f;
+        for (; q < m && e[q].key == e[j].key; q++) {
+            const uint32_t i = e[q].i;
+            const float pw = w[i];
+            if (pw < 1e-6f || (clearing && mw > 0.0f)) continue; /* kEpsilon; clearing: first only */
+            const float nw = mw + pw;
+            mx = (mx * mw + d[3 * i] * pw) / nw;
+            my = (my * mw + d[3 * i + 1] * pw) / nw;
+            mz = (mz * mw + d[3 * i + 2] * pw) / nw;
+            mw = mw + pw;
+        }
+        if (mw > 0.0f) {
+            float* r = out + 4 * nr;
+            r[0] = ox + mx; r[1] = oy + my; r[2] = oz + mz;
+            const float bw = mw < MG_W_CAP ? mw : MG_W_CAP;
+            r[3] = clearing ? -bw : bw;
+            e[nr].i = e[j].i; /* reuse: first point of bundle nr */
+            e[nr].key = nr;
+            nr++;
+        }
+        j = q;
+    }
+    /* order the bundles by first point (a stable order independent of the voxel keys) */
+    for (uint64_t k = 0; k < nr; k++) e[k].key = ((uint64_t)e[k].i << 32) | e[k].key;
+    qsort(e, nr, sizeof(mg_ent), cmp_mg);
+    float* res = (float*)malloc((nr ? nr : 1) * 4 * sizeof(float));
+    if (res)
+        for (uint64_t k = 0; k < nr; k++) memcpy(res + 4 * k, out + 4 * (e[k].key & 0xFFFFFFFFull), 16);
+    free(e); free(w); free(d); free(out);
+    *nb = nr;
+    return res;
+}
+
 static int integrate_scan(tsdf_ctx* c, const void* pts, uint64_t n, uint32_t point_step,
                           uint32_t xyz_offset, int32_t xyz_is_f64, const double origin[3]);
 
@@ -839,6 +980,21 @@ static int integrate_scan(tsdf_ctx* c, const void* pts, uint64_t n, uint32_t poi
     if (point_step < need || xyz_offset > point_step - need)
         return set_err(c, TSDF_EINVAL, "point_step/xyz_offset inconsistent");
     const float ox = (float)origin[0], oy = (float)origin[1], oz = (float)origin[2];
+    if (c->sem == TSDF_SEM_VOXBLOX && c->p.voxblox_method == TSDF_VB_MERGED && !c->mg_on) {
+        /* MergedTsdfIntegrator: walk the scan's bundled rays instead of its points */
+        uint64_t nb = 0;
+        float* b = mg_bundle(c, (const char*)pts, n, point_step, xyz_offset, xyz_is_f64, ox, oy, oz,
+                             &nb);
+        if (!b) return set_err(c, TSDF_ENOMEM, "oracle allocation failed");
+        c->mg_on = 1;
+        for (int t = 0; t < c->n_thr; t++) c->sub[t]->mg_on = 1;
+        const int rc = integrate_scan(c, b, nb, 16, 0, 0, origin);
+        c->mg_on = 0;
+        for (int t = 0; t < c->n_thr; t++) c->sub[t]->mg_on = 0;
+        free(b);
+        if (rc == TSDF_OK) c->st.n_points_in += n - nb; /* count the scan's points, not bundles */
+        return rc;
+    }
     c->scan_id++;
     c->st.n_voxels_last = 0;
     int fail = 0;
@@ -878,8 +1034,10 @@ static int integrate_scan(tsdf_ctx* c, const void* pts, uint64_t n, uint32_t poi
             memcpy(f, q, sizeof f);
             px = f[0]; py = f[1]; pz = f[2];
         }
+        float bw = 0.0f;
+        if (c->mg_on) memcpy(&bw, q + 12, sizeof bw);
         const int64_t r = c->sem == TSDF_SEM_VOXBLOX
-                              ? walk_ray_vb(c, px, py, pz, ox, oy, oz, visit_accum, &fail)
+                              ? walk_ray_vb(c, px, py, pz, ox, oy, oz, bw, visit_accum, &fail)
                               : walk_ray(c, px, py, pz, ox, oy, oz, visit_accum, &fail);
         if (r >= 0) c->st.n_rays_total++;
     }
@@ -1106,7 +1264,7 @@ int64_t tsdf_oracle_ray_voxels(tsdf_ctx* c, const float p[3], const double origi
     const float ox = (float)origin[0], oy = (float)origin[1], oz = (float)origin[2];
     const double pd[3] = {p[0], p[1], p[2]};
     int64_t v = c->sem == TSDF_SEM_VOXBLOX
-                    ? walk_ray_vb(c, p[0], p[1], p[2], ox, oy, oz, visit_record, &r)
+                    ? walk_ray_vb(c, p[0], p[1], p[2], ox, oy, oz, 0.0f, visit_record, &r)
                 : c->mode == ORACLE_MODE_VDB_LITERAL
                     ? walk_ray_vdb(c, pd, origin, visit_record, &r)
                     : walk_ray(c, p[0], p[1], p[2], ox, oy, oz, visit_record, &r);

@@ -22,8 +22,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=32)
     ap.add_argument("--sectors", type=int, default=0,
                     help="N > 1: the live N-GPU input path rehearsed on one GPU -- N sector contexts "
-                         "fed by tsdf_integrate_sectors (host classification + split, 1/N of each "
-                         "scan's points to each context)")
+                         "fed by tsdf_integrate_sectors (--sector-input: fanout = one H2D and "
+                         "device copies, h2d = one H2D per context, split = host classification)")
+    ap.add_argument("--sector-input", default="fanout", choices=("fanout", "h2d", "split"),
+                    help="tsdf_params.sector_input of the N contexts (ABI v8)")
     ap.add_argument("--semantics", default="vdbfusion_f64")
     ap.add_argument("--max-batch", type=int, default=32)
     args = ap.parse_args()
@@ -47,7 +49,8 @@ def main():
     n = max(1, args.sectors)
     vols = [HipTSDFVolume(0.05, 0.15, max_points=1 << 17, max_bricks=1 << 20,
                           max_batch=args.max_batch, semantics=args.semantics,
-                          n_sectors=n if n > 1 else 0, sector=k) for k in range(n)]
+                          n_sectors=n if n > 1 else 0, sector=k,
+                          sector_input=args.sector_input) for k in range(n)]
     vol = vols[0]
     lib = vol._lib
     ctxs = (C.c_void_p * n)(*[v._ctx.value for v in vols])
@@ -73,6 +76,7 @@ def main():
                                 ("tsdf_integrate_sectors over %d contexts on ONE GPU" % n if n > 1
                                  else "tsdf_integrate"),
                       "value": round(args.scans / dt, 2), "scans": args.scans, "sectors": n,
+                      "sector_input": args.sector_input if n > 1 else None,
                       "semantics": args.semantics, "max_batch": args.max_batch,
                       "bytes_per_scan_host": int(clouds[0].nbytes),
                       "h2d_bytes_per_scan": int(clouds[0].shape[0] * 12),

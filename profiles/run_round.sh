@@ -4,6 +4,10 @@
 #   perf:  2. PMC counters per kernel (separate --pmc passes, no tracing) -> $OUT/pmc/{summary.txt,traffic.json}
 #          3. the bench line, roofline.traffic read from step 2           -> $OUT/bench.json
 #          4. rocprofv3 --kernel-trace --stats of the same bench command  -> $OUT/kernel_stats.csv
+#          5. the same with --pipeline 0 (every kernel alone: the roofline kernel's duration is the
+#             serial leg's)                                              -> $OUT/kernel_stats_serial.csv
+#   copy $OUT/traffic.json to profiles/traffic_r0N.json afterwards (bench.py's default; it carries
+#   the library's sha, so a later kernel change shows as stale: roofline.traffic_source)
 #   bash profiles/run_round.sh <out> [tests|perf|all]
 # Every GPU step has its own time limit; the chain stops at the first failure.
 set -e
@@ -24,6 +28,10 @@ if [ "$WHAT" != tests ]; then
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/rocprof" -o bench -- \
       python3 bench.py --no-cpu --traffic-json "$OUT/traffic.json" > "$OUT/rocprof_bench.out" 2>&1
   find "$OUT/rocprof" -name '*kernel_stats.csv' -exec cp {} "$OUT/kernel_stats.csv" \;
+  rm -rf "$OUT/rocprof"
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/rocprof" -o bench -- \
+      python3 bench.py --no-cpu --pipeline 0 --traffic-json "$OUT/traffic.json" > "$OUT/rocprof_serial.out" 2>&1
+  find "$OUT/rocprof" -name '*kernel_stats.csv' -exec cp {} "$OUT/kernel_stats_serial.csv" \;
   rm -rf "$OUT/rocprof"
   cat "$OUT/bench.json"
   head -8 "$OUT/kernel_stats.csv"

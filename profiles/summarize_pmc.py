@@ -43,6 +43,14 @@ def main(root):
                        "correction per MI355X_MICROARCH.md, calibrated on this box's counters "
                        "for 4/8/12/16-B contiguous reads (exact) and random 4-B gathers (128 B, "
                        "one L2 line, per gather): profiles/r03/calib/calib.json)"}
+    # the build the counters were measured on: bench.py reports roofline.traffic only when this
+    # matches the library it loaded (a kernel change makes the file stale visibly, not silently)
+    import hashlib
+    lib = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                       "noetic-slam_amd", "lib", "libtsdf_hip.so")
+    lib = os.environ.get("TSDF_HIP_LIB") or lib
+    with open(lib, "rb") as fh:
+        traffic["lib_sha16"] = hashlib.sha256(fh.read()).hexdigest()[:16]
     for kname, d in out.items():
         if "FETCH_SIZE" in d and "WRITE_SIZE" in d and not kname.startswith("k_fill"):
             f, w = d["FETCH_SIZE"] * 1024.0, d["WRITE_SIZE"] * 1024.0

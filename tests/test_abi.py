@@ -37,7 +37,7 @@ def test_hip_library_exports_every_declared_symbol():
     missing = [f for f in header_functions() if f not in syms]
     assert not missing, missing
     lib = load_hip_library()
-    assert lib.tsdf_abi_version() == 7
+    assert lib.tsdf_abi_version() == 8
 
 
 def test_hip_library_is_gfx950_code():
@@ -64,8 +64,44 @@ def test_default_params_roundtrip():
     assert p.space_carving == 0 and np.isinf(p.max_range)
     assert p.walk == _abi.WALK_TWO == 0  # ABI v5: two walks unless the single walk is asked for
     assert p.depth_weight == 1  # ABI v6: Voxblox's 1/z^2 weight, upstream's default
-    # the ctypes mirror ends where the C struct ends (ABI v6 appended `depth_weight`)
-    assert _abi.TsdfParams._fields_[-1][0] == "depth_weight"
+    assert p.voxblox_method == _abi.VB_METHODS["simple"] == 0  # ABI v8
+    assert p.sector_input == _abi.SECTOR_INPUTS["fanout"] == 0
+    assert p.semantics == _abi.SEM_VDBFUSION_F64  # ABI v8 default
+    # the ctypes mirror ends where the C struct ends (ABI v8 appended `sector_input`)
+    assert _abi.TsdfParams._fields_[-1][0] == "sector_input"
+
+
+def test_struct_layouts_match_the_header(tmp_path):
+    """Every field of tsdf_params / tsdf_stats / tsdf_os_format sits at the same offset, with the
+    same size, in the ctypes mirror as in include/tsdf_hip.h compiled by the C compiler."""
+    import subprocess
+    from tsdf_map import _abi
+    structs = {"tsdf_params": _abi.TsdfParams, "tsdf_stats": _abi.TsdfStats,
+               "tsdf_os_format": _abi.OsFormat}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "tsdf_hip.h"', 'int main(void) {']
+    for cname, py in structs.items():
+        lines.append('printf("%s sizeof %%zu\\n", sizeof(%s));' % (cname, cname))
+        for f, _ in py._fields_:
+            lines.append('printf("%s %s %%zu %%zu\\n", offsetof(%s, %s), sizeof(((%s*)0)->%s));'
+                         % (cname, f, cname, f, cname, f))
+    lines.append("return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.check_call(["gcc", "-I", os.path.join(REPO, "include"), str(src), "-o", str(exe)])
+    out = subprocess.check_output([str(exe)], text=True).split("\n")
+    got = {}
+    for ln in out:
+        parts = ln.split()
+        if len(parts) == 3 and parts[1] == "sizeof":
+            got[(parts[0], "sizeof")] = int(parts[2])
+        elif len(parts) == 4:
+            got[(parts[0], parts[1])] = (int(parts[2]), int(parts[3]))
+    for cname, py in structs.items():
+        assert got[(cname, "sizeof")] == ctypes.sizeof(py), cname
+        for f, _ in py._fields_:
+            fld = getattr(py, f)
+            assert got[(cname, f)] == (fld.offset, fld.size), (cname, f)
 
 
 def test_header_kernel_kinds_match_the_binding():

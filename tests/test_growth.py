@@ -46,7 +46,7 @@ def test_full_c1_scan_from_64_bricks(scan0):
 
 
 @pytest.mark.parametrize("pipeline", [False, True, 2])
-@pytest.mark.parametrize("semantics", ["vdbfusion", "voxblox"])
+@pytest.mark.parametrize("semantics", ["vdbfusion_f64", "vdbfusion", "voxblox"])
 def test_host_path_sequence_grows(sim, pipeline, semantics):
     """Host-pointer scans in 2-scan batches: the staging checkpoint replays before overwriting."""
     kw = dict(max_bricks=128, max_batch=2, pipeline=pipeline, semantics=semantics)
@@ -63,7 +63,8 @@ def test_host_path_sequence_grows(sim, pipeline, semantics):
     assert g.stats()["n_grows"] >= 2
 
 
-def test_device_batches_grow(sim):
+@pytest.mark.parametrize("semantics", ["vdbfusion_f64", "vdbfusion"])
+def test_device_batches_grow(sim, semantics):
     import torch
     scans = [sim.scan(k) for k in (0, 5, 9, 14, 22)]
     allp = np.concatenate([p for p, _ in scans])
@@ -71,10 +72,10 @@ def test_device_batches_grow(sim):
     org = np.stack([o for _, o in scans])
     d = torch.from_numpy(allp).to("cuda:0")
     torch.cuda.synchronize()
-    g = hip(max_bricks=1000, max_batch=2)
+    g = hip(max_bricks=1000, max_batch=2, semantics=semantics)
     g.integrate_batch_device(d.data_ptr(), offs, org)
     g.sync()
-    o = ora()
+    o = ora(semantics=semantics)
     for p, q in scans:
         o.integrate(p, q)
     assert bitwise(g, o)

@@ -117,13 +117,14 @@ def emulated_reduce_host(vols):
     return splits
 
 
-def test_border_reduce_matches_oracle_bitwise(sim):
+@pytest.mark.parametrize("semantics", ["vdbfusion_f64", "vdbfusion"])
+def test_border_reduce_matches_oracle_bitwise(sim, semantics):
     from tsdf_map import bricks_to_voxels
     world, yaw0 = 3, 0.25
     dev = torch.device("cuda", 0)
-    g = [hip(n_sectors=world, sector=r, sector_yaw0=yaw0) for r in range(world)]
-    o = [ora(n_sectors=world, sector=r, sector_yaw0=yaw0) for r in range(world)]
-    ref = ora()
+    g = [hip(n_sectors=world, sector=r, sector_yaw0=yaw0, semantics=semantics) for r in range(world)]
+    o = [ora(n_sectors=world, sector=r, sector_yaw0=yaw0, semantics=semantics) for r in range(world)]
+    ref = ora(semantics=semantics)
     rounds = [(0, 1), (2, 40)]
     for i, ks in enumerate(rounds):
         for k in ks:
@@ -148,17 +149,18 @@ def test_border_reduce_matches_oracle_bitwise(sim):
     assert np.max(np.abs(ms - rs)) <= 1e-5
 
 
-def test_sharded_contexts_local_reduce_bitwise(sim):
+@pytest.mark.parametrize("semantics", ["vdbfusion_f64", "vdbfusion"])
+def test_sharded_contexts_local_reduce_bitwise(sim, semantics):
     """tsdf_create_sharded + tsdf_integrate_sectors + tsdf_border_reduce_local: one process
     driving n sector contexts (here all on GPU 0; on a node, one per GPU, tiles between GPUs by
     peer copy) gives every context the oracle's reduced field bit for bit, twice over."""
     from tsdf_map import HipTSDFVolume, border_reduce_local, integrate_sectors
     world, yaw0 = 4, 0.6
     g = HipTSDFVolume.sharded(world, VS, TAU, device_ids=[0] * world, sector_yaw0=yaw0,
-                              max_bricks=1 << 18, max_batch=4)
+                              max_bricks=1 << 18, max_batch=4, semantics=semantics)
     assert [v.params.sector for v in g] == list(range(world))
     assert all(v.params.n_sectors == world and v.params.device_id == 0 for v in g)
-    o = [ora(n_sectors=world, sector=r, sector_yaw0=yaw0) for r in range(world)]
+    o = [ora(n_sectors=world, sector=r, sector_yaw0=yaw0, semantics=semantics) for r in range(world)]
     moved = 0
     for ks in ((0, 1, 2), (30,)):
         for k in ks:
@@ -226,16 +228,21 @@ def test_border_reduce_two_processes(tmp_path, sim):
     assert np.max(np.abs(ms - rs)) <= 1e-5
 
 
-@pytest.mark.parametrize("n,f64", [(3, False), (4, True), (8, False)])
-def test_integrate_sectors_host_split_bitwise(sim, n, f64):
-    """tsdf_integrate_sectors (the live N-GPU input): one host cloud classified and
-    split on the host over n sector contexts equals each context integrating the full cloud with
-    its in-kernel sector filter (the oracle), bit for bit; the sectors' rays add up to the scan."""
+@pytest.mark.parametrize("n,f64,mode", [(3, False, "split"), (4, True, "split"),
+                                         (8, False, "split"), (3, False, "fanout"),
+                                         (4, True, "fanout"), (8, False, "h2d")])
+def test_integrate_sectors_bitwise(sim, n, f64, mode):
+    """tsdf_integrate_sectors (the live N-GPU input) equals each context integrating
+    the full cloud with its in-kernel sector filter (the oracle), bit for bit, for every transfer
+    (tsdf_params.sector_input): split (host classification, each context gets its sector's
+    points), fanout (one H2D, device-to-device copies to the other contexts) and h2d (one H2D per
+    context from one packed buffer)."""
     from tsdf_map import integrate_sectors
     yaw0 = 0.4
-    g = [hip(n_sectors=n, sector=r, sector_yaw0=yaw0, max_batch=2) for r in range(n)]
+    g = [hip(n_sectors=n, sector=r, sector_yaw0=yaw0, max_batch=2, sector_input=mode)
+         for r in range(n)]
     o = [ora(n_sectors=n, sector=r, sector_yaw0=yaw0) for r in range(n)]
-    rays = 0
+    rays = total = 0
     for k in (0, 1, 9):
         pts, org = sim.scan(k)
         pts = np.ascontiguousarray(pts[::2])
@@ -251,7 +258,41 @@ def test_integrate_sectors_host_split_bitwise(sim, n, f64):
         for v in o:
             v.integrate(pts, org)
         rays += pts.shape[0] - 3
+        total += pts.shape[0]
     for r in range(n):
         g[r].sync()
         assert voxels_equal_bitwise(g[r].export_voxels(), o[r].export_voxels()), r
-    assert sum(v.stats()["n_points_in"] for v in g) == rays  # each point went to one context
+    if mode == "split":
+        assert sum(v.stats()["n_points_in"] for v in g) == rays  # each point went to one context
+    else:
+        assert all(v.stats()["n_points_in"] == total for v in g)  # every context got the cloud
+
+
+def test_integrate_sectors_voxblox_merged(sim):
+    """MergedTsdfIntegrator bundles the whole scan before the sector filter, so the sectors take the
+    fan-out (a requested host split is overridden): every context equals its oracle twin."""
+    from tsdf_map import integrate_sectors
+    n, yaw0 = 3, 0.2
+    kw = dict(semantics="voxblox", method="merged", use_const_weight=False)
+    g = [hip(n_sectors=n, sector=r, sector_yaw0=yaw0, max_batch=2, sector_input="split", **kw)
+         for r in range(n)]
+    o = [ora(n_sectors=n, sector=r, sector_yaw0=yaw0, **kw) for r in range(n)]
+    for k in (0, 4):
+        pts, org = sim.scan(k)
+        q = np.array([0.0, 0.05 * k, 0.0, 1.0])
+        integrate_sectors(g, np.ascontiguousarray(pts[::2]), np.concatenate([org, q]))
+        for v in o:
+            v.integrate(np.ascontiguousarray(pts[::2]), np.concatenate([org, q]))
+    for r in range(n):
+        g[r].sync()
+        assert voxels_equal_bitwise(g[r].export_voxels(), o[r].export_voxels()), r
+
+
+def test_sharded_contexts_report_peer_reach():
+    """tsdf_create_sharded enables peer access between distinct devices; contexts on one device
+    reach each other directly (peer_mask has every bit)."""
+    from tsdf_map import HipTSDFVolume
+    g = HipTSDFVolume.sharded(3, VS, TAU, device_ids=[0, 0, 0], max_bricks=1 << 12, max_batch=2)
+    assert all(v.stats()["peer_mask"] == 0b111 for v in g)
+    for v in g:
+        v.close()
