@@ -315,11 +315,16 @@ int tsdf_extract_mesh(tsdf_ctx* ctx, float min_weight, float* tri, uint64_t cap,
 int tsdf_mc_table(uint8_t* out);
 
 /* ABI v6: marching-cubes case tables.  TSDF_MC_GENERATED: the table above (ambiguous faces paired
- * around their inside corners, so neighbouring cubes agree).  TSDF_MC_LORENSEN: the classic
- * Lorensen / Bourke table that VDBFusion's extract_triangle_mesh uses (the same triangles for
- * unambiguous cases; ambiguous faces are split the classic way, which can leave cracks). */
+ * around their inside corners, so neighbouring cubes agree).  TSDF_MC_LORENSEN (ABI v8: the
+ * literal data): the published Lorensen / Bourke triangle table that VDBFusion's
+ * extract_triangle_mesh compiles in (include/tsdf_mc_tables.h), renumbered into this library's
+ * corners and edges with its triangles' order and winding kept (ambiguous faces are split the
+ * classic way, which can leave cracks).  TSDF_MC_LORENSEN_RULE: this library's restatement of the
+ * classic ambiguity rule (round 3's TSDF_MC_LORENSEN), for comparison. */
 #define TSDF_MC_GENERATED 0
 #define TSDF_MC_LORENSEN 1
+#define TSDF_MC_LORENSEN_RULE 2
+#define TSDF_MC_TABLES 3
 int tsdf_extract_mesh_table(tsdf_ctx* ctx, float min_weight, int32_t table, float* tri,
                             uint64_t cap, uint64_t* n_tri);
 /* The case table `table` in tsdf_mc_table's layout (edges in this library's numbering). */

@@ -27,6 +27,7 @@
 #include <vector>
 
 #include "../../include/tsdf_hip.h"
+#include "../../include/tsdf_mc_tables.h"
 #include "pack_pool.h"
 #include "tsdf_device.h"
 
@@ -34,6 +35,7 @@ using namespace tsdf;
 
 static_assert(TSDF_MAX_BATCH == MAX_BATCH, "header and device batch limits differ");
 static_assert(TSDF_TILE_WORDS == TILE_WORDS && TSDF_MAX_WORLD == MAX_WORLD, "border tile layout differs");
+static_assert(TSDF_MC_TABLES == MC_TABLES, "marching-cubes table count differs");
 
 namespace {
 
@@ -896,8 +898,8 @@ struct McTable {
     uint8_t edge[12][2];   // edge -> (a, b), b = a | axis bit
 };
 
-// lorensen: the classic table's ambiguity rule instead (Lorensen & Cline's complement symmetry,
-// the table VDBFusion's extract_triangle_mesh transcribes): an ambiguous face pairs its crossings
+// lorensen: the classic table's ambiguity rule instead (Lorensen & Cline's complement symmetry;
+// TSDF_MC_LORENSEN_RULE, a restatement of the published table's topology): an ambiguous face pairs its crossings
 // around the inside corners when at most 4 corners of the cube are inside, around the outside
 // corners otherwise; the two cubes sharing a face can then disagree (the classic cracks).
 static McTable build_mc_table(bool lorensen) {
@@ -971,9 +973,28 @@ static McTable build_mc_table(bool lorensen) {
     return M;
 }
 
+// TSDF_MC_LORENSEN: the published table (include/tsdf_mc_tables.h, VDBFusion's), renumbered into
+// this library's corners and edges: Bourke vertex v -> corner kV[v], edge e -> edge kE[e]; the
+// triangles keep their order and winding.
+static McTable literal_mc_table() {
+    McTable M = build_mc_table(false);  // the edge list
+    static const int kV[8] = {0, 1, 3, 2, 4, 5, 7, 6};
+    static const int kE[12] = {0, 5, 1, 4, 2, 7, 3, 6, 8, 9, 11, 10};
+    for (int b = 0; b < 256; b++) {
+        int k = 0;
+        for (int v = 0; v < 8; v++)
+            if (b >> v & 1) k |= 1 << kV[v];
+        int nt = 0;
+        for (int i = 0; i < 15 && tsdf_mc_tri_table[b][i] >= 0; i += 3, nt++)
+            for (int j = 0; j < 3; j++) M.tab[k][1 + 3 * nt + j] = (uint8_t)kE[tsdf_mc_tri_table[b][i + j]];
+        M.tab[k][0] = (uint8_t)nt;
+    }
+    return M;
+}
+
 static const McTable& mc_table(int which = TSDF_MC_GENERATED) {
-    static const McTable G = build_mc_table(false), L = build_mc_table(true);
-    return which == TSDF_MC_LORENSEN ? L : G;
+    static const McTable G = build_mc_table(false), L = literal_mc_table(), R = build_mc_table(true);
+    return which == TSDF_MC_LORENSEN ? L : which == TSDF_MC_LORENSEN_RULE ? R : G;
 }
 
 extern "C" {
@@ -1260,10 +1281,9 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
     }
     HIPCHK(c, hipStreamSynchronize(c->stream));
     {
-        static uint8_t both[2][256][32];
-        std::memcpy(both[0], mc_table(TSDF_MC_GENERATED).tab, sizeof both[0]);
-        std::memcpy(both[1], mc_table(TSDF_MC_LORENSEN).tab, sizeof both[1]);
-        HIPCHK(c, upload_mc_table(both, mc_table().edge));
+        static uint8_t all[TSDF_MC_TABLES][256][32];
+        for (int t = 0; t < TSDF_MC_TABLES; t++) std::memcpy(all[t], mc_table(t).tab, sizeof all[t]);
+        HIPCHK(c, upload_mc_table(all, mc_table().edge));
     }
     return TSDF_OK;
 }
@@ -2012,7 +2032,7 @@ int tsdf_mc_table(uint8_t* out) {
 }
 
 int tsdf_mc_table_of(int32_t table, uint8_t* out) {
-    if (!out || (table != TSDF_MC_GENERATED && table != TSDF_MC_LORENSEN)) return TSDF_EINVAL;
+    if (!out || table < 0 || table >= TSDF_MC_TABLES) return TSDF_EINVAL;
     std::memcpy(out, mc_table(table).tab, sizeof(mc_table(table).tab));
     return TSDF_OK;
 }
@@ -2024,7 +2044,7 @@ int tsdf_extract_mesh(tsdf_ctx* c, float min_weight, float* tri, uint64_t cap, u
 int tsdf_extract_mesh_table(tsdf_ctx* c, float min_weight, int32_t table, float* tri, uint64_t cap,
                             uint64_t* n_tri) {
     if (!c || !n_tri) return TSDF_EINVAL;
-    if (table != TSDF_MC_GENERATED && table != TSDF_MC_LORENSEN)
+    if (table < 0 || table >= TSDF_MC_TABLES)
         return fail(c, TSDF_EINVAL, "unknown marching-cubes table %d", table);
     uint64_t nb = 0;
     int rc = pool_bricks(c, &nb);

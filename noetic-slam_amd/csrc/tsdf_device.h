@@ -386,7 +386,8 @@ hipError_t launch_os_xyz(const uint32_t* d_range, uint64_t n, const float* d_dir
                          const float* d_off, const OsPose& P, float* d_xyz, hipStream_t st);
 // marching cubes (tsdf_mesh.hip)
 // both case tables (TSDF_MC_GENERATED, TSDF_MC_LORENSEN); `tab` selects one per launch
-hipError_t upload_mc_table(const uint8_t tab[2][256][32], const uint8_t edge[12][2]);
+constexpr int MC_TABLES = 3;  // include/tsdf_hip.h TSDF_MC_TABLES
+hipError_t upload_mc_table(const uint8_t tab[MC_TABLES][256][32], const uint8_t edge[12][2]);
 hipError_t launch_mesh_count(const Table& T, const Pool& Pl, const uint64_t* d_keys, uint32_t nb,
                              float min_weight, int tab, uint32_t* d_counts, hipStream_t st);
 hipError_t launch_mesh_emit(const Table& T, const Pool& Pl, const uint64_t* d_keys, uint32_t nb,

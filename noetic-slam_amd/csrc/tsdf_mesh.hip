@@ -19,7 +19,7 @@
 
 namespace tsdf {
 
-__constant__ uint8_t c_mc[2][256][32];  // per table (TSDF_MC_*): [case][0] = triangles, then 3 edge ids each
+__constant__ uint8_t c_mc[MC_TABLES][256][32];  // per table (TSDF_MC_*): [case][0] = triangles, then 3 edge ids each
 __constant__ uint8_t c_edge[12][2];  // edge -> corners (a, b), b = a | axis bit
 
 constexpr int MESH_THREADS = 512;
@@ -145,8 +145,8 @@ __global__ __launch_bounds__(MESH_THREADS) void k_mesh_emit(Table T, Pool Pl,
     }
 }
 
-hipError_t upload_mc_table(const uint8_t tab[2][256][32], const uint8_t edge[12][2]) {
-    hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(c_mc), tab, 2 * 256 * 32);
+hipError_t upload_mc_table(const uint8_t tab[MC_TABLES][256][32], const uint8_t edge[12][2]) {
+    hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(c_mc), tab, MC_TABLES * 256 * 32);
     if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(c_edge), edge, 12 * 2);
     return e;
 }

@@ -29,7 +29,7 @@ SEMANTICS = {"vdbfusion": SEM_VDBFUSION, "voxblox": SEM_VOXBLOX,
 KERNEL_KINDS = ("count", "compact", "place", "integrate", "walk", "spans")
 WALK_TWO = 0     # tsdf_params.walk: k_count + k_place (default)
 WALK_SINGLE = 1  # k_walk + k_spans when the band allows it
-MC_TABLES = {"generated": 0, "lorensen": 1}  # TSDF_MC_GENERATED, TSDF_MC_LORENSEN
+MC_TABLES = {"generated": 0, "lorensen": 1, "lorensen_rule": 2}  # TSDF_MC_*
 VB_METHODS = {"simple": 0, "merged": 1}  # tsdf_params.voxblox_method (TSDF_VB_*)
 SECTOR_INPUTS = {"fanout": 0, "h2d": 1, "split": 2}  # tsdf_params.sector_input
 

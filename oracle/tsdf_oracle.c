@@ -50,6 +50,7 @@
 #include <string.h>
 
 #include "../include/tsdf_hip.h"
+#include "../include/tsdf_mc_tables.h"
 
 #define ORACLE_MODE_SCAN_FUSED 0
 #define ORACLE_MODE_SEQUENTIAL 1
@@ -1428,7 +1429,7 @@ int tsdf_border_merge_device(tsdf_ctx* c, const uint32_t* recv, const uint64_t* 
  *   Output: triangle soup, 9 floats per triangle, bricks in (z, y, x) order, cubes by their min
  *   voxel's in-brick index z*64 + y*8 + x, triangles in table order. */
 
-static uint8_t mc_tabs[2][256][32]; /* TSDF_MC_*: [case][0] = triangles, then 3 edge ids each */
+static uint8_t mc_tabs[TSDF_MC_TABLES][256][32]; /* TSDF_MC_*: [case][0] = triangles, then 3 edge ids each */
 static int mc_edge_a[12], mc_edge_b[12];
 static int mc_ready = 0;
 
@@ -1439,7 +1440,7 @@ static int mc_edge_of(int a, int b) {
     return -1;
 }
 
-/* TSDF_MC_LORENSEN: the classic table's ambiguity rule -- an ambiguous face pairs its crossings
+/* TSDF_MC_LORENSEN_RULE: the classic table's ambiguity rule -- an ambiguous face pairs its crossings
  * around the inside corners when at most 4 cube corners are inside, around the outside corners
  * otherwise (Lorensen & Cline's complement symmetry; neighbouring cubes can then disagree) */
 static void mc_build_table(int lorensen, uint8_t mc_tab[256][32]) {
@@ -1500,14 +1501,30 @@ static void mc_build(void) {
         for (int base = 0; base < 8; base++)
             if (!(base & (1 << d))) { mc_edge_a[ne] = base; mc_edge_b[ne] = base | (1 << d); ne++; }
     mc_build_table(0, mc_tabs[TSDF_MC_GENERATED]);
-    mc_build_table(1, mc_tabs[TSDF_MC_LORENSEN]);
+    mc_build_table(1, mc_tabs[TSDF_MC_LORENSEN_RULE]);
+    /* TSDF_MC_LORENSEN: the published table (include/tsdf_mc_tables.h) renumbered: Bourke vertex v
+     * -> corner kv[v], edge e -> edge ke[e]; triangle order and winding kept */
+    {
+        static const int kv[8] = {0, 1, 3, 2, 4, 5, 7, 6};
+        static const int ke[12] = {0, 5, 1, 4, 2, 7, 3, 6, 8, 9, 11, 10};
+        for (int b = 0; b < 256; b++) {
+            int k = 0, nt = 0;
+            for (int v = 0; v < 8; v++)
+                if (b >> v & 1) k |= 1 << kv[v];
+            memset(mc_tabs[TSDF_MC_LORENSEN][k], 0, 32);
+            for (int i = 0; i < 15 && tsdf_mc_tri_table[b][i] >= 0; i += 3, nt++)
+                for (int j = 0; j < 3; j++)
+                    mc_tabs[TSDF_MC_LORENSEN][k][1 + 3 * nt + j] = (uint8_t)ke[tsdf_mc_tri_table[b][i + j]];
+            mc_tabs[TSDF_MC_LORENSEN][k][0] = (uint8_t)nt;
+        }
+    }
     mc_ready = 1;
 }
 
 int tsdf_mc_table(uint8_t* out) { return tsdf_mc_table_of(TSDF_MC_GENERATED, out); }
 
 int tsdf_mc_table_of(int32_t table, uint8_t* out) {
-    if (!out || (table != TSDF_MC_GENERATED && table != TSDF_MC_LORENSEN)) return TSDF_EINVAL;
+    if (!out || table < 0 || table >= TSDF_MC_TABLES) return TSDF_EINVAL;
     if (!mc_ready) mc_build();
     memcpy(out, mc_tabs[table], sizeof mc_tabs[table]);
     return TSDF_OK;
@@ -1520,7 +1537,7 @@ int tsdf_extract_mesh(tsdf_ctx* c, float min_weight, float* tri, uint64_t cap, u
 int tsdf_extract_mesh_table(tsdf_ctx* c, float min_weight, int32_t table, float* tri,
                             uint64_t cap, uint64_t* n_tri) {
     if (!c || !n_tri) return TSDF_EINVAL;
-    if (table != TSDF_MC_GENERATED && table != TSDF_MC_LORENSEN)
+    if (table < 0 || table >= TSDF_MC_TABLES)
         return set_err(c, TSDF_EINVAL, "unknown marching-cubes table");
     if (!mc_ready) mc_build();
     const uint8_t(*mc_tab)[32] = mc_tabs[table];

@@ -7,7 +7,7 @@ O=gpurun_out/r04/a
 mkdir -p $O
 timeout -k 10 600 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu \
   tests/test_voxblox_merged.py tests/test_multigpu.py tests/test_abi.py tests/test_bench_workload.py \
-  tests/test_voxblox.py tests/test_growth.py > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+  tests/test_voxblox.py tests/test_growth.py tests/test_mesh.py > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
 tail -2 $O/pytest.log
 timeout -k 10 300 python3 bench.py > $O/bench.out 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
 grep '^{' $O/bench.out > $O/bench.json && cat $O/bench.json

@@ -1,7 +1,9 @@
 """Marching-cubes mesh extraction (VDBFusion VDBVolume::extract_triangle_mesh).
 
-The case table is generated, not transcribed, so it is pinned here by what a
-correct marching-cubes table must satisfy: the product library's table equals the oracle's
+The default case table is generated; TSDF_MC_LORENSEN is the published table
+VDBFusion compiles in (include/tsdf_mc_tables.h), checked structurally and compared case by case
+with the generated one below.  The generated table is pinned by what a correct marching-cubes
+table must satisfy: the product library's table equals the oracle's
 independent construction; single-corner cases give one triangle on that corner's three edges;
 and the mesh of a closed analytic surface is watertight, consistently oriented, of Euler
 characteristic 2 and encloses the analytic volume.  The GPU mesh is then compared with the
@@ -163,14 +165,130 @@ def _ambiguous_face(k):
     return False
 
 
-def test_lorensen_table_rule():
-    """TSDF_MC_LORENSEN (VDBFusion's classic table rule): it differs from the
-    generated table exactly on the cases with an ambiguous face and more than 4 inside corners,
-    and the product library builds the same table as the oracle."""
+def published_table():
+    """include/tsdf_mc_tables.h's triangle table (Bourke numbering), parsed from the header."""
+    import os
+    import re
+    from conftest import REPO
+    hdr = open(os.path.join(REPO, "include", "tsdf_mc_tables.h")).read()
+    body = hdr[hdr.index("tsdf_mc_tri_table[256][16] = {"):]
+    rows = re.findall(r"\{([-0-9, ]+)\}", body)
+    assert len(rows) == 256
+    return [[int(x) for x in r.split(",") if int(x) >= 0] for r in rows]
+
+
+BOURKE_V = [(0, 0, 0), (1, 0, 0), (1, 1, 0), (0, 1, 0), (0, 0, 1), (1, 0, 1), (1, 1, 1), (0, 1, 1)]
+BOURKE_E = [(0, 1), (1, 2), (2, 3), (3, 0), (4, 5), (5, 6), (6, 7), (7, 4), (0, 4), (1, 5), (2, 6),
+            (3, 7)]
+
+
+def test_published_table_structure():
+    """The committed triangle table is a marching-cubes table: every case uses exactly its
+    sign-change edges, its triangles form a consistently oriented manifold patch whose boundary runs
+    over the cube's faces through every crossing once, and every triangle faces the inside corners
+    (the trilinear field decreases along its normal)."""
+    rows = published_table()
+    mid = {e: (np.array(BOURKE_V[a]) + np.array(BOURKE_V[b])) / 2.0 for e, (a, b) in enumerate(BOURKE_E)}
+
+    def faces(e):
+        pa, pb = BOURKE_V[BOURKE_E[e][0]], BOURKE_V[BOURKE_E[e][1]]
+        return {(ax, pa[ax]) for ax in range(3) if pa[ax] == pb[ax]}
+
+    for k, r in enumerate(rows):
+        assert len(r) % 3 == 0 and len(r) <= 15, k
+        cross = {e for e, (a, b) in enumerate(BOURKE_E) if (k >> a & 1) != (k >> b & 1)}
+        assert set(r) == cross, k
+        de = {}
+        for t in range(0, len(r), 3):
+            tri = r[t:t + 3]
+            assert len(set(tri)) == 3, k
+            for i in range(3):
+                key = (tri[i], tri[(i + 1) % 3])
+                assert key not in de, k  # each directed edge once: consistent orientation
+                de[key] = 1
+        bnd = [(a, b) for (a, b) in de if (b, a) not in de]
+        assert sorted(a for a, _ in bnd) == sorted(cross) == sorted(b for _, b in bnd), k
+        for a, b in bnd:
+            assert faces(a) & faces(b), (k, a, b)
+
+        def f(x):
+            v = 0.0
+            for c, (vx, vy, vz) in enumerate(BOURKE_V):
+                w = (x[0] if vx else 1 - x[0]) * (x[1] if vy else 1 - x[1]) * (x[2] if vz else 1 - x[2])
+                v += w * (-1.0 if k >> c & 1 else 1.0)
+            return v
+        for t in range(0, len(r), 3):
+            p0, p1, p2 = (mid[e] for e in r[t:t + 3])
+            n = np.cross(p1 - p0, p2 - p0)
+            n /= np.linalg.norm(n)
+            c = (p0 + p1 + p2) / 3
+            assert f(c + 0.05 * n) < f(c - 0.05 * n), (k, t)
+
+
+def renumbered_published():
+    """The published table in this library's layout (corner c = (c&1, c>>1&1, c>>2&1), edges
+    axis-major): what TSDF_MC_LORENSEN must hold, triangle order and winding kept."""
+    kv = [0, 1, 3, 2, 4, 5, 7, 6]
+    ke = [0, 5, 1, 4, 2, 7, 3, 6, 8, 9, 11, 10]
+    out = np.zeros((256, 32), np.uint8)
+    for b, r in enumerate(published_table()):
+        k = sum(1 << kv[v] for v in range(8) if b >> v & 1)
+        out[k, 0] = len(r) // 3
+        out[k, 1:1 + len(r)] = [ke[e] for e in r]
+    return out
+
+
+def test_lorensen_is_the_published_table():
+    from tsdf_map._lib import load_hip_library
+    exp = renumbered_published()
+    assert np.array_equal(table_of(oracle.load(), 1), exp)
+    assert np.array_equal(table_of(load_hip_library(), 1), exp)
+
+
+def _cycles(t, k, reverse=False):
+    tris = [tuple(int(x) for x in t[k, 1 + 3 * i:4 + 3 * i]) for i in range(t[k, 0])]
+    if reverse:
+        tris = [(a, c, b) for a, b, c in tris]
+    de = {(x, y) for a, b, c in tris for x, y in ((a, b), (b, c), (c, a))}
+    nxt = {a: b for (a, b) in de if (b, a) not in de}
+    cyc, seen = set(), set()
+    for a in nxt:
+        if a in seen:
+            continue
+        c, x = [], a
+        while x not in seen:
+            seen.add(x)
+            c.append(x)
+            x = nxt[x]
+        i = c.index(min(c))
+        cyc.add(tuple(c[i:] + c[:i]))
+    return frozenset(cyc)
+
+
+def test_published_table_vs_the_builders_tables():
+    """Where the builder's tables differ from the published one: the GENERATED
+    table has the published table's polygons in every case (the same crossings joined into the same
+    cycles) with the opposite winding and its own fan triangulation; the round-3 'Lorensen rule'
+    (complement symmetry, now TSDF_MC_LORENSEN_RULE) joins them differently in exactly the 44 cases
+    that have an ambiguous face and more than 4 inside corners -- the published table does not
+    follow complement symmetry there."""
+    pub, gen, rule = renumbered_published(), table_of(oracle.load(), 0), table_of(oracle.load(), 2)
+    assert all(_cycles(pub, k) == _cycles(gen, k, reverse=True) for k in range(256))
+    differ = {k for k in range(256) if _cycles(pub, k) != _cycles(rule, k, reverse=True)}
+    expect = {k for k in range(256) if _ambiguous_face(k) and bin(k).count("1") > 4}
+    assert differ == expect and len(differ) == 44
+    same_rows = sum(np.array_equal(pub[k], gen[k]) for k in range(256))
+    assert same_rows == 2  # the empty and full cases: the triangulations themselves differ
+
+
+def test_lorensen_rule_table():
+    """TSDF_MC_LORENSEN_RULE (the classic complement-symmetry rule): it differs from the generated
+    table exactly on the cases with an ambiguous face and more than 4 inside corners, and the
+    product library builds the same table as the oracle."""
     from tsdf_map._lib import load_hip_library
     g = table_of(oracle.load(), 0)
-    lo = table_of(oracle.load(), 1)
-    assert np.array_equal(lo, table_of(load_hip_library(), 1))
+    lo = table_of(oracle.load(), 2)
+    assert np.array_equal(lo, table_of(load_hip_library(), 2))
     assert np.array_equal(g, table(oracle.load()))
     differ = {k for k in range(256) if not np.array_equal(g[k], lo[k])}
     expect = {k for k in range(256) if _ambiguous_face(k) and bin(k).count("1") > 4}
@@ -198,8 +316,8 @@ def test_gpu_sphere_mesh_lorensen_bitwise(radius):
 
 @pytest.mark.gpu
 def test_gpu_scan_mesh_lorensen_bitwise(sim):
-    """Integrated scans (noisy surfaces: ambiguous cubes occur) meshed with the classic table, GPU
-    == oracle bit for bit; the two tables' meshes differ only where ambiguous cubes are."""
+    """Integrated scans (noisy surfaces: ambiguous cubes occur) meshed with the published table,
+    GPU == oracle bit for bit."""
     from conftest import decimate
     from tsdf_map import HipTSDFVolume
     o = oracle.OracleTSDFVolume(VS, TAU)
