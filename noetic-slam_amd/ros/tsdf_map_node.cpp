@@ -83,6 +83,18 @@ class TsdfMapNode {
             p.allow_clear = clear ? 1 : 0;
             p.use_weight_dropoff = drop ? 1 : 0;
             p.depth_weight = const_w ? 0 : 1;
+            // voxblox_ros TsdfServer `method`: "merged" (its default) or "simple"
+            std::string method;
+            pnh.param<std::string>("method", method, "merged");
+            if (method == "merged") {
+                p.voxblox_method = TSDF_VB_MERGED;
+            } else if (method == "simple") {
+                p.voxblox_method = TSDF_VB_SIMPLE;
+            } else {  // "fast" is thread-order dependent
+                ROS_FATAL("unknown voxblox method '%s' (merged, simple)", method.c_str());
+                ros::shutdown();
+                return;
+            }
         } else if (sem == "vdbfusion_f64") {  // upstream's precisions
             p.semantics = TSDF_SEM_VDBFUSION_F64;
         } else if (sem == "vdbfusion") {  // the fp32 restatement

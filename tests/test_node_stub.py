@@ -29,21 +29,23 @@ def node_exe(tmp_path_factory):
     return str(exe)
 
 
-@pytest.mark.parametrize("semantics", ["vdbfusion_f64", "vdbfusion", "voxblox"])
+@pytest.mark.parametrize("semantics", ["vdbfusion_f64", "vdbfusion", "voxblox", "voxblox_simple"])
 def test_node_runs_topic_stream(tmp_path, sim, node_exe, semantics):
     recs, want = topic_stream(sim, tilt=0.5)
     write_topics(tmp_path / "in.topics", recs)
     out = tmp_path / "map.bricks"
     env = dict(os.environ, TSDF_STUB_STREAM=str(tmp_path / "in.topics"),
-               TSDF_STUB_PARAMS="map_path=%s;min_range=0;semantics=%s;max_ray_length_m=1000" %
-                                (out, semantics))
+               TSDF_STUB_PARAMS="map_path=%s;min_range=0;semantics=%s;max_ray_length_m=1000%s" %
+                                (out, semantics.split("_simple")[0],
+                                 ";method=simple" if semantics.endswith("_simple") else ""))
     r = subprocess.run([node_exe], env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     assert "saved" in r.stderr
     got = bricks_to_voxels(*read_bricks(out))
-    kw = dict(semantics=semantics)
-    if semantics == "voxblox":
-        kw.update(max_range=1000.0, use_const_weight=False)  # the node's voxblox defaults
+    kw = dict(semantics=semantics.split("_simple")[0])
+    if semantics.startswith("voxblox"):  # the node's voxblox defaults: merged (voxblox_ros')
+        kw.update(max_range=1000.0, use_const_weight=False,
+                  method="simple" if semantics.endswith("_simple") else "merged")
     ref = oracle_voxels(want, **kw)
     assert got[0].shape[0] > 1000
     for a, b in zip(got, ref):
