@@ -284,6 +284,14 @@ struct tsdf_ctx {
     // or the same device); tsdf_integrate_sectors' fan-out: its copy-done event (this device)
     uint64_t peer_mask = 0;
     hipEvent_t bc_ev = nullptr;
+    // tsdf_integrate_sectors' fan-out, batch-granular: a follower's pending points [fan_lo, fan_hi)
+    // are still in its leader's staging buffer fan_buf (same offsets: the contexts' batches run in
+    // lockstep) and are copied in ONE device-to-device copy before the follower's batch launches
+    // (fan_copy); the leader keeps its followers, so it never reuses a buffer they still read
+    tsdf_ctx* fan_src = nullptr;
+    const float* fan_buf = nullptr;
+    uint64_t fan_lo = 0, fan_hi = 0;
+    std::vector<tsdf_ctx*> fan_followers;
 };
 
 // Weight cap of the weighted-mean merges (import, border reduce): Voxblox's max_weight, else none
@@ -532,9 +540,44 @@ static int join(tsdf_ctx* c) {
     return TSDF_OK;
 }
 
+// A fan-out follower's pending points, still in its leader's staging, copied into its own staging
+// (device to device, xGMI between GPUs) after the leader's H2D copies; the leader's stream then
+// waits for the copy, so the leader never rewrites that region first.  Leaves the current device
+// as it found it.
+static int fan_copy_range(tsdf_ctx* c, tsdf_ctx* s, float* dst, const float* src, uint64_t bytes) {
+    int dev = 0;
+    HIPCHK(c, hipGetDevice(&dev));
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamWaitEvent(c->stream, s->bc_ev, 0));  // the leader's H2D copies so far
+    HIPCHK(c, c->device == s->device
+                  ? hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, c->stream)
+                  : hipMemcpyPeerAsync(dst, c->device, src, s->device, bytes, c->stream));
+    if (!c->bc_ev) HIPCHK(c, hipEventCreateWithFlags(&c->bc_ev, hipEventDisableTiming));
+    HIPCHK(c, hipEventRecord(c->bc_ev, c->stream));
+    HIPCHK(s, hipSetDevice(s->device));
+    HIPCHK(s, hipStreamWaitEvent(s->stream, c->bc_ev, 0));
+    HIPCHK(c, hipSetDevice(dev));
+    return TSDF_OK;
+}
+
+static int fan_copy(tsdf_ctx* c) {
+    if (!c->fan_src || !c->fan_buf || c->fan_hi <= c->fan_lo) {
+        c->fan_lo = c->fan_hi;
+        return TSDF_OK;
+    }
+    const int rc = fan_copy_range(c, c->fan_src, c->stage2[c->pend_stage] + 3 * c->fan_lo,
+                                  c->fan_buf + 3 * c->fan_lo, (c->fan_hi - c->fan_lo) * 12);
+    c->fan_lo = c->fan_hi;
+    return rc;
+}
+
 // Launch the queued host scans (integrate paths: no join, so batches keep overlapping).
 static int flush(tsdf_ctx* c) {
     if (c->pend.n_scans == 0) return TSDF_OK;
+    if (c->fan_src) {  // a fan-out follower: its points first
+        const int rc = fan_copy(c);
+        if (rc) return rc;
+    }
     // the buffer the pending scans were staged into; a replay that runs inside launch() (metrics
     // drain, log bound) re-reads only logged batches, none of which uses this buffer any more
     const int rc = launch(c, c->stage2[c->pend_stage], c->pend);
@@ -1029,6 +1072,18 @@ const char* tsdf_last_error(const tsdf_ctx* c) { return c ? c->err.c_str() : "nu
 
 void tsdf_destroy(tsdf_ctx* c) {
     if (!c) return;
+    // fan-out links (tsdf_integrate_sectors): a leader hands its followers their pending points
+    // before its staging goes; a follower leaves its leader's list
+    for (tsdf_ctx* f : c->fan_followers) {
+        (void)fan_copy(f);
+        f->fan_src = nullptr;
+        f->fan_buf = nullptr;
+    }
+    c->fan_followers.clear();
+    if (c->fan_src) {
+        auto& v = c->fan_src->fan_followers;
+        v.erase(std::remove(v.begin(), v.end(), c), v.end());
+    }
     if (c->device >= 0) {
         (void)hipSetDevice(c->device);
         if (c->stream) {
@@ -1359,6 +1414,11 @@ static void set_pose(BatchDesc& D, uint32_t s, const ScanPose& P) {
 static int pend_stage_buffer(tsdf_ctx* c) {
     if (c->pend.n_scans != 0) return TSDF_OK;
     const int k = c->last_stage ^ 1;
+    for (tsdf_ctx* f : c->fan_followers)  // fan-out followers still reading buffer k copy first
+        if (f->fan_buf == c->stage2[k] && f->fan_hi > f->fan_lo) {
+            const int rc = fan_copy(f);
+            if (rc) return rc;
+        }
     if (c->stage_reader[k] != ~0ull) {
         if (c->can_grow) {
             HIPCHK(c, hipEventSynchronize(c->stage_ev[k]));
@@ -1465,10 +1525,10 @@ int tsdf_integrate(tsdf_ctx* c, const void* pts, uint64_t n, uint32_t point_step
 // is packed ONCE into ctxs[0]'s pinned buffer h[0] (on every context's staging threads), and every
 // context receives all of it -- its kernels drop the other sectors' rays (R.sec_on), so the fields
 // are those of the split, bit for bit.
-//   FANOUT: one H2D copy into ctxs[0]'s staging, then ctxs[k] copies that region device to device
-//           (hipMemcpyPeerAsync: xGMI with peer access, tsdf_create_sharded) into its own staging,
-//           after ctxs[0]'s copy (an event); ctxs[0]'s stream then waits for those copies, so its
-//           staging region is not rewritten (and h[0] not reused) before they ran.
+//   FANOUT: one H2D copy into ctxs[0]'s staging (the leader); the other contexts (followers) take
+//           the scan into their pending batch and copy the batch's points from the leader's staging
+//           in ONE device-to-device copy before they launch it (fan_copy: hipMemcpyPeerAsync, xGMI
+//           with peer access, tsdf_create_sharded) -- O(1) API calls per follower per scan.
 //   H2D:    every context copies h[0] over its own PCIe link; ctxs[0]'s stream waits for them all
 //           before it records h[0]'s reuse event.
 static int sectors_broadcast(tsdf_ctx* const* ctxs, uint32_t n_ctx, const void* pts, uint64_t n,
@@ -1512,41 +1572,64 @@ static int sectors_broadcast(tsdf_ctx* const* ctxs, uint32_t n_ctx, const void* 
         for (uint32_t k = 1; k < n_ctx; k++)
             if (ctxs[k]->pack) ctxs[k]->pack->wait();
     }
-    // the copies: ctxs[0] first (FANOUT reads its staging region)
-    float* dst0 = nullptr;
-    for (uint32_t k = 0; k < n_ctx; k++) {
+    c0->split_ht.lap(1);  // TSDF_HOST_TIMING: 0 prep, 1 pack, 2 copies + queue
+    // the leader's H2D copy first
+    HIPCHK(c0, hipSetDevice(c0->device));
+    int rc = pend_stage_buffer(c0);
+    if (rc) return rc;
+    const uint64_t off0 = c0->pend.s[c0->pend.n_scans].off;
+    float* buf0 = c0->stage2[c0->pend_stage];
+    if (n) HIPCHK(c0, hipMemcpyAsync(buf0 + 3 * off0, hx, n * 12, hipMemcpyHostToDevice, c0->stream));
+    if (!c0->bc_ev) HIPCHK(c0, hipEventCreateWithFlags(&c0->bc_ev, hipEventDisableTiming));
+    HIPCHK(c0, hipEventRecord(c0->bc_ev, c0->stream));
+    for (uint32_t k = 1; k < n_ctx; k++) {
         tsdf_ctx* c = ctxs[k];
         HIPCHK(c, hipSetDevice(c->device));
-        int rc = pend_stage_buffer(c);
+        rc = pend_stage_buffer(c);
         if (rc) return rc;
-        float* dst = c->stage2[c->pend_stage] + 3 * (uint64_t)c->pend.s[c->pend.n_scans].off;
-        if (k == 0) {
-            dst0 = dst;
-            if (n) HIPCHK(c, hipMemcpyAsync(dst, hx, n * 12, hipMemcpyHostToDevice, c->stream));
-            if (fanout && n_ctx > 1) {
-                if (!c->bc_ev) HIPCHK(c, hipEventCreateWithFlags(&c->bc_ev, hipEventDisableTiming));
-                HIPCHK(c, hipEventRecord(c->bc_ev, c->stream));
+        const uint64_t off = c->pend.s[c->pend.n_scans].off;
+        if (fanout) {
+            // batch-granular: extend the follower's uncopied range when it continues in the same
+            // leader buffer at the same offset (lockstep batches), else copy what it holds first
+            if (c->fan_src != c0 || c->fan_buf != buf0 || c->fan_hi != off || off != off0) {
+                rc = fan_copy(c);
+                if (rc) return rc;
+                if (c->fan_src && c->fan_src != c0) {  // a new leader
+                    auto& v = c->fan_src->fan_followers;
+                    v.erase(std::remove(v.begin(), v.end(), c), v.end());
+                }
+                if (std::find(c0->fan_followers.begin(), c0->fan_followers.end(), c) ==
+                    c0->fan_followers.end())
+                    c0->fan_followers.push_back(c);
+                c->fan_src = c0;
+                c->fan_buf = buf0;
+                c->fan_lo = c->fan_hi = off;
+                if (off != off0) {  // out of lockstep: this scan alone, now
+                    c->fan_buf = nullptr;  // nothing pending; the next scan starts afresh
+                    if (n) {
+                        rc = fan_copy_range(c, c0, c->stage2[c->pend_stage] + 3 * off,
+                                            buf0 + 3 * off0, n * 12);
+                        if (rc) return rc;
+                    }
+                }
             }
+            if (c->fan_buf) c->fan_hi = off + n;
         } else if (n) {
-            if (fanout) {
-                HIPCHK(c, hipStreamWaitEvent(c->stream, c0->bc_ev, 0));
-                HIPCHK(c, c->device == c0->device
-                              ? hipMemcpyAsync(dst, dst0, n * 12, hipMemcpyDeviceToDevice, c->stream)
-                              : hipMemcpyPeerAsync(dst, c->device, dst0, c0->device, n * 12, c->stream));
-            } else {
-                HIPCHK(c, hipMemcpyAsync(dst, hx, n * 12, hipMemcpyHostToDevice, c->stream));
-            }
-            // ctxs[0] must not rewrite its staging region or h[0] before this copy ran
+            // H2D: this context's own PCIe copy of h[0]; the leader must not reuse h[0] first
+            HIPCHK(c, hipMemcpyAsync(c->stage2[c->pend_stage] + 3 * off, hx, n * 12,
+                                     hipMemcpyHostToDevice, c->stream));
             if (!c->bc_ev) HIPCHK(c, hipEventCreateWithFlags(&c->bc_ev, hipEventDisableTiming));
             HIPCHK(c, hipEventRecord(c->bc_ev, c->stream));
+            HIPCHK(c0, hipStreamWaitEvent(c0->stream, c->bc_ev, 0));
         }
-        if (k) HIPCHK(c, hipEventRecord(c->stage_done[hb[k]], c->stream));
-        rc = pend_push(c, n, P);
+        rc = pend_push(c, n, P);  // a full batch launches here (fan-out: after its copy)
         if (rc) return rc;
     }
     HIPCHK(c0, hipSetDevice(c0->device));
-    for (uint32_t k = 1; k < n_ctx && n; k++) HIPCHK(c0, hipStreamWaitEvent(c0->stream, ctxs[k]->bc_ev, 0));
     HIPCHK(c0, hipEventRecord(c0->stage_done[hb[0]], c0->stream));
+    rc = pend_push(c0, n, P);
+    if (rc) return rc;
+    c0->split_ht.lap(2);
     return TSDF_OK;
 }
 
@@ -1601,6 +1684,7 @@ int tsdf_integrate_sectors(tsdf_ctx* const* ctxs, uint32_t n_ctx, const void* pt
     // would bundle each sector's points apart
     if (mode == TSDF_SECTOR_INPUT_SPLIT && n_ctx > 1 && c0->merged) mode = TSDF_SECTOR_INPUT_FANOUT;
     if (mode == TSDF_SECTOR_INPUT_FANOUT || mode == TSDF_SECTOR_INPUT_H2D) {
+        ht.lap(0);
         const int rc = sectors_broadcast(ctxs, n_ctx, pts, n, point_step, xyz_offset, xyz_is_f64,
                                          P, h, hb, mode == TSDF_SECTOR_INPUT_FANOUT);
         if (rc) return rc;

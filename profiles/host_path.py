@@ -56,19 +56,24 @@ def main():
     ctxs = (C.c_void_p * n)(*[v._ctx.value for v in vols])
     poses = [np.concatenate([o, [0.0, 0.0, 0.0, 1.0]]) for o in origins]
 
+    in_call = [0.0]
+
     def run(lo, hi):
         for k in range(lo, hi):
             c = clouds[k]
-            if n > 1:  # one host cloud, split over the sector contexts
+            t = time.perf_counter()
+            if n > 1:  # one host cloud for the sector contexts
                 rc = lib.tsdf_integrate_sectors(ctxs, n, c.ctypes.data_as(C.c_void_p), c.shape[0], 32,
                                                 0, 0, poses[k].ctypes.data_as(_abi.D3))
                 vol._check(rc, "integrate_sectors")
             else:
                 vol.integrate_cloud(c, c.shape[0], 32, 0, origins[k])
+            in_call[0] += time.perf_counter() - t
         for v in vols:
             v.sync()
 
     run(0, args.warmup)
+    in_call[0] = 0.0
     t0 = time.perf_counter()
     run(args.warmup, args.warmup + args.scans)
     dt = time.perf_counter() - t0
@@ -80,7 +85,10 @@ def main():
                       "semantics": args.semantics, "max_batch": args.max_batch,
                       "bytes_per_scan_host": int(clouds[0].nbytes),
                       "h2d_bytes_per_scan": int(clouds[0].shape[0] * 12),
-                      "h2d_GBps_equiv": round(args.scans * clouds[0].nbytes / dt / 1e9, 2)}))
+                      "h2d_GBps_equiv": round(args.scans * clouds[0].nbytes / dt / 1e9, 2),
+                      # time inside the integrate calls (packing, copies, API calls, and any wait
+                      # for a staging buffer still in use on the GPU)
+                      "call_us_per_scan": round(in_call[0] / args.scans * 1e6, 1)}))
 
 
 if __name__ == "__main__":

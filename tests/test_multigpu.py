@@ -268,6 +268,47 @@ def test_integrate_sectors_bitwise(sim, n, f64, mode):
         assert all(v.stats()["n_points_in"] == total for v in g)  # every context got the cloud
 
 
+def test_fanout_out_of_lockstep(sim):
+    """The fan-out copies a follower's pending points from the leader's staging once per batch;
+    partial flushes (a read-out of the leader alone), a follower's own scan in between, and the
+    leader destroyed while its followers still hold uncopied points all leave every context equal
+    to its oracle twin."""
+    from tsdf_map import integrate_sectors
+    n, yaw0 = 3, 0.3
+    g = [hip(n_sectors=n, sector=r, sector_yaw0=yaw0, max_batch=3) for r in range(n)]
+    o = [ora(n_sectors=n, sector=r, sector_yaw0=yaw0) for r in range(n)]
+    scans = []
+    for k in (0, 1, 2, 5, 7, 9, 11):
+        pts, org = sim.scan(k)
+        scans.append((np.ascontiguousarray(pts[::4]), org))
+
+    def both(i, only=None):
+        pts, org = scans[i]
+        if only is None:
+            integrate_sectors(g, pts, np.concatenate([org, [0.0, 0.0, 0.0, 1.0]]))
+            for v in o:
+                v.integrate(pts, org)
+        else:
+            g[only].integrate(pts, org)
+            o[only].integrate(pts, org)
+
+    both(0)
+    both(1)
+    g[0].sync()              # the leader flushes alone; followers keep their pending range
+    both(2)
+    both(3, only=1)          # a follower's own scan between fan-out scans
+    both(4)
+    both(5)
+    ref = [v.export_voxels() for v in o]
+    for r in range(n):
+        g[r].sync()
+        assert voxels_equal_bitwise(g[r].export_voxels(), ref[r]), r
+    both(6)                  # pending everywhere, then the leader goes first
+    g[0].close()
+    for r in (1, 2):
+        assert voxels_equal_bitwise(g[r].export_voxels(), o[r].export_voxels()), r
+
+
 def test_integrate_sectors_voxblox_merged(sim):
     """MergedTsdfIntegrator bundles the whole scan before the sector filter, so the sectors take the
     fan-out (a requested host split is overridden): every context equals its oracle twin."""
