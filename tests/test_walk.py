@@ -70,9 +70,10 @@ def test_sequences_both_front_ends(sim, mb, pipe):
 @pytest.mark.parametrize("semantics,extra,want", [
     ("vdbfusion", {}, "walk"),
     ("vdbfusion_f64", {}, "walk"),
-    ("voxblox", {}, "walk"),                      # max_range = inf: no clearing ray can exist
-    ("voxblox", {"max_range": 30.0}, "count"),    # clearing rays up to 30 m
-    ("voxblox", {"max_range": 30.0, "allow_clear": False}, "walk"),
+    ("voxblox", {"use_const_weight": True}, "walk"),  # max_range = inf: no clearing ray can exist
+    ("voxblox", {}, "count"),                     # 1/z^2 weights (the default) are per sample
+    ("voxblox", {"use_const_weight": True, "max_range": 30.0}, "count"),  # clearing rays to 30 m
+    ("voxblox", {"use_const_weight": True, "max_range": 30.0, "allow_clear": False}, "walk"),
     ("vdbfusion", {"space_carving": True, "max_range": 40.0}, "count"),
     ("vdbfusion", {"sdf_trunc": 0.1745}, "walk"),  # band 6.98 voxels: the 32-slot walk
     ("vdbfusion", {"sdf_trunc": 0.2}, "count"),    # band 8 voxels: up to 7 bricks per ray
