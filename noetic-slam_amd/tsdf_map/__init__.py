@@ -6,7 +6,8 @@ in the reference snapshot and so are listed but not constructibl
 """
 from ._abi import BRICK_SIDE, BRICK_VOX  # noqa: F401
 from ._lib import HIP_LIB, load_hip_library  # noqa: F401
-from .volume import (HipTSDFVolume, SimpleTsdfIntegrator, TSDFVolume,  # noqa: F401
+from .volume import (HipTSDFVolume, MergedTsdfIntegrator, SimpleTsdfIntegrator,  # noqa: F401
+                     TSDFVolume,
                      TsdfError, TsdfIntegratorConfig, border_reduce_local, bricks_to_voxels,
                      integrate_sectors,
                      sector_ids, select_sector)

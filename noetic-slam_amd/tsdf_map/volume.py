@@ -456,6 +456,8 @@ class SimpleTsdfIntegrator:
     on the GPU): `integratePointCloud(T_G_C, points_C)` transforms the sensor-frame points by the
     4x4 pose (float64, then float32) and integrates them from the pose's translation."""
 
+    METHOD = "simple"
+
     def __init__(self, config, voxel_size, volume_cls=None, **kw):
         cls = volume_cls or HipTSDFVolume
         self.config = config
@@ -465,7 +467,7 @@ class SimpleTsdfIntegrator:
                           semantics="voxblox", allow_clear=config.allow_clear,
                           use_weight_dropoff=config.use_weight_dropoff,
                           max_weight=config.max_weight, use_const_weight=config.use_const_weight,
-                          **kw)
+                          method=self.METHOD, **kw)
 
     def integratePointCloud(self, T_G_C, points_C, colors=None, freespace_points=False):  # noqa: N802
         if freespace_points:
@@ -474,6 +476,13 @@ class SimpleTsdfIntegrator:
         pc = np.asarray(points_C, np.float64).reshape(-1, 3)
         pts_g = (pc @ T[:3, :3].T + T[:3, 3]).astype(np.float32)
         self.volume.integrate(pts_g, T)
+
+
+class MergedTsdfIntegrator(SimpleTsdfIntegrator):
+    """voxblox's MergedTsdfIntegrator (voxblox_ros's default `method`): the
+    scan's points bundled per voxel, one weighted ray per bundle (tsdf_params.voxblox_method)."""
+
+    METHOD = "merged"
 
 
 def sector_ids(points, origin, n_sectors, yaw0=0.0):

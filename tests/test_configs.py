@@ -115,6 +115,45 @@ def test_c5_voxblox_upstream_defaults(c5_bag_sparse):
     assert over <= 1e-3 * dd.size and np.quantile(dd, 0.999) <= 0.1 * tau
 
 
+def test_c5_voxblox_merged_upstream_defaults(c5_bag_sparse):
+    """C5 against voxblox_ros's default integrator, MergedTsdfIntegrator, with
+    voxblox's own config defaults at 2 cm: GPU == the oracle's scan-fused twin bit for bit; against
+    the literal per-sample update of the same bundles the |dS| over 0.1 tau are counted and
+    bounded; against SimpleTsdfIntegrator's field the differences are reported (bundling moves the
+    rays' end points, so these differ by construction)."""
+    from tsdf_map import HipTSDFVolume, TsdfIntegratorConfig, ingest
+    cfg = TsdfIntegratorConfig()
+    kw = dict(semantics="voxblox", space_carving=cfg.voxel_carving_enabled,
+              min_range=cfg.min_ray_length_m, max_range=cfg.max_ray_length_m,
+              use_const_weight=cfg.use_const_weight, allow_clear=cfg.allow_clear,
+              use_weight_dropoff=cfg.use_weight_dropoff, max_weight=cfg.max_weight)
+    vs, tau = 0.02, cfg.default_truncation_distance
+    g = HipTSDFVolume(vs, tau, max_bricks=1 << 18, method="merged", **kw)
+    assert ingest.ingest_bag(g, c5_bag_sparse) == (6, 0)
+    g.sync()
+    gv = g.export_voxels()
+    o = oracle.OracleTSDFVolume(vs, tau, threads=8, method="merged", **kw)
+    assert ingest.ingest_bag(o, c5_bag_sparse) == (6, 0)
+    r = compare(gv, o.export_voxels())
+    assert r["only_a"] == r["only_b"] == r["weight_mismatch"] == 0
+    assert r["bitwise_equal"] == r["voxels_a"] > 100_000, r
+    del o
+    lit = oracle.OracleTSDFVolume(vs, tau, mode=oracle.MODE_SEQUENTIAL, method="merged", **kw)
+    assert ingest.ingest_bag(lit, c5_bag_sparse) == (6, 0)
+    lv = lit.export_voxels()
+    d = compare(gv, lv)
+    _, ia, ib = np.intersect1d(_keys(gv[0]), _keys(lv[0]), assume_unique=True, return_indices=True)
+    dd = np.abs(gv[1][ia].astype(np.float64) - lv[1][ib])
+    over = int((dd > 0.1 * tau).sum())
+    simple = oracle.OracleTSDFVolume(vs, tau, threads=8, **kw)
+    assert ingest.ingest_bag(simple, c5_bag_sparse) == (6, 0)
+    vs_simple = compare(gv, simple.export_voxels())
+    print("C5 voxblox merged vs literal:", d, "over 0.1 tau:", over,
+          "p99.9:", float(np.quantile(dd, 0.999)), "| merged vs simple:", vs_simple)
+    assert d["only_a"] == d["only_b"] == 0
+    assert over <= 1e-3 * dd.size and np.quantile(dd, 0.999) <= 0.1 * tau
+
+
 @pytest.mark.parametrize("semantics", ["vdbfusion_f64", "voxblox"])
 def test_c5_bag_2cm_field_and_mesh(c5_bag, semantics):
     from tsdf_map import HipTSDFVolume, ingest
