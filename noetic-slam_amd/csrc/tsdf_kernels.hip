@@ -193,14 +193,7 @@ __global__ __launch_bounds__(NT, SEM == 2 && NT == CNT_THREADS ? TSDF_F64_COUNT_
                 uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0, curc = ~0u, ccount = 0;
                 auto walk = [&](auto chk) {
                     for (int it = 0; it < MAX_DDA_STEPS; it++) {
-                        bool g;
-#ifndef TSDF_NO_GATE_SKIP
-                        // the band before the hit passes the gate for sure (gate_skip_bound): while
-                        // every lane is there, the wave skips the gate's arithmetic
-                        if (!decltype(chk)::value && __all(Walk<SEM>::ahead(r))) g = true;
-                        else
-#endif
-                            g = Walk<SEM>::gate_sel(R, ox, oy, oz, r, decltype(chk)::value);
+                        const bool g = Walk<SEM>::gate_sel(R, ox, oy, oz, r, decltype(chk)::value);
                         const uint32_t bc = brick_code_of(r.vx, r.vy, r.vz);
                         const bool nb = g && bc != curc;
                         const bool cl = nb && curc != ~0u;  // the previous pair closes

@@ -15,9 +15,6 @@ namespace tsdf {
 struct RayState {
     float px, py, pz;  // hit point (world)
     float t1i;         // band end (index units)
-    // k_count's gate skip (gate_skip_bound): while the current voxel's exit time min(tn) is at most
-    // tsafe, the voxel's centre is provably in front of the hit (proj > 0), so it passes the gate
-    float tsafe;
     float tnx, tny, tnz;
     float tdx, tdy, tdz;
     int vx, vy, vz;
@@ -43,28 +40,6 @@ __device__ __forceinline__ void axis_init(float u, float s, float t0i, int v, fl
     }
 }
 
-// k_count's gate skip.  The DDA's current voxel v is left at t_out = min(tn) (index units: the ray
-// parameter over vs), and the ray is inside v just before, so v's centre c lies within
-// h = sqrt(3)/2 (+ slack for the fp32 walk) of the ray point at t_out: its projection t_c onto the
-// ray is in [t_out - h, t_out + h] and its distance from the ray r_perp <= h.  With the hit
-// p = o + d u, ComputeSDF's proj = (c - o).(p - c) = t_c (d - t_c) - r_perp^2 (index^2 units), and
-// for t_c in [A, B] with 0 < A <= B < d, t_c (d - t_c) >= A (d - B).  Every voxel of the band has
-// t_c >= A = t0i - 2h, so with B = t_out + h:
-//     t_out <= tsafe = d - h - (h^2 + eps) / A   implies   proj >= eps,
-// eps bounding the error of the evaluated proj: the fp32 one of SEM 0 (catastrophic cancellation in
-// b = p - c: <= ~4u (|a| + 1)(|o| + d + 2) with u = 2^-24, |a| <= d + 2, all in index units; taken
-// twice) or the double one of SEM 2 (far smaller).  Such a voxel passes sdf > -tau (sdf = +dist),
-// so k_count's walk skips the gate when every lane of the wave is there: the verdict is the
-// gate's, bit for bit.  Carving rays (t0 = 0: voxels at the origin have proj ~ 0) and rays with
-// A < 1 never skip.
-__device__ __forceinline__ float gate_skip_bound(float d_i, float t0i, float o_i, bool carving) {
-    constexpr float h = 0.8660254f + 0.05f;
-    const float A = t0i - 2.0f * h;
-    if (carving || !(A >= 1.0f) || !(o_i < 1e7f)) return -__builtin_inff();
-    const float eps = 0.05f + 5e-7f * (d_i + 3.0f) * (o_i + d_i + 2.0f);
-    return d_i - h - (h * h + eps) / A - 0.01f * (1.0f + 1e-4f * d_i);
-}
-
 // Returns false when the ray is filtered out (zero/NaN length, outside [min_range, max_range]).
 __device__ __forceinline__ bool ray_init(const RayConst& R, float ox, float oy, float oz, float px,
                                          float py, float pz, RayState& r) {
@@ -78,8 +53,6 @@ __device__ __forceinline__ bool ray_init(const RayConst& R, float ox, float oy, 
     const float t1 = depth + R.tau;
     const float t0i = t0 * R.inv_vs;
     r.t1i = t1 * R.inv_vs;
-    r.tsafe = gate_skip_bound(depth * R.inv_vs, t0i,
-                              fmaxf(fmaxf(fabsf(ox), fabsf(oy)), fabsf(oz)) * R.inv_vs, R.carving);
     const float sx = ox * R.inv_vs + ux * t0i;
     const float sy = oy * R.inv_vs + uy * t0i;
     const float sz = oz * R.inv_vs + uz * t0i;
@@ -427,10 +400,6 @@ struct Walk<0> {  // TSDF_SEM_VDBFUSION
     }
     __device__ static __forceinline__ bool step(State& r) { return ray_step(r); }
     __device__ static __forceinline__ bool step_sel(State& r) { return ray_step_sel(r); }
-    // the current voxel passes the gate for sure (gate_skip_bound)
-    __device__ static __forceinline__ bool ahead(const State& r) {
-        return fminf(fminf(r.tnx, r.tny), r.tnz) <= r.tsafe;
-    }
 };
 
 template <>
@@ -465,7 +434,6 @@ struct Walk<1> {  // TSDF_SEM_VOXBLOX
     }
     __device__ static __forceinline__ bool step(State& r) { return vb_step(r); }
     __device__ static __forceinline__ bool step_sel(State& r) { return vb_step_sel(r); }
-    __device__ static __forceinline__ bool ahead(const State&) { return false; }  // no skip
 };
 
 // Voxblox with the 1/z^2 weight (internal sem 3): the same walk; k_place stores every sample's
@@ -560,8 +528,6 @@ __device__ __forceinline__ bool vdb_init(const RayConst& R, const BatchRef& D, u
     const float dix = jx / L, diy = jy / L, diz = jz / L;
     const float t0i = L * t0;
     r.t1i = L * t1;
-    r.tsafe = gate_skip_bound(L * depth, t0i,
-                              fmaxf(fmaxf(fabsf(ex), fabsf(ey)), fabsf(ez)), R.carving);
     // math::DDA::init
     const float qx = ex + dix * t0i, qy = ey + diy * t0i, qz = ez + diz * t0i;
     r.vx = (int)__builtin_floorf(qx);
@@ -724,9 +690,6 @@ struct Walk<2> {  // TSDF_SEM_VDBFUSION_F64
     }
     __device__ static __forceinline__ bool step(State& r) { return ray_step(r); }
     __device__ static __forceinline__ bool step_sel(State& r) { return ray_step_sel(r); }
-    __device__ static __forceinline__ bool ahead(const State& r) {
-        return fminf(fminf(r.tnx, r.tny), r.tnz) <= r.tsafe;
-    }
 };
 
 __device__ __forceinline__ uint64_t pack_brick(int bx, int by, int bz) {

@@ -19,3 +19,5 @@ for r in 1 2; do
 done
 timeout -k 10 300 python3 bench.py --no-cpu --batch 128 --steps 16 > $O/b128.json 2> $O/b128.err || { tail -5 $O/b128.err; exit 1; }
 python3 -c "import json;d=json.loads(open('$O/b128.json').read().strip().splitlines()[-1]);print('b128', d['value'], d['ms_per_step'], d['serial_kernel_ms_per_launch'])"
+timeout -k 10 300 python3 bench.py --no-cpu --batch 32 --steps 32 > $O/b32.json 2> $O/b32.err || { tail -5 $O/b32.err; exit 1; }
+python3 -c "import json;d=json.loads(open('$O/b32.json').read().strip().splitlines()[-1]);print('b32', d['value'], d['ms_per_step'], d['serial_kernel_ms_per_launch'])"
