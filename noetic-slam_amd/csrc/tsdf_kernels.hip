@@ -98,6 +98,20 @@ __device__ __forceinline__ bool block_any(bool p, uint32_t* s_vote) {
 #ifndef TSDF_CNT_THREADS
 #define TSDF_CNT_THREADS 256
 #endif
+// Diagnostic build only (-DTSDF_CNT_PHASE, never shipped): thread 0 of every 61st k_count
+// workgroup prints its wall-clock cycles per phase (walk and pair emission summed over its rays).
+#ifdef TSDF_CNT_PHASE
+#define CPH(k)                                             \
+    do {                                                   \
+        const unsigned long long t_ = __builtin_readcyclecounter(); \
+        cph[k] += t_ - cpl;                                \
+        cpl = t_;                                          \
+    } while (0)
+#else
+#define CPH(k) \
+    do {       \
+    } while (0)
+#endif
 constexpr int CNT_THREADS = TSDF_CNT_THREADS;
 
 // NT: threads per workgroup (NT; 1024 for batches too small to fill the chip, one ray
@@ -129,6 +143,9 @@ __global__ __launch_bounds__(NT, SEM == 2 && NT == CNT_THREADS ? TSDF_F64_COUNT_
         if (blockIdx.x >= C->n_act) return;
         bx = Wk.act[blockIdx.x];
     }
+#ifdef TSDF_CNT_PHASE
+    unsigned long long cph[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, cpl = __builtin_readcyclecounter();
+#endif
     uint32_t t, r0, r1;
     block_range(D, bx, t, r0, r1);
     const float ox = D.s[t].ox, oy = D.s[t].oy, oz = D.s[t].oz;
@@ -138,6 +155,7 @@ __global__ __launch_bounds__(NT, SEM == 2 && NT == CNT_THREADS ? TSDF_F64_COUNT_
     }
     for (int j = threadIdx.x; j < 2 * PLC_WORDS; j += NT) (&s_bm[0][0])[j] = 0u;
     __syncthreads();
+    CPH(0);  // LDS init
     const uint32_t maxp = Wk.maxp;
     uint32_t valid = 0, npairs = 0;
     // The pair code of (ray, brick run): LDS-hash rank in the workgroup's run for the brick, or a
@@ -257,6 +275,7 @@ __global__ __launch_bounds__(NT, SEM == 2 && NT == CNT_THREADS ? TSDF_F64_COUNT_
                 }
 #endif
             }
+            CPH(1);  // point load + walk
             if (np > maxp) atomicOr(&C->ovf, OVF_PAIRS);  // beyond the geometric bound
             k = min(np, maxp);
             uint4 code = make_uint4(NO_PAIR, NO_PAIR, NO_PAIR, NO_PAIR);
@@ -302,8 +321,10 @@ __global__ __launch_bounds__(NT, SEM == 2 && NT == CNT_THREADS ? TSDF_F64_COUNT_
             for (uint32_t j = k; j < maxp; j++) pc[j] = NO_PAIR;
         }
         npairs += k;
+        CPH(2);  // pair emission (LDS hash) + pair-code store
     }
     __syncthreads();
+    CPH(3);  // the block's slowest wave
     // one global find-or-insert + one atomic per distinct brick of the workgroup: the cell
     // (brick, scan) count reserves the workgroup's ranks; `touched` (a plain store) lists the brick
     // for k_compact, which also derives the brick's total from its cells.  Each thread takes
@@ -359,6 +380,7 @@ __global__ __launch_bounds__(NT, SEM == 2 && NT == CNT_THREADS ? TSDF_F64_COUNT_
     // overlap instead of running one slot after another: (1) first-probe loads of all keys,
     // (2) resolve (a hit needs nothing more; an empty or taken first slot takes the probing path),
     // (3) the cell atomics of all found bricks.
+    CPH(4);  // block scan
     uint64_t key[SPT], h0[SPT], k0[SPT];
 #pragma unroll
     for (int j = 0; j < SPT; j++) {
@@ -374,6 +396,7 @@ __global__ __launch_bounds__(NT, SEM == 2 && NT == CNT_THREADS ? TSDF_F64_COUNT_
         if (key[j] != EMPTY_KEY)
             hx[j] = k0[j] == key[j] ? (int64_t)h0[j] : table_insert(T, key[j], &C->ovf);
     }
+    CPH(5);  // first probes + inserts
     uint32_t old[SPT];
 #pragma unroll
     for (int j = 0; j < SPT; j++) {
@@ -410,9 +433,11 @@ __global__ __launch_bounds__(NT, SEM == 2 && NT == CNT_THREADS ? TSDF_F64_COUNT_
             off1 += n1;
         }
     }
+    CPH(6);  // cell atomics + run lists
     // k_place's staging plan for each half: the run-start bitmap and its exclusive popcount
     // prefix per word (wave h writes half h's)
     __syncthreads();
+    CPH(7);
     {
         const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
         if (wv < 2) {
@@ -453,6 +478,13 @@ __global__ __launch_bounds__(NT, SEM == 2 && NT == CNT_THREADS ? TSDF_F64_COUNT_
         if (v) atomicAdd(&C->n_rays[blockIdx.x & 7], v);  // -> G->tot_rays at k_finish
         if (q) atomicAdd(&C->n_pairs[blockIdx.x & 7], q);
     }
+#ifdef TSDF_CNT_PHASE
+    CPH(8);  // plan + stats
+    if (threadIdx.x == 0 && blockIdx.x % 61 == 0 && NT == CNT_THREADS)
+        printf("cntphase %u init %llu walk %llu emit %llu bar %llu scan %llu probe %llu atom %llu "
+               "bar2 %llu tail %llu\n", blockIdx.x, cph[0], cph[1], cph[2], cph[3], cph[4], cph[5],
+               cph[6], cph[7], cph[8]);
+#endif
 }
 
 // ------------------------------------------------------------------------------------------------
