@@ -73,6 +73,39 @@ __device__ __forceinline__ int lds_insert(unsigned long long* s_key, uint64_t ke
     return -1;
 }
 
+// k_count's LDS brick hash with 32-bit keys (TSDF_CNT_KEY32): a brick relative to the
+// workgroup's base brick (its scan origin's), 11 bits per horizontal axis and 10 vertical
+// (+-1023 / +-511 bricks: 409 / 204 m at 5 cm); a brick beyond takes the global fallback.  Halves
+// the hash's LDS (16 -> 8 KiB), so more k_count workgroups fit beside k_integrate's (pipeline 2).
+constexpr uint32_t EMPTY32 = 0xFFFFFFFFu;
+struct KeyBase {
+    int bx, by, bz;
+};
+__device__ __forceinline__ uint32_t key32_of(uint64_t key, const KeyBase& kb) {
+    const int dx = (int)(key & 0x1FFFFFu) - BRICK_COORD_BIAS - kb.bx + 1024;
+    const int dy = (int)((key >> 21) & 0x1FFFFFu) - BRICK_COORD_BIAS - kb.by + 1024;
+    const int dz = (int)((key >> 42) & 0x1FFFFFu) - BRICK_COORD_BIAS - kb.bz + 512;
+    const bool ok = (uint32_t)dx < 2047u && (uint32_t)dy < 2047u && (uint32_t)dz < 1023u;
+    return ok ? (uint32_t)dx | ((uint32_t)dy << 11) | ((uint32_t)dz << 22) : EMPTY32;
+}
+__device__ __forceinline__ uint64_t key64_of(uint32_t k, const KeyBase& kb) {
+    return pack_brick((int)(k & 2047u) - 1024 + kb.bx, (int)((k >> 11) & 2047u) - 1024 + kb.by,
+                      (int)(k >> 22) - 512 + kb.bz);
+}
+__device__ __forceinline__ int lds_insert32(uint32_t* s_key, uint32_t key) {
+    uint32_t hs = (key * 0x9E3779B1u) >> (32 - __builtin_ctz((unsigned)HCAP));
+    for (int p = 0; p < LDS_PROBES; p++) {
+        const uint32_t k = s_key[hs];
+        if (k == key) return (int)hs;
+        if (k == EMPTY32) {
+            const uint32_t old = atomicCAS(&s_key[hs], EMPTY32, key);
+            if (old == EMPTY32 || old == key) return (int)hs;
+        }
+        hs = (hs + 1) & (HCAP - 1);
+    }
+    return -1;
+}
+
 // A workgroup-wide OR in one barrier: each wave publishes its vote in its own LDS slot
 // (__syncthreads_or takes three barriers: store, atomic OR, load).  Every lane of the workgroup
 // must call it; the slots may be reused after the next barrier.
@@ -128,7 +161,13 @@ template <int SEM, int NT = CNT_THREADS>
 __global__ __launch_bounds__(NT, SEM == 2 && NT == CNT_THREADS ? TSDF_F64_COUNT_WAVES : 1) void k_count(const float* __restrict__ xyz, BatchRef D,
                                                       RayConst R, Table T, Work Wk, Globals* G,
                                                       int parity) {
+#ifdef TSDF_CNT_KEY32
+    __shared__ uint32_t s_key[HCAP];
+    constexpr uint32_t S_EMPTY = EMPTY32;
+#else
     __shared__ unsigned long long s_key[HCAP];
+    constexpr unsigned long long S_EMPTY = EMPTY_KEY;
+#endif
     __shared__ uint32_t s_cnt[HCAP];
     __shared__ unsigned long long red[2][NT / 64];
     __shared__ unsigned long long s_wsum[NT / 64];
@@ -149,8 +188,12 @@ __global__ __launch_bounds__(NT, SEM == 2 && NT == CNT_THREADS ? TSDF_F64_COUNT_
     uint32_t t, r0, r1;
     block_range(D, bx, t, r0, r1);
     const float ox = D.s[t].ox, oy = D.s[t].oy, oz = D.s[t].oz;
+#ifdef TSDF_CNT_KEY32
+    const KeyBase kb{(int)__builtin_floorf(ox * R.inv_vs) >> 3, (int)__builtin_floorf(oy * R.inv_vs) >> 3,
+                     (int)__builtin_floorf(oz * R.inv_vs) >> 3};
+#endif
     for (int j = threadIdx.x; j < HCAP; j += NT) {
-        s_key[j] = EMPTY_KEY;
+        s_key[j] = S_EMPTY;
         s_cnt[j] = 0u;
     }
     for (int j = threadIdx.x; j < 2 * PLC_WORDS; j += NT) (&s_bm[0][0])[j] = 0u;
@@ -164,7 +207,12 @@ __global__ __launch_bounds__(NT, SEM == 2 && NT == CNT_THREADS ? TSDF_F64_COUNT_
     // runs one 512-lane workgroup per half), packed in s_cnt as n0 | n1 << 16 (a run holds at
     // most RPB/2 * MAX_IN_BRICK samples per half); the pair's rank is within its half's sub-run.
     auto pair_code = [&](uint64_t bkey, uint32_t cnt_in, uint32_t half) -> uint32_t {
+#ifdef TSDF_CNT_KEY32
+        const uint32_t k32 = key32_of(bkey, kb);
+        const int lid = k32 != EMPTY32 ? lds_insert32(s_key, k32) : -1;
+#else
         const int lid = lds_insert(s_key, bkey);
+#endif
         if (lid >= 0) {
             const uint32_t old = atomicAdd(&s_cnt[lid], half ? cnt_in << 16 : cnt_in);
             const uint32_t lr = half ? old >> 16 : old & 0xFFFFu;
@@ -339,7 +387,7 @@ __global__ __launch_bounds__(NT, SEM == 2 && NT == CNT_THREADS ? TSDF_F64_COUNT_
 #pragma unroll
     for (int j = 0; j < SPT; j++) {
         const int slot = threadIdx.x * SPT + j;
-        const uint32_t c = s_key[slot] != EMPTY_KEY ? s_cnt[slot] : 0u;
+        const uint32_t c = s_key[slot] != S_EMPTY ? s_cnt[slot] : 0u;
         n0s += c & 0xFFFFu;
         n1s += c >> 16;
         c01 += ((c & 0xFFFFu) ? 1u : 0u) | ((c >> 16) ? 1u << 16 : 0u);
@@ -385,7 +433,11 @@ __global__ __launch_bounds__(NT, SEM == 2 && NT == CNT_THREADS ? TSDF_F64_COUNT_
 #pragma unroll
     for (int j = 0; j < SPT; j++) {
         const int slot = threadIdx.x * SPT + j;
+#ifdef TSDF_CNT_KEY32
+        key[j] = s_key[slot] != EMPTY32 ? key64_of(s_key[slot], kb) : EMPTY_KEY;
+#else
         key[j] = s_key[slot];
+#endif
         h0[j] = mix64(key[j]) & T.mask;
         k0[j] = key[j] != EMPTY_KEY ? T.keys[h0[j]] : EMPTY_KEY;
     }
