@@ -328,10 +328,59 @@ __global__ __launch_bounds__(NT, SEM == 2 && NT == CNT_THREADS ? TSDF_F64_COUNT_
             k = min(np, maxp);
             uint4 code = make_uint4(NO_PAIR, NO_PAIR, NO_PAIR, NO_PAIR);
             const uint32_t hf = i - r0 >= (uint32_t)(RPB / 2) ? 1u : 0u;
+#if defined(TSDF_CNT_EMIT4) && !defined(TSDF_CNT_KEY32)
+            // The ray's <= 4 pairs go into the LDS hash side by side rather than one chain after
+            // the other: all first probes, then the CASes they call for, then the count atomics,
+            // so a lane has up to four LDS round trips in flight per stage instead of one.  A
+            // first probe that meets another key (rare: ~0.3 load) takes lds_insert's full probe.
+            {
+                const uint64_t qk[4] = {q0, q1, q2, q3};
+                const uint32_t qn[4] = {n0, n1, n2, n3};
+                uint32_t hs[4];
+                unsigned long long kv[4];
+                int lid[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    hs[j] = (uint32_t)(mix64(qk[j]) >> 40) & (HCAP - 1);
+                    kv[j] = (uint32_t)j < k ? s_key[hs[j]] : 0ull;
+                }
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    lid[j] = -1;
+                    if ((uint32_t)j < k) {
+                        if (kv[j] == qk[j]) {
+                            lid[j] = (int)hs[j];
+                        } else if (kv[j] == EMPTY_KEY) {
+                            const unsigned long long o = atomicCAS(&s_key[hs[j]], EMPTY_KEY, qk[j]);
+                            lid[j] = (o == EMPTY_KEY || o == qk[j]) ? (int)hs[j] : -2;
+                        } else {
+                            lid[j] = -2;
+                        }
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    if (lid[j] == -2) lid[j] = lds_insert(s_key, qk[j]);
+                uint32_t cv[4] = {NO_PAIR, NO_PAIR, NO_PAIR, NO_PAIR};
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    if ((uint32_t)j >= k) continue;
+                    if (lid[j] >= 0) {
+                        const uint32_t o = atomicAdd(&s_cnt[lid[j]], hf ? qn[j] << 16 : qn[j]);
+                        const uint32_t lr = hf ? o >> 16 : o & 0xFFFFu;
+                        cv[j] = (qn[j] << PAIR_CNT_SHIFT) | ((uint32_t)lid[j] << PAIR_LID_SHIFT) | lr;
+                    } else {
+                        cv[j] = pair_code(qk[j], qn[j], hf);  // the LDS hash is full: global path
+                    }
+                }
+                code = make_uint4(cv[0], cv[1], cv[2], cv[3]);
+            }
+#else
             if (k > 0) code.x = pair_code(q0, n0, hf);
             if (k > 1) code.y = pair_code(q1, n1, hf);
             if (k > 2) code.z = pair_code(q2, n2, hf);
             if (k > 3) code.w = pair_code(q3, n3, hf);
+#endif
             if (maxp == 4) {
                 *reinterpret_cast<uint4*>(pc) = code;  // one 16-B store per ray
             } else {
