@@ -216,6 +216,9 @@ struct tsdf_ctx {
     // batches of at most count_wide k_count blocks (about 4 full scans: too few workgroups of 256
     // lanes to fill the chip) run k_count with 1024-lane workgroups (TSDF_COUNT_WIDE; 0: never)
     uint32_t count_wide = 512;
+    // TSDF_COUNT_PAIRED=1: larger batches run k_count with two blocks per 512-lane workgroup
+    // (bit-exact, ~29% fewer cell atomics, but measured slower: DESIGN.md §10, round 4)
+    bool count_paired = false;
     // host-pointer path: pinned double buffer per scan; the pending batch's points are staged in
     // stage2[batch parity]
     float* h_stage[2] = {nullptr, nullptr};
@@ -459,7 +462,8 @@ static int launch(tsdf_ctx* c, const float* d_xyz, BatchDesc& D) {
         if (c->R.sec_on) HIPCHK(c, launch_sector_flags(d_rays, B, R, W, c->G, par, st));
         if (c->fused) HIPCHK(c, launch_walk(d_rays, B, R, T, W, c->G, par, c->nstep, st));
         else HIPCHK(c, launch_count(d_rays, B, R, T, W, c->G, par, st, kt(KIND_COUNT),
-                                    !c->R.sec_on && D.n_blocks <= c->count_wide));
+                                    !c->R.sec_on && D.n_blocks <= c->count_wide,
+                                    !c->R.sec_on && c->count_paired));
         c->ht.lap(3);
         if (tm && c->fused) tm->next(k_front, KIND_COMPACT, st);
         HIPCHK(c, launch_compact(B, T, W, c->G, par, c->fused, st, kt(KIND_COMPACT)));
@@ -1286,6 +1290,7 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
     HIPCHK(c, hipMalloc(&c->G, sizeof(Globals)));
     if (const char* e = std::getenv("TSDF_SMALL_NS")) c->small_ns = std::max(0, std::min(8, std::atoi(e)));
     if (const char* e = std::getenv("TSDF_COUNT_WIDE")) c->count_wide = (uint32_t)std::max(0, std::atoi(e));
+    if (const char* e = std::getenv("TSDF_COUNT_PAIRED")) c->count_paired = std::atoi(e) != 0;
     {
         // host staging threads: 3 workers + the caller (TSDF_PACK_THREADS overrides; 1 = none)
         int nt = 4;

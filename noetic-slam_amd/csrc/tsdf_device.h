@@ -283,7 +283,7 @@ struct KernelTimer {
 
 hipError_t launch_count(const float* d_xyz, const BatchRef& D, const RayConst& R, const Table& T,
                         const Work& Wk, Globals* G, int parity, hipStream_t st, const KTime& kt = {},
-                        bool wide = false);
+                        bool wide = false, bool paired = false);
 // table chunks of k_compact (Work::cagg holds two uint4 per chunk)
 #ifndef TSDF_CMP_CHUNK
 #define TSDF_CMP_CHUNK 1024

@@ -73,39 +73,6 @@ __device__ __forceinline__ int lds_insert(unsigned long long* s_key, uint64_t ke
     return -1;
 }
 
-// k_count's LDS brick hash with 32-bit keys (TSDF_CNT_KEY32): a brick relative to the
-// workgroup's base brick (its scan origin's), 11 bits per horizontal axis and 10 vertical
-// (+-1023 / +-511 bricks: 409 / 204 m at 5 cm); a brick beyond takes the global fallback.  Halves
-// the hash's LDS (16 -> 8 KiB), so more k_count workgroups fit beside k_integrate's (pipeline 2).
-constexpr uint32_t EMPTY32 = 0xFFFFFFFFu;
-struct KeyBase {
-    int bx, by, bz;
-};
-__device__ __forceinline__ uint32_t key32_of(uint64_t key, const KeyBase& kb) {
-    const int dx = (int)(key & 0x1FFFFFu) - BRICK_COORD_BIAS - kb.bx + 1024;
-    const int dy = (int)((key >> 21) & 0x1FFFFFu) - BRICK_COORD_BIAS - kb.by + 1024;
-    const int dz = (int)((key >> 42) & 0x1FFFFFu) - BRICK_COORD_BIAS - kb.bz + 512;
-    const bool ok = (uint32_t)dx < 2047u && (uint32_t)dy < 2047u && (uint32_t)dz < 1023u;
-    return ok ? (uint32_t)dx | ((uint32_t)dy << 11) | ((uint32_t)dz << 22) : EMPTY32;
-}
-__device__ __forceinline__ uint64_t key64_of(uint32_t k, const KeyBase& kb) {
-    return pack_brick((int)(k & 2047u) - 1024 + kb.bx, (int)((k >> 11) & 2047u) - 1024 + kb.by,
-                      (int)(k >> 22) - 512 + kb.bz);
-}
-__device__ __forceinline__ int lds_insert32(uint32_t* s_key, uint32_t key) {
-    uint32_t hs = (key * 0x9E3779B1u) >> (32 - __builtin_ctz((unsigned)HCAP));
-    for (int p = 0; p < LDS_PROBES; p++) {
-        const uint32_t k = s_key[hs];
-        if (k == key) return (int)hs;
-        if (k == EMPTY32) {
-            const uint32_t old = atomicCAS(&s_key[hs], EMPTY32, key);
-            if (old == EMPTY32 || old == key) return (int)hs;
-        }
-        hs = (hs + 1) & (HCAP - 1);
-    }
-    return -1;
-}
-
 // A workgroup-wide OR in one barrier: each wave publishes its vote in its own LDS slot
 // (__syncthreads_or takes three barriers: store, atomic OR, load).  Every lane of the workgroup
 // must call it; the slots may be reused after the next barrier.
@@ -147,9 +114,15 @@ __device__ __forceinline__ bool block_any(bool p, uint32_t* s_vote) {
 #endif
 constexpr int CNT_THREADS = TSDF_CNT_THREADS;
 
-// NT: threads per workgroup (NT; 1024 for batches too small to fill the chip, one ray
-// per lane, so each SIMD holds four waves of one workgroup).
-template <int SEM, int NT = CNT_THREADS>
+// NT: threads per workgroup (1024 for batches too small to fill the chip, one ray per lane, so
+// each SIMD holds four waves of one workgroup).  G: RPB-ray blocks per workgroup.  G = 2 (the
+// default for full batches) takes two adjacent blocks of a scan in one 512-lane
+// workgroup with one LDS brick hash, so a brick both wedges reach costs ONE global probe and ONE
+// cell atomic instead of two (runs per 64-scan launch ~5.2 M -> ~3.7 M).  The run lists, staging
+// plans and pair codes stay per (block, half), exactly as k_place reads them; a brick's LDS slot
+// counts its samples in 2G 16-bit sub-counters, one per (block, half).  Two blocks of different
+// scans (a scan with an odd block count) keep their bricks apart by a block bit in the LDS key.
+template <int SEM, int NT = CNT_THREADS, int G = 1>
 // TSDF_SEM_VDBFUSION_F64: the fp32 filter's rare double branch would lift k_count to 93 VGPRs (5
 // waves per SIMD); the bound keeps the LDS-limited 6, spilling only inside that branch
 #ifndef TSDF_F64_COUNT_WAVES
@@ -158,64 +131,60 @@ template <int SEM, int NT = CNT_THREADS>
 #ifndef TSDF_F64_PLACE_WAVES
 #define TSDF_F64_PLACE_WAVES 1
 #endif
-__global__ __launch_bounds__(NT, SEM == 2 && NT == CNT_THREADS ? TSDF_F64_COUNT_WAVES : 1) void k_count(const float* __restrict__ xyz, BatchRef D,
-                                                      RayConst R, Table T, Work Wk, Globals* G,
+__global__ __launch_bounds__(NT, SEM == 2 && (NT == CNT_THREADS || G == 2) ? TSDF_F64_COUNT_WAVES : 1) void k_count(const float* __restrict__ xyz, BatchRef D,
+                                                      RayConst R, Table T, Work Wk, Globals* G_,
                                                       int parity) {
-#ifdef TSDF_CNT_KEY32
-    __shared__ uint32_t s_key[HCAP];
-    constexpr uint32_t S_EMPTY = EMPTY32;
-#else
+    static_assert(G == 1 || G == 2, "one or two blocks per workgroup");
+    static_assert(G == 1 || RPB % NT == 0, "a pass over the rays stays inside one block");
+    using CntT = typename std::conditional<G == 2, unsigned long long, uint32_t>::type;
+    constexpr int NSUB = 2 * G;  // (block, half) sub-runs
+    constexpr uint64_t KEY_G1 = 1ull << 63;  // LDS key bit: block 1 of a workgroup spanning two scans
     __shared__ unsigned long long s_key[HCAP];
-    constexpr unsigned long long S_EMPTY = EMPTY_KEY;
-#endif
-    __shared__ uint32_t s_cnt[HCAP];
+    __shared__ CntT s_cnt[HCAP];
     __shared__ unsigned long long red[2][NT / 64];
-    __shared__ unsigned long long s_wsum[NT / 64];
-    __shared__ uint32_t s_wcnt[NT / 64];
-    __shared__ uint32_t s_bm[2][PLC_WORDS];  // per half: staging positions where a run starts
-    Counters* C = &G->ctr[parity];  // zeroed by the previous batch of this parity (k_finish)
+    __shared__ unsigned long long s_wsum[G][NT / 64];
+    __shared__ uint32_t s_wcnt[G][NT / 64];
+    __shared__ uint32_t s_bm[NSUB][PLC_WORDS];  // per sub-run list: staging positions where a run starts
+    Counters* C = &G_->ctr[parity];  // zeroed by the previous batch of this parity (k_finish)
     // sector sharding: every GPU sees every scan, and a block of 1024 consecutive rays (~3 degrees
     // of azimuth) usually lies wholly in one sector; the workgroups take the blocks k_sector_flags
-    // listed, the rest of the grid leaves at once
-    uint32_t bx = xcd_wedge(blockIdx.x, gridDim.x, 16);
-    if (R.sec_on) {
-        if (blockIdx.x >= C->n_act) return;
-        bx = Wk.act[blockIdx.x];
+    // listed, the rest of the grid leaves at once (G = 1 only)
+    uint32_t bx = xcd_wedge(blockIdx.x, gridDim.x, 16 / G);
+    if constexpr (G == 1) {
+        if (R.sec_on) {
+            if (blockIdx.x >= C->n_act) return;
+            bx = Wk.act[blockIdx.x];
+        }
     }
 #ifdef TSDF_CNT_PHASE
     unsigned long long cph[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, cpl = __builtin_readcyclecounter();
 #endif
-    uint32_t t, r0, r1;
-    block_range(D, bx, t, r0, r1);
-    const float ox = D.s[t].ox, oy = D.s[t].oy, oz = D.s[t].oz;
-#ifdef TSDF_CNT_KEY32
-    const KeyBase kb{(int)__builtin_floorf(ox * R.inv_vs) >> 3, (int)__builtin_floorf(oy * R.inv_vs) >> 3,
-                     (int)__builtin_floorf(oz * R.inv_vs) >> 3};
-#endif
+    // block g of the workgroup is G bx + g (past the batch's last block: an empty range)
+    uint32_t tb[G], r0b[G], r1b[G];
+#pragma unroll
+    for (int g = 0; g < G; g++) block_range(D, G * bx + g, tb[g], r0b[g], r1b[g]);
+    const bool split = G == 2 && tb[G - 1] != tb[0];
     for (int j = threadIdx.x; j < HCAP; j += NT) {
-        s_key[j] = S_EMPTY;
+        s_key[j] = EMPTY_KEY;
         s_cnt[j] = 0u;
     }
-    for (int j = threadIdx.x; j < 2 * PLC_WORDS; j += NT) (&s_bm[0][0])[j] = 0u;
+    for (int j = threadIdx.x; j < NSUB * PLC_WORDS; j += NT) (&s_bm[0][0])[j] = 0u;
     __syncthreads();
     CPH(0);  // LDS init
     const uint32_t maxp = Wk.maxp;
     uint32_t valid = 0, npairs = 0;
     // The pair code of (ray, brick run): LDS-hash rank in the workgroup's run for the brick, or a
     // fallback record when the LDS hash is full.  cnt_in = the pair's gated voxels (<= MAX_IN_BRICK).
-    // A run's samples are counted per half workgroup (rays [0, RPB/2) and [RPB/2, RPB): k_place
-    // runs one 512-lane workgroup per half), packed in s_cnt as n0 | n1 << 16 (a run holds at
-    // most RPB/2 * MAX_IN_BRICK samples per half); the pair's rank is within its half's sub-run.
-    auto pair_code = [&](uint64_t bkey, uint32_t cnt_in, uint32_t half) -> uint32_t {
-#ifdef TSDF_CNT_KEY32
-        const uint32_t k32 = key32_of(bkey, kb);
-        const int lid = k32 != EMPTY32 ? lds_insert32(s_key, k32) : -1;
-#else
-        const int lid = lds_insert(s_key, bkey);
-#endif
+    // A run's samples are counted per (block, half) -- rays [0, RPB/2) and [RPB/2, RPB) of the
+    // block: k_place runs one 512-lane workgroup per half -- as 16-bit fields of s_cnt, field
+    // sub = 2 g + half (a field holds at most RPB/2 * MAX_IN_BRICK samples); the pair's rank is
+    // within its sub-run.
+    auto pair_code = [&](uint64_t bkey, uint32_t cnt_in, uint32_t sub, uint32_t t) -> uint32_t {
+        const uint64_t lkey = split && sub >= 2 ? bkey | KEY_G1 : bkey;
+        const int lid = lds_insert(s_key, lkey);
         if (lid >= 0) {
-            const uint32_t old = atomicAdd(&s_cnt[lid], half ? cnt_in << 16 : cnt_in);
-            const uint32_t lr = half ? old >> 16 : old & 0xFFFFu;
+            const CntT old = atomicAdd(&s_cnt[lid], (CntT)cnt_in << (16 * sub));
+            const uint32_t lr = (uint32_t)(old >> (16 * sub)) & 0xFFFFu;
             return (cnt_in << PAIR_CNT_SHIFT) | ((uint32_t)lid << PAIR_LID_SHIFT) | lr;
         }
         const uint32_t f = atomicAdd(&C->n_fb, 1u);  // LDS hash full: the global path
@@ -231,77 +200,108 @@ __global__ __launch_bounds__(NT, SEM == 2 && NT == CNT_THREADS ? TSDF_F64_COUNT_
         Wk.fb[f] = make_uint4(h, t, rk, 0u);
         return PAIR_FB | (cnt_in << PAIR_CNT_SHIFT) | f;
     };
-    for (uint32_t i = r0 + threadIdx.x; i < r1; i += NT) {
-        uint32_t* pc = Wk.pair + (size_t)i * maxp;
-        uint32_t k = 0;
-        typename Walk<SEM>::State r;
-        const bool ok = Walk<SEM>::init(R, D, t, i, xyz[3 * (size_t)i], xyz[3 * (size_t)i + 1],
-                                        xyz[3 * (size_t)i + 2], r);
-        valid += ok ? 1u : 0u;
-        // One pair per distinct brick; a line visits a brick in one contiguous run of DDA voxels,
-        // so a pair closes when the next gated voxel's brick differs.
-        if (maxp <= 4) {
-            // Short rays (no carving): the walk only records its <= 4 pairs in registers; all lanes
-            // then emit pair j together, so the LDS hash work runs convergent, not once per lane.
-            uint64_t q0 = EMPTY_KEY, q1 = EMPTY_KEY, q2 = EMPTY_KEY, q3 = EMPTY_KEY;
-            uint32_t n0 = 0, n1 = 0, n2 = 0, n3 = 0, np = 0;
+    // G = 1: the lanes stride the block's rays; G = 2: pass q covers rays [q NT, (q + 1) NT) of
+    // the workgroup's 2 RPB, so the block (and its scan) is uniform in a pass
+    constexpr int PASSES = G == 1 ? 1 : G * RPB / NT;
+#pragma unroll 1
+    for (int pass = 0; pass < PASSES; pass++) {
+        const int g = G == 1 ? 0 : pass * NT / RPB;
+        // selects, not array indexing: a dynamically indexed private array would live in scratch
+        const uint32_t t = g ? tb[G - 1] : tb[0], r0 = g ? r0b[G - 1] : r0b[0];
+        const uint32_t r1 = g ? r1b[G - 1] : r1b[0];
+        const float ox = D.s[t].ox, oy = D.s[t].oy, oz = D.s[t].oz;
+        const uint32_t lo = G == 1 ? r0 + threadIdx.x : r0 + (uint32_t)(pass * NT) % RPB + threadIdx.x;
+        const uint32_t hi = G == 1 ? r1 : min(r1, r0 + (uint32_t)(pass * NT) % RPB + NT);
+        for (uint32_t i = lo; i < hi; i += NT) {
+            uint32_t* pc = Wk.pair + (size_t)i * maxp;
+            uint32_t k = 0;
+            typename Walk<SEM>::State r;
+            const bool ok = Walk<SEM>::init(R, D, t, i, xyz[3 * (size_t)i], xyz[3 * (size_t)i + 1],
+                                            xyz[3 * (size_t)i + 2], r);
+            valid += ok ? 1u : 0u;
+            const uint32_t sub = 2u * (uint32_t)g + (i - r0 >= (uint32_t)(RPB / 2) ? 1u : 0u);
+            // One pair per distinct brick; a line visits a brick in one contiguous run of DDA
+            // voxels, so a pair closes when the next gated voxel's brick differs.
+            if (maxp <= 4) {
+                // Short rays (no carving): the walk only records its <= 4 pairs in registers; all
+                // lanes then emit pair j together, so the LDS hash work runs convergent, not once
+                // per lane.
+                uint64_t q0 = EMPTY_KEY, q1 = EMPTY_KEY, q2 = EMPTY_KEY, q3 = EMPTY_KEY;
+                uint32_t n0 = 0, n1 = 0, n2 = 0, n3 = 0, np = 0;
 #ifdef TSDF_ABLATE_CNT_NOWALK
-            if (ok && r.px == 1e30f) {
+                if (ok && r.px == 1e30f) {
 #else
-            if (ok) {
+                if (ok) {
 #endif
-#ifndef TSDF_CNT_BRANCHY
-                // Branch-free walk (lanes are at different steps of different rays): the gate and
-                // the pair bookkeeping are selects on 32-bit brick codes; the 64-bit keys are built
-                // from the codes after the walk (code_key: a ray's bricks lie within one brick of
-                // its first one per axis).
-                const int bx0 = r.vx >> 3, by0 = r.vy >> 3, bz0 = r.vz >> 3;
-                uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0, curc = ~0u, ccount = 0;
-                auto walk = [&](auto chk) {
-                    for (int it = 0; it < MAX_DDA_STEPS; it++) {
-                        const bool g = Walk<SEM>::gate_sel(R, ox, oy, oz, r, decltype(chk)::value);
-                        const uint32_t bc = brick_code_of(r.vx, r.vy, r.vz);
-                        const bool nb = g && bc != curc;
-                        const bool cl = nb && curc != ~0u;  // the previous pair closes
-                        c0 = (cl && np == 0) ? curc : c0; n0 = (cl && np == 0) ? ccount : n0;
-                        c1 = (cl && np == 1) ? curc : c1; n1 = (cl && np == 1) ? ccount : n1;
-                        c2 = (cl && np == 2) ? curc : c2; n2 = (cl && np == 2) ? ccount : n2;
-                        c3 = (cl && np == 3) ? curc : c3; n3 = (cl && np == 3) ? ccount : n3;
-                        np += cl ? 1u : 0u;
-                        curc = nb ? bc : curc;
-                        ccount = (nb ? 0u : ccount) + (g ? 1u : 0u);
-                        if (!Walk<SEM>::step(r)) break;
+                    // Branch-free walk (lanes are at different steps of different rays): the gate
+                    // and the pair bookkeeping are selects on 32-bit brick codes; the 64-bit keys
+                    // are built from the codes after the walk (code_key: a ray's bricks lie within
+                    // one brick of its first one per axis).
+                    const int bx0 = r.vx >> 3, by0 = r.vy >> 3, bz0 = r.vz >> 3;
+                    uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0, curc = ~0u, ccount = 0;
+                    auto walk = [&](auto chk) {
+                        for (int it = 0; it < MAX_DDA_STEPS; it++) {
+                            const bool gt = Walk<SEM>::gate_sel(R, ox, oy, oz, r, decltype(chk)::value);
+                            const uint32_t bc = brick_code_of(r.vx, r.vy, r.vz);
+                            const bool nb = gt && bc != curc;
+                            const bool cl = nb && curc != ~0u;  // the previous pair closes
+                            c0 = (cl && np == 0) ? curc : c0; n0 = (cl && np == 0) ? ccount : n0;
+                            c1 = (cl && np == 1) ? curc : c1; n1 = (cl && np == 1) ? ccount : n1;
+                            c2 = (cl && np == 2) ? curc : c2; n2 = (cl && np == 2) ? ccount : n2;
+                            c3 = (cl && np == 3) ? curc : c3; n3 = (cl && np == 3) ? ccount : n3;
+                            np += cl ? 1u : 0u;
+                            curc = nb ? bc : curc;
+                            ccount = (nb ? 0u : ccount) + (gt ? 1u : 0u);
+                            if (!Walk<SEM>::step(r)) break;
+                        }
+                    };
+                    // rays far from the index-domain edge (all, in practice) skip the per-voxel check
+                    if (__all(Walk<SEM>::inside(R, r))) walk(std::false_type{});
+                    else walk(std::true_type{});
+                    if (curc != ~0u) {
+                        c0 = np == 0 ? curc : c0; n0 = np == 0 ? ccount : n0;
+                        c1 = np == 1 ? curc : c1; n1 = np == 1 ? ccount : n1;
+                        c2 = np == 2 ? curc : c2; n2 = np == 2 ? ccount : n2;
+                        c3 = np == 3 ? curc : c3; n3 = np == 3 ? ccount : n3;
+                        np++;
                     }
-                };
-                if (__all(Walk<SEM>::inside(R, r))) walk(std::false_type{});
-                else walk(std::true_type{});
-                if (curc != ~0u) {
-                    c0 = np == 0 ? curc : c0; n0 = np == 0 ? ccount : n0;
-                    c1 = np == 1 ? curc : c1; n1 = np == 1 ? ccount : n1;
-                    c2 = np == 2 ? curc : c2; n2 = np == 2 ? ccount : n2;
-                    c3 = np == 3 ? curc : c3; n3 = np == 3 ? ccount : n3;
-                    np++;
+                    if (np > 0) q0 = code_key(c0, bx0, by0, bz0);
+                    if (np > 1) q1 = code_key(c1, bx0, by0, bz0);
+                    if (np > 2) q2 = code_key(c2, bx0, by0, bz0);
+                    if (np > 3) q3 = code_key(c3, bx0, by0, bz0);
                 }
-                if (np > 0) q0 = code_key(c0, bx0, by0, bz0);
-                if (np > 1) q1 = code_key(c1, bx0, by0, bz0);
-                if (np > 2) q2 = code_key(c2, bx0, by0, bz0);
-                if (np > 3) q3 = code_key(c3, bx0, by0, bz0);
-#else
-                uint64_t cur = EMPTY_KEY;
-                uint32_t curc = ~0u, ccount = 0;
-                // a pair boundary is a brick-code change (32-bit); the full key is built per pair
-                auto walk = [&](auto chk) {
+                CPH(1);  // point load + walk
+                if (np > maxp) atomicOr(&C->ovf, OVF_PAIRS);  // beyond the geometric bound
+                k = min(np, maxp);
+                uint4 code = make_uint4(NO_PAIR, NO_PAIR, NO_PAIR, NO_PAIR);
+                if (k > 0) code.x = pair_code(q0, n0, sub, t);
+                if (k > 1) code.y = pair_code(q1, n1, sub, t);
+                if (k > 2) code.z = pair_code(q2, n2, sub, t);
+                if (k > 3) code.w = pair_code(q3, n3, sub, t);
+                if (maxp == 4) {
+                    *reinterpret_cast<uint4*>(pc) = code;  // one 16-B store per ray
+                } else {
+                    const uint32_t cv[4] = {code.x, code.y, code.z, code.w};
+#pragma unroll
+                    for (uint32_t j = 0; j < 4; j++)
+                        if (j < maxp) pc[j] = cv[j];
+                }
+            } else {
+                if (ok) {
+                    uint64_t cur = EMPTY_KEY;
+                    uint32_t curc = ~0u, ccount = 0;
+                    auto emit = [&](uint64_t bkey, uint32_t cnt_in) {
+                        if (k >= maxp) {
+                            atomicOr(&C->ovf, OVF_PAIRS);
+                            return;
+                        }
+                        pc[k++] = pair_code(bkey, cnt_in, sub, t);
+                    };
                     for (int it = 0; it < MAX_DDA_STEPS; it++) {
-                        if (Walk<SEM>::gate(R, ox, oy, oz, r, decltype(chk)::value)) {
+                        if (Walk<SEM>::gate(R, ox, oy, oz, r)) {
                             const uint32_t bc = brick_code_of(r.vx, r.vy, r.vz);
                             if (bc != curc) {
-                                if (cur != EMPTY_KEY) {
-                                    q0 = np == 0 ? cur : q0; n0 = np == 0 ? ccount : n0;
-                                    q1 = np == 1 ? cur : q1; n1 = np == 1 ? ccount : n1;
-                                    q2 = np == 2 ? cur : q2; n2 = np == 2 ? ccount : n2;
-                                    q3 = np == 3 ? cur : q3; n3 = np == 3 ? ccount : n3;
-                                    np++;
-                                }
+                                if (cur != EMPTY_KEY) emit(cur, ccount);
                                 cur = brick_key_of(r.vx, r.vy, r.vz);
                                 curc = bc;
                                 ccount = 0;
@@ -310,211 +310,149 @@ __global__ __launch_bounds__(NT, SEM == 2 && NT == CNT_THREADS ? TSDF_F64_COUNT_
                         }
                         if (!Walk<SEM>::step(r)) break;
                     }
-                };
-                // rays far from the index-domain edge (all, in practice) skip the per-voxel check
-                if (__all(Walk<SEM>::inside(R, r))) walk(std::false_type{});
-                else walk(std::true_type{});
-                if (cur != EMPTY_KEY) {
-                    q0 = np == 0 ? cur : q0; n0 = np == 0 ? ccount : n0;
-                    q1 = np == 1 ? cur : q1; n1 = np == 1 ? ccount : n1;
-                    q2 = np == 2 ? cur : q2; n2 = np == 2 ? ccount : n2;
-                    q3 = np == 3 ? cur : q3; n3 = np == 3 ? ccount : n3;
-                    np++;
+                    if (cur != EMPTY_KEY) emit(cur, ccount);
                 }
-#endif
+                for (uint32_t j = k; j < maxp; j++) pc[j] = NO_PAIR;
             }
-            CPH(1);  // point load + walk
-            if (np > maxp) atomicOr(&C->ovf, OVF_PAIRS);  // beyond the geometric bound
-            k = min(np, maxp);
-            uint4 code = make_uint4(NO_PAIR, NO_PAIR, NO_PAIR, NO_PAIR);
-            const uint32_t hf = i - r0 >= (uint32_t)(RPB / 2) ? 1u : 0u;
-#if defined(TSDF_CNT_EMIT4) && !defined(TSDF_CNT_KEY32)
-            // The ray's <= 4 pairs go into the LDS hash side by side rather than one chain after
-            // the other: all first probes, then the CASes they call for, then the count atomics,
-            // so a lane has up to four LDS round trips in flight per stage instead of one.  A
-            // first probe that meets another key (rare: ~0.3 load) takes lds_insert's full probe.
-            {
-                const uint64_t qk[4] = {q0, q1, q2, q3};
-                const uint32_t qn[4] = {n0, n1, n2, n3};
-                uint32_t hs[4];
-                unsigned long long kv[4];
-                int lid[4];
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    hs[j] = (uint32_t)(mix64(qk[j]) >> 40) & (HCAP - 1);
-                    kv[j] = (uint32_t)j < k ? s_key[hs[j]] : 0ull;
-                }
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    lid[j] = -1;
-                    if ((uint32_t)j < k) {
-                        if (kv[j] == qk[j]) {
-                            lid[j] = (int)hs[j];
-                        } else if (kv[j] == EMPTY_KEY) {
-                            const unsigned long long o = atomicCAS(&s_key[hs[j]], EMPTY_KEY, qk[j]);
-                            lid[j] = (o == EMPTY_KEY || o == qk[j]) ? (int)hs[j] : -2;
-                        } else {
-                            lid[j] = -2;
-                        }
-                    }
-                }
-#pragma unroll
-                for (int j = 0; j < 4; j++)
-                    if (lid[j] == -2) lid[j] = lds_insert(s_key, qk[j]);
-                uint32_t cv[4] = {NO_PAIR, NO_PAIR, NO_PAIR, NO_PAIR};
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    if ((uint32_t)j >= k) continue;
-                    if (lid[j] >= 0) {
-                        const uint32_t o = atomicAdd(&s_cnt[lid[j]], hf ? qn[j] << 16 : qn[j]);
-                        const uint32_t lr = hf ? o >> 16 : o & 0xFFFFu;
-                        cv[j] = (qn[j] << PAIR_CNT_SHIFT) | ((uint32_t)lid[j] << PAIR_LID_SHIFT) | lr;
-                    } else {
-                        cv[j] = pair_code(qk[j], qn[j], hf);  // the LDS hash is full: global path
-                    }
-                }
-                code = make_uint4(cv[0], cv[1], cv[2], cv[3]);
-            }
-#else
-            if (k > 0) code.x = pair_code(q0, n0, hf);
-            if (k > 1) code.y = pair_code(q1, n1, hf);
-            if (k > 2) code.z = pair_code(q2, n2, hf);
-            if (k > 3) code.w = pair_code(q3, n3, hf);
-#endif
-            if (maxp == 4) {
-                *reinterpret_cast<uint4*>(pc) = code;  // one 16-B store per ray
-            } else {
-                const uint32_t cv[4] = {code.x, code.y, code.z, code.w};
-#pragma unroll
-                for (uint32_t j = 0; j < 4; j++)
-                    if (j < maxp) pc[j] = cv[j];
-            }
-        } else {
-            if (ok) {
-                uint64_t cur = EMPTY_KEY;
-                uint32_t curc = ~0u, ccount = 0;
-                auto emit = [&](uint64_t bkey, uint32_t cnt_in) {
-                    if (k >= maxp) {
-                        atomicOr(&C->ovf, OVF_PAIRS);
-                        return;
-                    }
-                    pc[k++] = pair_code(bkey, cnt_in, i - r0 >= (uint32_t)(RPB / 2) ? 1u : 0u);
-                };
-                for (int it = 0; it < MAX_DDA_STEPS; it++) {
-                    if (Walk<SEM>::gate(R, ox, oy, oz, r)) {
-                        const uint32_t bc = brick_code_of(r.vx, r.vy, r.vz);
-                        if (bc != curc) {
-                            if (cur != EMPTY_KEY) emit(cur, ccount);
-                            cur = brick_key_of(r.vx, r.vy, r.vz);
-                            curc = bc;
-                            ccount = 0;
-                        }
-                        ccount++;
-                    }
-                    if (!Walk<SEM>::step(r)) break;
-                }
-                if (cur != EMPTY_KEY) emit(cur, ccount);
-            }
-            for (uint32_t j = k; j < maxp; j++) pc[j] = NO_PAIR;
+            npairs += k;
+            CPH(2);  // pair emission (LDS hash) + pair-code store
         }
-        npairs += k;
-        CPH(2);  // pair emission (LDS hash) + pair-code store
     }
     __syncthreads();
     CPH(3);  // the block's slowest wave
     // one global find-or-insert + one atomic per distinct brick of the workgroup: the cell
     // (brick, scan) count reserves the workgroup's ranks; `touched` (a plain store) lists the brick
     // for k_compact, which also derives the brick's total from its cells.  Each thread takes
-    // HCAP / NT consecutive slots; a block scan over their sample and run counts gives
-    // every run its offset in the workgroup's sample order (k_place stages the samples in that
-    // order) and its index in the workgroup's DENSE run list (slot order = sample order).
+    // HCAP / NT consecutive slots; a block scan over their sample and run counts gives every
+    // sub-run its offset in its (block, half)'s sample order (k_place stages the samples in that
+    // order) and its index in the (block, half)'s DENSE run list (slot order = sample order).
     constexpr int SPT = HCAP / NT;
-    // two dense run lists per workgroup, one per half (k_place workgroup 2 b + half)
-    uint4* bt0 = Wk.blk + (size_t)bx * 2 * HCAP;
-    uint4* bt1 = bt0 + HCAP;
-    uint32_t n0s = 0, n1s = 0, c01 = 0;
+    static_assert(SPT >= 1, "LDS hash slots per thread");
+    // The thread's SPT slots go to the global table in three batched stages, so their round trips
+    // overlap instead of running one slot after another: (1) first-probe loads of all keys, issued
+    // before the block scan so that their round trip overlaps it, (2) resolve (a hit needs nothing
+    // more; an empty or taken first slot takes the probing path), (3) the cell atomics of all
+    // found bricks, in flight while the run-start bitmap is built.
+    // (only the loads are kept across the scan; keys, hashes and scans are re-derived after it)
+    uint64_t key[SPT], k0[SPT];
+    uint32_t ts[SPT];
+    auto slot_key = [&](int j) {
+        const uint64_t lk = s_key[threadIdx.x * SPT + j];
+        const bool g1 = split && lk != EMPTY_KEY && (lk & KEY_G1);
+        key[j] = g1 ? lk & ~KEY_G1 : lk;
+        ts[j] = g1 ? tb[G - 1] : tb[0];
+    };
+#pragma unroll
+    for (int j = 0; j < SPT; j++) {
+        slot_key(j);
+        k0[j] = key[j] != EMPTY_KEY ? T.keys[mix64(key[j]) & T.mask] : EMPTY_KEY;
+    }
+    // one dense run list per (block, half): k_place workgroup 2 b + half
+    uint32_t ns[NSUB], cc[G];
+#pragma unroll
+    for (int s = 0; s < NSUB; s++) ns[s] = 0u;
+#pragma unroll
+    for (int g = 0; g < G; g++) cc[g] = 0u;
 #pragma unroll
     for (int j = 0; j < SPT; j++) {
         const int slot = threadIdx.x * SPT + j;
-        const uint32_t c = s_key[slot] != S_EMPTY ? s_cnt[slot] : 0u;
-        n0s += c & 0xFFFFu;
-        n1s += c >> 16;
-        c01 += ((c & 0xFFFFu) ? 1u : 0u) | ((c >> 16) ? 1u << 16 : 0u);
+        const CntT c = s_key[slot] != EMPTY_KEY ? s_cnt[slot] : (CntT)0;
+#pragma unroll
+        for (int s = 0; s < NSUB; s++) {
+            const uint32_t n = (uint32_t)(c >> (16 * s)) & 0xFFFFu;
+            ns[s] += n;
+            cc[s >> 1] += (n ? 1u : 0u) << (16 * (s & 1));
+        }
     }
-    uint32_t off0, off1, idx0, idx1;
+    uint32_t off[NSUB], idx[NSUB];
     {
         const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-        const uint32_t i0 = wave_incl_scan(n0s), i1 = wave_incl_scan(n1s), ic = wave_incl_scan(c01);
+        uint32_t in[NSUB], ic[G];
+#pragma unroll
+        for (int s = 0; s < NSUB; s++) in[s] = wave_incl_scan(ns[s]);
+#pragma unroll
+        for (int g = 0; g < G; g++) ic[g] = wave_incl_scan(cc[g]);
         if (lane == 63) {
-            s_wsum[wid] = (unsigned long long)i0 | ((unsigned long long)i1 << 32);
-            s_wcnt[wid] = ic;
+#pragma unroll
+            for (int g = 0; g < G; g++) {
+                s_wsum[g][wid] = (unsigned long long)in[2 * g] | ((unsigned long long)in[2 * g + 1] << 32);
+                s_wcnt[g][wid] = ic[g];
+            }
         }
         __syncthreads();
-        unsigned long long ex = 0;
-        uint32_t exc = 0, totc = 0;
-        for (int w = 0; w < NT / 64; w++) {
-            ex += w < wid ? s_wsum[w] : 0ull;
-            exc += w < wid ? s_wcnt[w] : 0u;
-            totc += s_wcnt[w];
-        }
-        off0 = (uint32_t)ex + (i0 - n0s);
-        off1 = (uint32_t)(ex >> 32) + (i1 - n1s);
-        idx0 = (exc & 0xFFFFu) + ((ic - c01) & 0xFFFFu);
-        idx1 = (exc >> 16) + ((ic - c01) >> 16);
-        if (threadIdx.x == NT - 1) {
-            Wk.blk_n[2 * bx] = totc & 0xFFFFu;
-            Wk.blk_n[2 * bx + 1] = totc >> 16;
-            // each half's staged sample count: its samples, up to the staging capacity
-            unsigned long long tot = 0;
-            for (int w = 0; w < NT / 64; w++) tot += s_wsum[w];
-            Wk.plan[(size_t)(2 * bx) * PLAN_STRIDE + PLAN_STRIDE - 1] =
-                min((uint32_t)tot, (uint32_t)PLC_STAGE);
-            Wk.plan[(size_t)(2 * bx + 1) * PLAN_STRIDE + PLAN_STRIDE - 1] =
-                min((uint32_t)(tot >> 32), (uint32_t)PLC_STAGE);
-        }
-    }
-    // The thread's SPT slots go to the global table in three batched stages, so their round trips
-    // overlap instead of running one slot after another: (1) first-probe loads of all keys,
-    // (2) resolve (a hit needs nothing more; an empty or taken first slot takes the probing path),
-    // (3) the cell atomics of all found bricks.
-    CPH(4);  // block scan
-    uint64_t key[SPT], h0[SPT], k0[SPT];
 #pragma unroll
-    for (int j = 0; j < SPT; j++) {
-        const int slot = threadIdx.x * SPT + j;
-#ifdef TSDF_CNT_KEY32
-        key[j] = s_key[slot] != EMPTY32 ? key64_of(s_key[slot], kb) : EMPTY_KEY;
-#else
-        key[j] = s_key[slot];
-#endif
-        h0[j] = mix64(key[j]) & T.mask;
-        k0[j] = key[j] != EMPTY_KEY ? T.keys[h0[j]] : EMPTY_KEY;
+        for (int g = 0; g < G; g++) {
+            unsigned long long ex = 0, tot = 0;
+            uint32_t exc = 0, totc = 0;
+            for (int w = 0; w < NT / 64; w++) {
+                ex += w < wid ? s_wsum[g][w] : 0ull;
+                exc += w < wid ? s_wcnt[g][w] : 0u;
+                tot += s_wsum[g][w];
+                totc += s_wcnt[g][w];
+            }
+            off[2 * g] = (uint32_t)ex + (in[2 * g] - ns[2 * g]);
+            off[2 * g + 1] = (uint32_t)(ex >> 32) + (in[2 * g + 1] - ns[2 * g + 1]);
+            idx[2 * g] = (exc & 0xFFFFu) + ((ic[g] - cc[g]) & 0xFFFFu);
+            idx[2 * g + 1] = (exc >> 16) + ((ic[g] - cc[g]) >> 16);
+            if (threadIdx.x == NT - 1) {
+                const uint32_t b = G * bx + g;
+                Wk.blk_n[2 * b] = totc & 0xFFFFu;
+                Wk.blk_n[2 * b + 1] = totc >> 16;
+                // each half's staged sample count: its samples, up to the staging capacity
+                Wk.plan[(size_t)(2 * b) * PLAN_STRIDE + PLAN_STRIDE - 1] =
+                    min((uint32_t)tot, (uint32_t)PLC_STAGE);
+                Wk.plan[(size_t)(2 * b + 1) * PLAN_STRIDE + PLAN_STRIDE - 1] =
+                    min((uint32_t)(tot >> 32), (uint32_t)PLC_STAGE);
+            }
+        }
     }
+    CPH(4);  // block scan
     int64_t hx[SPT];
 #pragma unroll
     for (int j = 0; j < SPT; j++) {
+        slot_key(j);
         hx[j] = -1;
         if (key[j] != EMPTY_KEY)
-            hx[j] = k0[j] == key[j] ? (int64_t)h0[j] : table_insert(T, key[j], &C->ovf);
+            hx[j] = k0[j] == key[j] ? (int64_t)(mix64(key[j]) & T.mask) : table_insert(T, key[j], &C->ovf);
     }
     CPH(5);  // first probes + inserts
     uint32_t old[SPT];
 #pragma unroll
     for (int j = 0; j < SPT; j++) {
         const int slot = threadIdx.x * SPT + j;
-        const uint32_t c = s_cnt[slot];
-        old[j] = hx[j] >= 0
-                     ? atomicAdd(&T.cell[(size_t)hx[j] * T.cell_stride + t], (c & 0xFFFFu) + (c >> 16))
-                     : 0u;
+        const CntT c = s_cnt[slot];
+        uint32_t tot = 0;
+#pragma unroll
+        for (int s = 0; s < NSUB; s++) tot += (uint32_t)(c >> (16 * s)) & 0xFFFFu;
+        old[j] = hx[j] >= 0 ? atomicAdd(&T.cell[(size_t)hx[j] * T.cell_stride + ts[j]], tot) : 0u;
     }
     // dense run lists: (table index | NO_PAIR, rank in the (brick, scan) cell, run offset in the
-    // half's sample order, run samples | slot << 16); the half-1 sub-run follows half 0's
+    // sub-run's sample order, run samples | slot << 16); in the cell the sub-runs follow each
+    // other in (block, half) order
     static_assert((RPB / 2) * MAX_IN_BRICK < (1 << 16) && HCAP <= (1 << 16), "run record packing");
+    // the run-start bits need only the offsets: set them while the atomics are in flight
+    uint32_t boff[NSUB];
+#pragma unroll
+    for (int s = 0; s < NSUB; s++) boff[s] = off[s];
 #pragma unroll
     for (int j = 0; j < SPT; j++) {
         const int slot = threadIdx.x * SPT + j;
         if (key[j] == EMPTY_KEY) continue;
-        const uint32_t c = s_cnt[slot], n0 = c & 0xFFFFu, n1 = c >> 16;
+        const CntT c = s_cnt[slot];
+#pragma unroll
+        for (int s = 0; s < NSUB; s++) {
+            const uint32_t n = (uint32_t)(c >> (16 * s)) & 0xFFFFu;
+            if (n) {
+                if (boff[s] < (uint32_t)PLC_STAGE) atomicOr(&s_bm[s][boff[s] >> 5], 1u << (boff[s] & 31));
+                boff[s] += n;
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < SPT; j++) {
+        const int slot = threadIdx.x * SPT + j;
+        if (key[j] == EMPTY_KEY) continue;
+        const CntT c = s_cnt[slot];
         uint32_t tx = NO_PAIR, rk = 0u;
         if (hx[j] >= 0) {
             tx = (uint32_t)hx[j];
@@ -523,29 +461,30 @@ __global__ __launch_bounds__(NT, SEM == 2 && NT == CNT_THREADS ? TSDF_F64_COUNT_
             // per (workgroup, brick): partial-line stores from every XCD cost HBM writes)
             if (old[j] == 0u) T.touched[tx] = 1u;
         }
-        if (n0) {
-            bt0[idx0++] = make_uint4(tx, rk, off0, n0 | ((uint32_t)slot << 16));
-            if (off0 < (uint32_t)PLC_STAGE) atomicOr(&s_bm[0][off0 >> 5], 1u << (off0 & 31));
-            off0 += n0;
-        }
-        if (n1) {
-            bt1[idx1++] = make_uint4(tx, rk + n0, off1, n1 | ((uint32_t)slot << 16));
-            if (off1 < (uint32_t)PLC_STAGE) atomicOr(&s_bm[1][off1 >> 5], 1u << (off1 & 31));
-            off1 += n1;
+#pragma unroll
+        for (int s = 0; s < NSUB; s++) {
+            const uint32_t n = (uint32_t)(c >> (16 * s)) & 0xFFFFu;
+            if (n) {
+                uint4* bt = Wk.blk + (size_t)(2 * (G * bx + (s >> 1)) + (s & 1)) * HCAP;
+                bt[idx[s]++] = make_uint4(tx, rk, off[s], n | ((uint32_t)slot << 16));
+                off[s] += n;
+                rk += n;
+            }
         }
     }
     CPH(6);  // cell atomics + run lists
-    // k_place's staging plan for each half: the run-start bitmap and its exclusive popcount
-    // prefix per word (wave h writes half h's)
+    // k_place's staging plan for each (block, half): the run-start bitmap and its exclusive
+    // popcount prefix per word (wave s writes sub-run list s's)
     __syncthreads();
     CPH(7);
     {
         const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
-        if (wv < 2) {
+        static_assert(NT / 64 >= NSUB, "one wave per sub-run list");
+        if (wv < NSUB) {
             // WPL consecutive bitmap words per lane; the prefix is one u16 per word
             constexpr int WPL = (PLC_WORDS + 63) / 64;
             static_assert(WPL >= 1 && WPL <= 4, "bitmap words per lane");
-            uint32_t* pl = Wk.plan + (size_t)(2 * bx + wv) * PLAN_STRIDE;
+            uint32_t* pl = Wk.plan + (size_t)(2 * (G * bx + (wv >> 1)) + (wv & 1)) * PLAN_STRIDE;
             uint16_t* pp = reinterpret_cast<uint16_t*>(pl + PLC_WORDS);
             uint32_t b[WPL], cs = 0;
 #pragma unroll
@@ -581,7 +520,7 @@ __global__ __launch_bounds__(NT, SEM == 2 && NT == CNT_THREADS ? TSDF_F64_COUNT_
     }
 #ifdef TSDF_CNT_PHASE
     CPH(8);  // plan + stats
-    if (threadIdx.x == 0 && blockIdx.x % 61 == 0 && NT == CNT_THREADS)
+    if (threadIdx.x == 0 && blockIdx.x % 61 == 0 && NT == CNT_THREADS * G)
         printf("cntphase %u init %llu walk %llu emit %llu bar %llu scan %llu probe %llu atom %llu "
                "bar2 %llu tail %llu\n", blockIdx.x, cph[0], cph[1], cph[2], cph[3], cph[4], cph[5],
                cph[6], cph[7], cph[8]);
@@ -1395,11 +1334,15 @@ static int grid_for(uint64_t items, int per_block, int cap) {
 // (tsdf_capi.cpp) interleaves the cross-batch waits between them.
 hipError_t launch_count(const float* d_xyz, const BatchRef& D, const RayConst& R, const Table& T,
                         const Work& Wk, Globals* G, int parity, hipStream_t st, const KTime& kt,
-                        bool wide) {
+                        bool wide, bool paired) {
     // sem 3 (Voxblox 1/z^2) counts with Walk<1>: the weight only matters where it is stored
     if (wide) {  // a batch too small to fill the chip: 1024-lane workgroups
         auto k = R.sem == 1 || R.sem == 3 ? k_count<1, 1024> : R.sem == 2 ? k_count<2, 1024> : k_count<0, 1024>;
         tlaunch(k, D.n_blocks, 1024, st, kt.start, kt.stop, d_xyz, D, R, T, Wk, G, parity);
+    } else if (paired) {  // two blocks per 512-lane workgroup (no sector sharding)
+        constexpr int NT2 = 2 * CNT_THREADS;
+        auto k = R.sem == 1 || R.sem == 3 ? k_count<1, NT2, 2> : R.sem == 2 ? k_count<2, NT2, 2> : k_count<0, NT2, 2>;
+        tlaunch(k, (D.n_blocks + 1) / 2, NT2, st, kt.start, kt.stop, d_xyz, D, R, T, Wk, G, parity);
     } else {
         auto k = R.sem == 1 || R.sem == 3 ? k_count<1> : R.sem == 2 ? k_count<2> : k_count<0>;
         tlaunch(k, D.n_blocks, CNT_THREADS, st, kt.start, kt.stop, d_xyz, D, R, T, Wk, G, parity);
