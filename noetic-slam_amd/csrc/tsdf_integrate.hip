@@ -82,8 +82,11 @@ constexpr uint32_t NO_SPAN = 0xFFFFFFFFu;
 // FUSED (single walk, tsdf_walk.hip): a brick's samples are read through its span records (active
 // record = (table index, slot, first span, spans); 64-bit cells = relative sample prefix | absolute
 // span position, the totals at scan n_scans).  Otherwise they are one contiguous segment (k_place).
+#ifndef TSDF_INT_WAVES
+#define TSDF_INT_WAVES 1
+#endif
 template <int SEM, int MAXS, bool FUSED>
-__global__ __launch_bounds__(INT_THREADS) void k_integrate(BatchRef D, Table T, Work Wk, Pool Pl,
+__global__ __launch_bounds__(INT_THREADS, TSDF_INT_WAVES) void k_integrate(BatchRef D, Table T, Work Wk, Pool Pl,
                                                           Globals* G, int parity, RayConst R) {
     constexpr int NSLOT = FUSED ? INT_SPT * SPAN : INT_PER;  // register-cached samples per thread
     constexpr bool VB = SEM == 1 || SEM == 3;  // Voxblox fuse (3: per-sample weights in Work::smw)

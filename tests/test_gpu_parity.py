@@ -158,6 +158,19 @@ def test_small_batch_kernel_bitwise(sim, monkeypatch, semantics):
                     assert np.array_equal(x, y), (mb, extra)
 
 
+def test_paired_count_workgroups_bitwise(sim, monkeypatch):
+    """TSDF_COUNT_PAIRED=1: k_count takes two 1024-ray blocks per 512-lane workgroup (one LDS brick
+    hash, per-(block, half) sub-runs).  Scans decimated by 3 have an odd block count (43), so
+    workgroups also straddle two scans (the block bit in the LDS key); with and without carving
+    (long rays: the per-pair emission path).  Equal to the oracle bit for bit."""
+    monkeypatch.setenv("TSDF_COUNT_PAIRED", "1")
+    monkeypatch.setenv("TSDF_COUNT_WIDE", "0")
+    scans = [(decimate(p, 3), org) for p, org in (sim.scan(k) for k in range(5))]
+    for extra in ({}, dict(space_carving=True, max_range=20.0)):
+        g, o = run_both(scans, max_batch=5, **extra)
+        assert assert_bitwise(g, o) > 10000, extra
+
+
 def test_pipelined_and_64_scan_batches_bitwise(sim):
     """Overlapped batches (tsdf_params.pipeline: batch b+1's count/compact/place beside batch b's
     integrate, two streams) and 64-scan batches give the oracle's bits, through the host queue and
