@@ -424,7 +424,12 @@ __global__ __launch_bounds__(NT, SEM == 2 && (NT == CNT_THREADS || G == 2) ? TSD
         uint32_t tot = 0;
 #pragma unroll
         for (int s = 0; s < NSUB; s++) tot += (uint32_t)(c >> (16 * s)) & 0xFFFFu;
+#ifndef TSDF_ABLATE_CNT_NORET
         old[j] = hx[j] >= 0 ? atomicAdd(&T.cell[(size_t)hx[j] * T.cell_stride + ts[j]], tot) : 0u;
+#else  // diagnostic: the cell atomics not waited for (every run ranked 0: wrong, in-bounds)
+        if (hx[j] >= 0) atomicAdd(&T.cell[(size_t)hx[j] * T.cell_stride + ts[j]], tot);
+        old[j] = 0u;
+#endif
     }
     // dense run lists: (table index | NO_PAIR, rank in the (brick, scan) cell, run offset in the
     // sub-run's sample order, run samples | slot << 16); in the cell the sub-runs follow each
