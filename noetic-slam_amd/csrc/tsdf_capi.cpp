@@ -1110,7 +1110,8 @@ void tsdf_destroy(tsdf_ctx* c) {
                    c->W2[1].blk_n, c->W2[1].fb,        c->W2[1].smp,     c->W2[1].active,
                    c->W2[0].cagg,    c->W2[1].cagg,      c->W2[0].act,     c->W2[1].act,
                    c->W2[0].spn,     c->W2[1].spn,       c->W2[0].smw,     c->W2[1].smw,
-                   c->W2[0].plan,    c->W2[1].plan};
+                   c->W2[0].plan,    c->W2[1].plan,      c->W2[0].rsv,     c->W2[1].rsv,
+                   c->W2[0].rsv_n,   c->W2[1].rsv_n};
     for (void* d : dev)
         if (d) (void)hipFree(d);
     for (int i = 0; i < 2; i++) {
@@ -1262,6 +1263,10 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
         HIPCHK(c, hipMalloc(&W.blk, (size_t)c->max_blocks * 2 * HCAP * sizeof(uint4)));
         HIPCHK(c, hipMalloc(&W.blk_n, (size_t)c->max_blocks * 2 * sizeof(uint32_t)));
         HIPCHK(c, hipMalloc(&W.plan, (size_t)c->max_blocks * 2 * PLAN_STRIDE * sizeof(uint32_t)));
+#ifdef TSDF_CNT_SPLIT
+        HIPCHK(c, hipMalloc(&W.rsv, (size_t)c->max_blocks * HCAP * sizeof(uint4)));
+        HIPCHK(c, hipMalloc(&W.rsv_n, (size_t)c->max_blocks * sizeof(uint32_t)));
+#endif
         HIPCHK(c, hipMalloc(&W.fb, (size_t)W.max_fb * sizeof(uint4)));
         HIPCHK(c, hipMalloc(&W.smp, (size_t)W.max_smp * sizeof(uint2)));
         if (c->R.sem == 3) HIPCHK(c, hipMalloc(&W.smw, (size_t)W.max_smp * sizeof(float)));

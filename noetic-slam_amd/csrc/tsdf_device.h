@@ -199,6 +199,8 @@ struct Work {
     uint32_t* ord_hist; // per (slice, size class): counts [64][32], then first positions [64][32]
     uint4* cagg;    // k_compact: per table chunk (touched bricks, samples, new bricks), then bases
     uint32_t* act;  // sector sharding: the k_count blocks holding a ray of this GPU's sector (n_act)
+    uint4* rsv;     // TSDF_CNT_SPLIT variant: per k_count block, its distinct bricks for k_resolve
+    uint32_t* rsv_n;  // (key, n0 | n1 << 16, run-list index 0 | index 1 << 11 | scan << 22); count
     uint32_t* spn;  // single walk: span records (sample position | (samples - 1) << 30), per brick
                     // contiguous and scan-ordered (k_spans)
     uint32_t maxp;        // pair slots per ray

@@ -137,6 +137,13 @@ __global__ __launch_bounds__(NT, SEM == 2 && (NT == CNT_THREADS || G == 2) ? TSD
     static_assert(G == 1 || G == 2, "one or two blocks per workgroup");
     static_assert(G == 1 || RPB % NT == 0, "a pass over the rays stays inside one block");
     using CntT = typename std::conditional<G == 2, unsigned long long, uint32_t>::type;
+#ifdef TSDF_CNT_SPLIT
+    // variant build: the global phase (find-or-insert, cell atomic) runs in k_resolve
+    constexpr bool SPLIT = G == 1;
+#else
+    constexpr bool SPLIT = false;
+#endif
+    __shared__ uint32_t s_wsl[SPLIT ? NT / 64 : 1];
     constexpr int NSUB = 2 * G;  // (block, half) sub-runs
     constexpr uint64_t KEY_G1 = 1ull << 63;  // LDS key bit: block 1 of a workgroup spanning two scans
     __shared__ unsigned long long s_key[HCAP];
@@ -342,10 +349,12 @@ __global__ __launch_bounds__(NT, SEM == 2 && (NT == CNT_THREADS || G == 2) ? TSD
         key[j] = g1 ? lk & ~KEY_G1 : lk;
         ts[j] = g1 ? tb[G - 1] : tb[0];
     };
+    if constexpr (!SPLIT) {
 #pragma unroll
-    for (int j = 0; j < SPT; j++) {
-        slot_key(j);
-        k0[j] = key[j] != EMPTY_KEY ? T.keys[mix64(key[j]) & T.mask] : EMPTY_KEY;
+        for (int j = 0; j < SPT; j++) {
+            slot_key(j);
+            k0[j] = key[j] != EMPTY_KEY ? T.keys[mix64(key[j]) & T.mask] : EMPTY_KEY;
+        }
     }
     // one dense run list per (block, half): k_place workgroup 2 b + half
     uint32_t ns[NSUB], cc[G];
@@ -364,9 +373,16 @@ __global__ __launch_bounds__(NT, SEM == 2 && (NT == CNT_THREADS || G == 2) ? TSD
             cc[s >> 1] += (n ? 1u : 0u) << (16 * (s & 1));
         }
     }
+    uint32_t nsl = 0, rbase = 0;  // SPLIT: the thread's distinct bricks, their first record
+    if constexpr (SPLIT) {
+#pragma unroll
+        for (int j = 0; j < SPT; j++) nsl += s_key[threadIdx.x * SPT + j] != EMPTY_KEY ? 1u : 0u;
+    }
     uint32_t off[NSUB], idx[NSUB];
     {
         const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+        const uint32_t isl = SPLIT ? wave_incl_scan(nsl) : 0u;
+        if (SPLIT && lane == 63) s_wsl[wid] = isl;
         uint32_t in[NSUB], ic[G];
 #pragma unroll
         for (int s = 0; s < NSUB; s++) in[s] = wave_incl_scan(ns[s]);
@@ -380,6 +396,15 @@ __global__ __launch_bounds__(NT, SEM == 2 && (NT == CNT_THREADS || G == 2) ? TSD
             }
         }
         __syncthreads();
+        if constexpr (SPLIT) {
+            uint32_t ex = 0, tot = 0;
+            for (int w = 0; w < NT / 64; w++) {
+                ex += w < wid ? s_wsl[w] : 0u;
+                tot += s_wsl[w];
+            }
+            rbase = ex + isl - nsl;
+            if (threadIdx.x == NT - 1) Wk.rsv_n[bx] = tot;
+        }
 #pragma unroll
         for (int g = 0; g < G; g++) {
             unsigned long long ex = 0, tot = 0;
@@ -407,6 +432,36 @@ __global__ __launch_bounds__(NT, SEM == 2 && (NT == CNT_THREADS || G == 2) ? TSD
         }
     }
     CPH(4);  // block scan
+    if constexpr (SPLIT) {
+        // one record per distinct brick for k_resolve, which fills the runs' (table index, cell
+        // rank); this kernel writes the runs' (offset, samples | slot) and the run-start bits
+        static_assert(G == 1 && HCAP <= 2048 && MAX_BATCH <= 1024, "record packing");
+        uint32_t r = rbase;
+#pragma unroll
+        for (int j = 0; j < SPT; j++) {
+            const int slot = threadIdx.x * SPT + j;
+            slot_key(j);
+            if (key[j] == EMPTY_KEY) continue;
+            const uint32_t c = (uint32_t)s_cnt[slot], n0 = c & 0xFFFFu, n1 = c >> 16;
+            uint32_t w = ts[j] << 22;
+            uint4* bt = Wk.blk + (size_t)(2 * bx) * HCAP;
+            if (n0) {
+                reinterpret_cast<uint2*>(bt + idx[0])[1] = make_uint2(off[0], n0 | ((uint32_t)slot << 16));
+                if (off[0] < (uint32_t)PLC_STAGE) atomicOr(&s_bm[0][off[0] >> 5], 1u << (off[0] & 31));
+                w |= idx[0]++;
+                off[0] += n0;
+            }
+            if (n1) {
+                reinterpret_cast<uint2*>(bt + HCAP + idx[NSUB - 1])[1] =
+                    make_uint2(off[NSUB - 1], n1 | ((uint32_t)slot << 16));
+                if (off[NSUB - 1] < (uint32_t)PLC_STAGE)
+                    atomicOr(&s_bm[NSUB - 1][off[NSUB - 1] >> 5], 1u << (off[NSUB - 1] & 31));
+                w |= idx[NSUB - 1]++ << 11;
+                off[NSUB - 1] += n1;
+            }
+            Wk.rsv[(size_t)bx * HCAP + r++] = make_uint4((uint32_t)key[j], (uint32_t)(key[j] >> 32), c, w);
+        }
+    } else {
     int64_t hx[SPT];
 #pragma unroll
     for (int j = 0; j < SPT; j++) {
@@ -477,6 +532,7 @@ __global__ __launch_bounds__(NT, SEM == 2 && (NT == CNT_THREADS || G == 2) ? TSD
             }
         }
     }
+    }  // !SPLIT
     CPH(6);  // cell atomics + run lists
     // k_place's staging plan for each (block, half): the run-start bitmap and its exclusive
     // popcount prefix per word (wave s writes sub-run list s's)
@@ -531,6 +587,43 @@ __global__ __launch_bounds__(NT, SEM == 2 && (NT == CNT_THREADS || G == 2) ? TSD
                cph[6], cph[7], cph[8]);
 #endif
 }
+
+#ifdef TSDF_CNT_SPLIT
+// k_resolve (TSDF_CNT_SPLIT variant): k_count's global phase as its own launch, so the LDS-bound
+// k_count workgroups do not hold their LDS through the find-or-insert and cell-atomic round trips.
+// One workgroup per k_count block, one lane per distinct brick of the block's LDS hash: find or
+// insert the brick, reserve its samples in the (brick, scan) cell, and write the (table index,
+// cell rank) half of the block's run records.
+constexpr int RSV_THREADS = 256;
+__global__ __launch_bounds__(RSV_THREADS) void k_resolve(BatchRef D, RayConst R, Table T, Work Wk,
+                                                        Globals* G, int parity) {
+    Counters* C = &G->ctr[parity];
+    uint32_t b = blockIdx.x;
+    if (R.sec_on) {
+        if (blockIdx.x >= C->n_act) return;
+        b = Wk.act[blockIdx.x];
+    }
+    if (b >= D.n_blocks) return;
+    const uint32_t n = Wk.rsv_n[b];
+    const uint4* rec = Wk.rsv + (size_t)b * HCAP;
+    uint4* bt = Wk.blk + (size_t)(2 * b) * HCAP;
+    for (uint32_t i = threadIdx.x; i < n; i += RSV_THREADS) {
+        const uint4 q = rec[i];
+        const uint64_t key = (uint64_t)q.x | ((uint64_t)q.y << 32);
+        const uint32_t n0 = q.z & 0xFFFFu, n1 = q.z >> 16, t = q.w >> 22;
+        const uint64_t h0 = mix64(key) & T.mask;
+        const int64_t hx = T.keys[h0] == key ? (int64_t)h0 : table_insert(T, key, &C->ovf);
+        uint32_t tx = NO_PAIR, rk = 0u;
+        if (hx >= 0) {
+            tx = (uint32_t)hx;
+            rk = atomicAdd(&T.cell[(size_t)hx * T.cell_stride + t], n0 + n1);
+            if (rk == 0u) T.touched[tx] = 1u;
+        }
+        if (n0) reinterpret_cast<uint2*>(bt + (q.w & 2047u))[0] = make_uint2(tx, rk);
+        if (n1) reinterpret_cast<uint2*>(bt + HCAP + ((q.w >> 11) & 2047u))[0] = make_uint2(tx, rk + n0);
+    }
+}
+#endif
 
 // ------------------------------------------------------------------------------------------------
 // k_sector_flags (sector sharding only): one wave per k_count block of RPB rays, 16 points per lane,
@@ -1343,15 +1436,26 @@ hipError_t launch_count(const float* d_xyz, const BatchRef& D, const RayConst& R
     // sem 3 (Voxblox 1/z^2) counts with Walk<1>: the weight only matters where it is stored
     if (wide) {  // a batch too small to fill the chip: 1024-lane workgroups
         auto k = R.sem == 1 || R.sem == 3 ? k_count<1, 1024> : R.sem == 2 ? k_count<2, 1024> : k_count<0, 1024>;
+#ifndef TSDF_CNT_SPLIT
         tlaunch(k, D.n_blocks, 1024, st, kt.start, kt.stop, d_xyz, D, R, T, Wk, G, parity);
+#else
+        tlaunch(k, D.n_blocks, 1024, st, kt.start, nullptr, d_xyz, D, R, T, Wk, G, parity);
+#endif
     } else if (paired) {  // two blocks per 512-lane workgroup (no sector sharding)
         constexpr int NT2 = 2 * CNT_THREADS;
         auto k = R.sem == 1 || R.sem == 3 ? k_count<1, NT2, 2> : R.sem == 2 ? k_count<2, NT2, 2> : k_count<0, NT2, 2>;
         tlaunch(k, (D.n_blocks + 1) / 2, NT2, st, kt.start, kt.stop, d_xyz, D, R, T, Wk, G, parity);
     } else {
         auto k = R.sem == 1 || R.sem == 3 ? k_count<1> : R.sem == 2 ? k_count<2> : k_count<0>;
+#ifndef TSDF_CNT_SPLIT
         tlaunch(k, D.n_blocks, CNT_THREADS, st, kt.start, kt.stop, d_xyz, D, R, T, Wk, G, parity);
+#else
+        tlaunch(k, D.n_blocks, CNT_THREADS, st, kt.start, nullptr, d_xyz, D, R, T, Wk, G, parity);
+#endif
     }
+#ifdef TSDF_CNT_SPLIT
+    if (!paired) tlaunch(k_resolve, D.n_blocks, RSV_THREADS, st, nullptr, kt.stop, D, R, T, Wk, G, parity);
+#endif
     return hipGetLastError();
 }
 
