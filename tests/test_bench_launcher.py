@@ -63,3 +63,27 @@ def test_bench_gpus2_without_launcher_sets_world(tmp_path):
                        timeout=300)
     assert r.returncode != 0
     assert '"n_gpus"' not in r.stdout
+
+
+def test_traffic_file_is_used_only_for_its_own_build(tmp_path, monkeypatch):
+    """roofline.traffic comes from a PMC run only when that run measured THIS library build
+    (VERDICT r3 weak #8): the committed profiles/traffic_r04.json carries the sha of the shipped
+    libtsdf_hip.so, and a file of another build (or an unreadable one) yields None, with the reason
+    in traffic_source."""
+    import json
+    lib = tmp_path / "libfake.so"
+    lib.write_bytes(b"kernels v1")
+    monkeypatch.setenv("TSDF_HIP_LIB", str(lib))
+    sha = bench.lib_sha16()
+    good = tmp_path / "t.json"
+    good.write_text(json.dumps({"lib_sha16": sha, "bytes_per_launch": {"k_count": 123}}))
+    val, src = bench.read_traffic(str(good), "count")
+    assert val == 123 and src["matches_build"] and src["this_build_sha16"] == sha
+    lib.write_bytes(b"kernels v2")  # the kernels changed after the PMC run
+    val, src = bench.read_traffic(str(good), "count")
+    assert val is None and not src["matches_build"]
+    bad = tmp_path / "bad.json"
+    bad.write_text("{not json")
+    val, src = bench.read_traffic(str(bad), "count")
+    assert val is None and src["error"] == "unreadable"
+
