@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define TSDF_ABI_VERSION 8
+#define TSDF_ABI_VERSION 9
 #define TSDF_MAX_BATCH 512 /* scans per GPU batch (see tsdf_params.max_batch) */
 #define TSDF_BRICK_SIDE 8 /* voxels per brick edge: a brick is 8^3 = 512 voxels */
 
@@ -213,6 +213,14 @@ const char* tsdf_last_error(const tsdf_ctx* ctx);
 int tsdf_integrate(tsdf_ctx* ctx, const void* pts, uint64_t n, uint32_t point_step,
                    uint32_t xyz_offset, int32_t xyz_is_f64, const double origin[3]);
 
+/* ABI v9: tsdf_integrate_sectors with a bare origin instead of a pose: like tsdf_integrate, the
+ * scan carries no orientation, so Voxblox takes the constant weight (a bare origin on the
+ * sectors path was given an identity orientation, i.e. world-z 1/z^2 weights, so the sharded field
+ * differed from the unsharded tsdf_integrate one). */
+int tsdf_integrate_sectors_origin(tsdf_ctx* const* ctxs, uint32_t n_ctx, const void* pts,
+                                  uint64_t n, uint32_t point_step, uint32_t xyz_offset,
+                                  int32_t xyz_is_f64, const double origin[3]);
+
 /* ABI v6: tsdf_integrate with the sensor's full pose: pose = (x, y, z, qx, qy, qz, qw), the
  * position (the ray origin) and orientation of the sensor in the world frame, in
  * geometry_msgs/Pose order (DLIO's /robot/dlio/odom_node/pose, odom.cc:315-356).  The orientation
@@ -386,10 +394,16 @@ int tsdf_select_sector(const float* xyz, uint64_t n, const double origin[3], dou
  * caller's collective (RCCL all-to-all over xGMI; the library does no communication):
  *   1. tsdf_brick_keys_device: this rank's brick keys -> all-gathered by the caller;
  *   2. tsdf_border_pack_device: this rank's bricks owned by a lower rank are packed as tiles
- *      (grouped by owner) and reset to the background (their mass now travels to the owner);
+ *      (grouped by owner); ABI v9: they keep their mass until step 4;
  *   3. all_to_all of the tiles (caller), then tsdf_border_merge_device on every rank merges the
  *      received tiles into its bricks, sources in ascending rank order, by the rule of
- *      tsdf_import_bricks (weighted mean; copy where W == 0).
+ *      tsdf_import_bricks (weighted mean; copy where W == 0), after a snapshot of those bricks;
+ *   4. (ABI v9) tsdf_border_commit_device on every rank, with commit = 1 only when the collective
+ *      and EVERY rank's merge succeeded (the caller agrees on it, e.g. an all-reduce of the ranks'
+ *      status): the sent bricks are reset to the background.  commit = 0 aborts: the merged bricks
+ *      are restored from their snapshots and the sent bricks keep their mass, so every field is the
+ *      one before the reduce, bit for bit -- a failed reduce neither loses nor double-counts mass.
+ *      Between steps 2 and 4 (the reduce is open) the context refuses integrate and import calls.
  * Afterwards every brick's full mass sits on its owner (the others hold it at W = 0), so
  * integration may continue and the reduce may be repeated.  All buffers are DEVICE memory of the
  * context's GPU and must be ready when the call is made; the calls return after their own GPU work
@@ -413,6 +427,11 @@ int tsdf_border_pack_device(tsdf_ctx* ctx, const uint64_t* d_all_keys, const uin
 int tsdf_border_merge_device(tsdf_ctx* ctx, const uint32_t* d_recv, const uint64_t* recv_counts,
                              uint32_t world);
 
+/* ABI v9: close the context's open border reduce: commit = 1 resets the bricks its pack sent;
+ * commit = 0 restores the bricks its merges touched and keeps the sent ones.  No open reduce: a
+ * no-op.  On a HIP error the reduce stays open (retry the call). */
+int tsdf_border_commit_device(tsdf_ctx* ctx, int32_t commit);
+
 /* ---- ABI v7: several GPUs in ONE process (SURVEY §8b's num_gpus / device_ids) ----------------
  * tsdf_create_sharded: n contexts, context k on device_ids[k] (NULL: device k) as azimuth sector k
  * of n (p's n_sectors / sector / device_id are overridden), into out[0..n).  ABI v8: peer access
@@ -426,7 +445,32 @@ int tsdf_border_merge_device(tsdf_ctx* ctx, const uint32_t* d_recv, const uint64
  * different processes use the three device entry points with a collective instead. */
 int tsdf_create_sharded(const tsdf_params* p, uint32_t n, const int32_t* device_ids,
                         tsdf_ctx** out);
+/* ABI v9: transactional (every context packs without resetting, every owner snapshots before it
+ * merges; any failure rolls every context back), so a failed call leaves the fields unchanged. */
 int tsdf_border_reduce_local(tsdf_ctx* const* ctxs, uint32_t n, uint64_t* bricks_moved);
+
+/* ---- ABI v9: marching cubes of a sector-sharded field (C5: 2 cm + mesh on N GPUs) -----------
+ * After a border reduce every brick's mass sits on one context, but a cube on a brick's +x/+y/+z
+ * faces also reads voxels of neighbour bricks, which another context may own.  Each context meshes
+ * ITS bricks (a cube belongs to the brick of its min voxel, so every cube is meshed exactly once)
+ * with a one-brick halo of the neighbours it lacks:
+ *   tsdf_halo_keys_device   the keys of the +x/+y/+z neighbour bricks (7 per brick) of this
+ *                           context's observed bricks that it does not observe itself (device,
+ *                           sorted; TSDF_EOVERFLOW with *n_out = the count when cap is short)
+ *   tsdf_halo_pack_device   on a holder: tiles (TSDF_TILE_WORDS rows: S, W, key) of the requested
+ *                           bricks it observes, in any row order; *n_rows = tiles
+ *   tsdf_extract_mesh_halo  tsdf_extract_mesh_table over this context's bricks, neighbours looked up
+ *                           in the halo tiles first
+ * The union of the contexts' soups is the mesh of the union field (tests/test_multigpu.py).
+ * tsdf_extract_mesh_local runs all of it among the contexts of one process (border reduce, halo
+ * exchange by peer copies, one mesh per context; soups concatenated in context order). */
+int tsdf_halo_keys_device(tsdf_ctx* ctx, uint64_t* d_keys, uint64_t cap, uint64_t* n_out);
+int tsdf_halo_pack_device(tsdf_ctx* ctx, const uint64_t* d_req, uint64_t n_req, uint32_t* d_send,
+                          uint64_t cap_rows, uint64_t* n_rows);
+int tsdf_extract_mesh_halo(tsdf_ctx* ctx, float min_weight, int32_t table, const uint32_t* d_halo,
+                           uint64_t n_halo, float* tri, uint64_t cap, uint64_t* n_tri);
+int tsdf_extract_mesh_local(tsdf_ctx* const* ctxs, uint32_t n, float min_weight, int32_t table,
+                            float* tri, uint64_t cap, uint64_t* n_tri);
 
 #ifdef __cplusplus
 }

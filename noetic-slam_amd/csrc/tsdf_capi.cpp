@@ -295,7 +295,18 @@ struct tsdf_ctx {
     const float* fan_buf = nullptr;
     uint64_t fan_lo = 0, fan_hi = 0;
     std::vector<tsdf_ctx*> fan_followers;
+    // border-reduce transaction (ABI v9): the pool slots the open reduce's pack sent
+    // (reset at commit) and, per merge, the received bricks' pre-merge tiles (written back at
+    // abort).  While a reduce is open the context takes no scan and no import.
+    bool brd_open = false;
+    uint32_t* brd_sent = nullptr;
+    uint64_t brd_n_sent = 0;
+    std::vector<std::pair<uint32_t*, uint64_t>> brd_backup;
 };
+
+// A context with an open border reduce refuses new mass until the reduce is committed or aborted
+// (a commit resets the sent bricks: mass integrated into them meanwhile would be lost).
+static bool border_busy(tsdf_ctx* c);
 
 // Weight cap of the weighted-mean merges (import, border reduce): Voxblox's max_weight, else none
 static float merge_cap(const tsdf_ctx* c) {
@@ -1098,6 +1109,8 @@ void tsdf_destroy(tsdf_ctx* c) {
         }
     }
     if (c->metrics) fclose(c->metrics);
+    if (c->brd_sent) (void)hipFree(c->brd_sent);
+    for (auto& b : c->brd_backup) (void)hipFree(b.first);
     delete c->timer;
     delete c->pack;
     void* dev[] = {c->T.keys,        c->T.slots,
@@ -1472,6 +1485,7 @@ static int pend_room(tsdf_ctx* c, uint64_t n) {
 
 static int integrate_impl(tsdf_ctx* c, const void* pts, uint64_t n, uint32_t point_step,
                           uint32_t xyz_offset, int32_t xyz_is_f64, const ScanPose& P) {
+    if (border_busy(c)) return TSDF_EINVAL;
     const uint32_t need = xyz_is_f64 ? 24u : 12u;
     if (point_step < need || xyz_offset > point_step - need)
         return fail(c, TSDF_EINVAL, "point_step/xyz_offset inconsistent");
@@ -1649,19 +1663,50 @@ extern "C" {
 // point is classified once (the kernels' in_sector rule on each context's bounds) and packed into
 // its context's pinned staging; each context then copies only its sector's points to its GPU, so a
 // scan crosses PCIe once in total, split over the N links.
+static int sectors_impl(tsdf_ctx* const* ctxs, uint32_t n_ctx, const void* pts, uint64_t n,
+                        uint32_t point_step, uint32_t xyz_offset, int32_t xyz_is_f64,
+                        const ScanPose& P);
+
 int tsdf_integrate_sectors(tsdf_ctx* const* ctxs, uint32_t n_ctx, const void* pts, uint64_t n,
                            uint32_t point_step, uint32_t xyz_offset, int32_t xyz_is_f64,
                            const double pose[7]) {
     if (!ctxs || n_ctx == 0 || n_ctx > TSDF_MAX_WORLD) return TSDF_EINVAL;
     for (uint32_t k = 0; k < n_ctx; k++)
         if (!ctxs[k]) return TSDF_EINVAL;
+    if (!pose) return fail(ctxs[0], TSDF_EINVAL, "null argument");
+    const double qn = pose[3] * pose[3] + pose[4] * pose[4] + pose[5] * pose[5] + pose[6] * pose[6];
+    if (!(qn > 0.0) || !std::isfinite(qn)) return fail(ctxs[0], TSDF_EINVAL, "pose quaternion is zero");
+    return sectors_impl(ctxs, n_ctx, pts, n, point_step, xyz_offset, xyz_is_f64, pose_of(pose));
+}
+
+// ABI v9: the sectors path with a bare origin keeps tsdf_integrate's "no orientation"
+// (Voxblox's constant weight), so the sharded field equals the unsharded one for every semantics
+int tsdf_integrate_sectors_origin(tsdf_ctx* const* ctxs, uint32_t n_ctx, const void* pts,
+                                  uint64_t n, uint32_t point_step, uint32_t xyz_offset,
+                                  int32_t xyz_is_f64, const double origin[3]) {
+    if (!ctxs || n_ctx == 0 || n_ctx > TSDF_MAX_WORLD) return TSDF_EINVAL;
+    for (uint32_t k = 0; k < n_ctx; k++)
+        if (!ctxs[k]) return TSDF_EINVAL;
+    if (!origin) return fail(ctxs[0], TSDF_EINVAL, "null argument");
+    return sectors_impl(ctxs, n_ctx, pts, n, point_step, xyz_offset, xyz_is_f64,
+                        pose_of_origin(origin));
+}
+
+}  // extern "C"
+
+static int sectors_impl(tsdf_ctx* const* ctxs, uint32_t n_ctx, const void* pts, uint64_t n,
+                        uint32_t point_step, uint32_t xyz_offset, int32_t xyz_is_f64,
+                        const ScanPose& P) {
     tsdf_ctx* c0 = ctxs[0];
-    if ((!pts && n) || !pose) return fail(c0, TSDF_EINVAL, "null argument");
+    if (!pts && n) return fail(c0, TSDF_EINVAL, "null argument");
     const uint32_t need = xyz_is_f64 ? 24u : 12u;
     if (point_step < need || xyz_offset > point_step - need)
         return fail(c0, TSDF_EINVAL, "point_step/xyz_offset inconsistent");
-    const double qn = pose[3] * pose[3] + pose[4] * pose[4] + pose[5] * pose[5] + pose[6] * pose[6];
-    if (!(qn > 0.0) || !std::isfinite(qn)) return fail(c0, TSDF_EINVAL, "pose quaternion is zero");
+    for (uint32_t k = 0; k < n_ctx; k++)
+        if (border_busy(ctxs[k])) {
+            if (k) c0->err = ctxs[k]->err;
+            return TSDF_EINVAL;
+        }
     for (uint32_t k = 0; k < n_ctx; k++) {
         const tsdf_ctx* c = ctxs[k];
         const bool sharded = n_ctx == 1 ? c->p.n_sectors <= 1 : c->p.n_sectors == n_ctx;
@@ -1672,7 +1717,6 @@ int tsdf_integrate_sectors(tsdf_ctx* const* ctxs, uint32_t n_ctx, const void* pt
             return fail(c0, TSDF_EINVAL, "scan of %llu points exceeds max_points of context %u",
                         (unsigned long long)n, k);
     }
-    const ScanPose P = pose_of(pose);
     const float ox = (float)P.o[0], oy = (float)P.o[1];
     HostTiming& ht = c0->split_ht;
     ht.start();
@@ -1828,6 +1872,8 @@ int tsdf_integrate_sectors(tsdf_ctx* const* ctxs, uint32_t n_ctx, const void* pt
     return TSDF_OK;
 }
 
+extern "C" {
+
 int tsdf_integrate_pose(tsdf_ctx* c, const void* pts, uint64_t n, uint32_t point_step,
                         uint32_t xyz_offset, int32_t xyz_is_f64, const double pose[7]) {
     if (!c) return TSDF_EINVAL;
@@ -1841,6 +1887,7 @@ int tsdf_integrate_pose(tsdf_ctx* c, const void* pts, uint64_t n, uint32_t point
 static int batch_device_impl(tsdf_ctx* c, const float* d_xyz, const uint64_t* offs,
                              uint32_t n_scans, const double* origins, int pose_stride) {
     if (!c) return TSDF_EINVAL;
+    if (border_busy(c)) return TSDF_EINVAL;
     if (!offs || !origins || (!d_xyz && n_scans)) return fail(c, TSDF_EINVAL, "null argument");
     for (uint32_t s = 0; s < n_scans; s++) {
         if (offs[s + 1] < offs[s]) return fail(c, TSDF_EINVAL, "scan_offsets not monotone");
@@ -1895,6 +1942,7 @@ int tsdf_integrate_batch_device_pose(tsdf_ctx* c, const float* d_xyz, const uint
 // (and a capacity replay re-reads the library's copy, not the caller's memory).
 int tsdf_integrate_device(tsdf_ctx* c, const float* d_xyz, uint64_t n, const double origin[3]) {
     if (!c) return TSDF_EINVAL;
+    if (border_busy(c)) return TSDF_EINVAL;
     if ((!d_xyz && n) || !origin) return fail(c, TSDF_EINVAL, "null argument");
     if (n > c->max_points)
         return fail(c, TSDF_EINVAL, "scan of %llu points exceeds max_points %llu",
@@ -2119,6 +2167,130 @@ int tsdf_os_cartesian_device(tsdf_ctx* c, const uint32_t* d_range, uint64_t n, c
     return TSDF_OK;
 }
 
+}  // extern "C"
+
+// A context's halo for meshing (ABI v9): received tiles as a small hash table + pool on the
+// context's device (the mesh kernels look neighbours up there first).
+struct Halo {
+    Table H{};
+    Pool HP{};
+    void* mem[4] = {};
+    void release() {
+        for (void*& q : mem)
+            if (q) {
+                (void)hipFree(q);
+                q = nullptr;
+            }
+    }
+};
+
+static int halo_build(tsdf_ctx* c, const uint32_t* d_halo, uint64_t n_halo, Halo& h) {
+    if (!n_halo) return TSDF_OK;
+    if (!d_halo) return fail(c, TSDF_EINVAL, "null halo tiles");
+    if (n_halo >= (1ull << 30)) return fail(c, TSDF_EINVAL, "too many halo tiles");
+    const uint64_t cap = next_pow2(2 * n_halo);
+    hipError_t e = hipMalloc(&h.mem[0], cap * 8);
+    if (e == hipSuccess) e = hipMalloc(&h.mem[1], cap * 4);
+    if (e == hipSuccess) e = hipMalloc(&h.mem[2], n_halo * BRICK_VOX * 8);
+    if (e == hipSuccess) e = hipMalloc(&h.mem[3], 16);
+    if (e == hipSuccess) {
+        h.H.keys = static_cast<uint64_t*>(h.mem[0]);
+        h.H.slots = static_cast<uint32_t*>(h.mem[1]);
+        h.H.mask = cap - 1;
+        h.H.max_bricks = (uint32_t)n_halo;
+        h.HP.sdf = static_cast<float*>(h.mem[2]);
+        h.HP.weight = h.HP.sdf + n_halo * BRICK_VOX;
+        e = launch_fill_u64(h.H.keys, EMPTY_KEY, cap, c->stream);
+    }
+    if (e == hipSuccess) e = hipMemsetAsync(h.mem[3], 0, 16, c->stream);
+    if (e == hipSuccess)
+        e = launch_halo_build(h.H, h.HP, d_halo, (uint32_t)n_halo, static_cast<uint32_t*>(h.mem[3]),
+                              c->stream);
+    uint32_t ovf = 0;
+    if (e == hipSuccess) e = hipMemcpyAsync(&ovf, h.mem[3], 4, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) {
+        h.release();
+        return fail(c, TSDF_EHIP, "halo: %s", hipGetErrorString(e));
+    }
+    if (ovf) {
+        h.release();
+        return fail(c, TSDF_EINVAL, "halo: table overflow");
+    }
+    return TSDF_OK;
+}
+
+// tsdf_extract_mesh_table, with optional halo tiles (device, TSDF_TILE_WORDS rows) looked up before
+// the context's own table for the +x/+y/+z neighbours of its bricks
+static int mesh_impl(tsdf_ctx* c, float min_weight, int32_t table, const uint32_t* d_halo,
+                     uint64_t n_halo, float* tri, uint64_t cap, uint64_t* n_tri) {
+    if (!c || !n_tri) return TSDF_EINVAL;
+    if (table < 0 || table >= TSDF_MC_TABLES)
+        return fail(c, TSDF_EINVAL, "unknown marching-cubes table %d", table);
+    uint64_t nb = 0;
+    int rc = pool_bricks(c, &nb);
+    if (rc) return rc;
+    *n_tri = 0;
+    if (!nb) return TSDF_OK;
+    if (nb >= 0xFFFFFFFFull) return fail(c, TSDF_EINVAL, "too many bricks");
+    HIPCHK(c, hipSetDevice(c->device));
+    Halo halo;
+    rc = halo_build(c, d_halo, n_halo, halo);
+    if (rc) return rc;
+    // bricks in (z, y, x) order: the triangle soup's order (and the oracle's)
+    std::vector<uint64_t> keys(nb);
+    hipError_t e = hipMemcpy(keys.data(), c->T.brick_keys, nb * 8, hipMemcpyDeviceToHost);
+    std::sort(keys.begin(), keys.end(), [](uint64_t a, uint64_t b) {
+        for (int ax = 2; ax >= 0; ax--) {
+            const uint64_t x = (a >> (21 * ax)) & 0x1FFFFF, y = (b >> (21 * ax)) & 0x1FFFFF;
+            if (x != y) return x < y;
+        }
+        return false;
+    });
+    uint64_t* dk = nullptr;
+    uint32_t* dc = nullptr;
+    uint64_t* doff = nullptr;
+    float* dt = nullptr;
+    std::vector<uint32_t> cnt(nb);
+    std::vector<uint64_t> off(nb);
+    uint64_t total = 0;
+    if (e == hipSuccess) e = hipMalloc(&dk, nb * 8);
+    if (e == hipSuccess) e = hipMalloc(&dc, nb * 4);
+    if (e == hipSuccess) e = hipMemcpyAsync(dk, keys.data(), nb * 8, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess)
+        e = launch_mesh_count(c->T, c->Pl, halo.H, halo.HP, dk, (uint32_t)nb, min_weight, table, dc,
+                              c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(cnt.data(), dc, nb * 4, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess) {
+        for (uint64_t i = 0; i < nb; i++) {
+            off[i] = total;
+            total += cnt[i];
+        }
+        *n_tri = total;
+    }
+    if (e == hipSuccess && tri && total <= cap && total) {
+        e = hipMalloc(&doff, nb * 8);
+        if (e == hipSuccess) e = hipMalloc(&dt, total * 36);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(doff, off.data(), nb * 8, hipMemcpyHostToDevice, c->stream);
+        if (e == hipSuccess)
+            e = launch_mesh_emit(c->T, c->Pl, halo.H, halo.HP, dk, (uint32_t)nb, min_weight, table,
+                                 c->R.vs, doff, dt, c->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(tri, dt, total * 36, hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    }
+    for (void* p : {(void*)dk, (void*)dc, (void*)doff, (void*)dt})
+        if (p) (void)hipFree(p);
+    halo.release();
+    if (e != hipSuccess) return fail(c, TSDF_EHIP, "extract_mesh: %s", hipGetErrorString(e));
+    if (tri && total > cap)
+        return fail(c, TSDF_EOVERFLOW, "mesh has %llu triangles", (unsigned long long)total);
+    return TSDF_OK;
+}
+
+extern "C" {
+
 int tsdf_mc_table(uint8_t* out) {
     if (!out) return TSDF_EINVAL;
     std::memcpy(out, mc_table().tab, sizeof(mc_table().tab));
@@ -2137,68 +2309,13 @@ int tsdf_extract_mesh(tsdf_ctx* c, float min_weight, float* tri, uint64_t cap, u
 
 int tsdf_extract_mesh_table(tsdf_ctx* c, float min_weight, int32_t table, float* tri, uint64_t cap,
                             uint64_t* n_tri) {
-    if (!c || !n_tri) return TSDF_EINVAL;
-    if (table < 0 || table >= TSDF_MC_TABLES)
-        return fail(c, TSDF_EINVAL, "unknown marching-cubes table %d", table);
-    uint64_t nb = 0;
-    int rc = pool_bricks(c, &nb);
-    if (rc) return rc;
-    *n_tri = 0;
-    if (!nb) return TSDF_OK;
-    if (nb >= 0xFFFFFFFFull) return fail(c, TSDF_EINVAL, "too many bricks");
-    // bricks in (z, y, x) order: the triangle soup's order (and the oracle's)
-    std::vector<uint64_t> keys(nb);
-    HIPCHK(c, hipMemcpy(keys.data(), c->T.brick_keys, nb * 8, hipMemcpyDeviceToHost));
-    std::sort(keys.begin(), keys.end(), [](uint64_t a, uint64_t b) {
-        for (int ax = 2; ax >= 0; ax--) {
-            const uint64_t x = (a >> (21 * ax)) & 0x1FFFFF, y = (b >> (21 * ax)) & 0x1FFFFF;
-            if (x != y) return x < y;
-        }
-        return false;
-    });
-    uint64_t* dk = nullptr;
-    uint32_t* dc = nullptr;
-    uint64_t* doff = nullptr;
-    float* dt = nullptr;
-    std::vector<uint32_t> cnt(nb);
-    std::vector<uint64_t> off(nb);
-    uint64_t total = 0;
-    hipError_t e = hipMalloc(&dk, nb * 8);
-    if (e == hipSuccess) e = hipMalloc(&dc, nb * 4);
-    if (e == hipSuccess) e = hipMemcpyAsync(dk, keys.data(), nb * 8, hipMemcpyHostToDevice, c->stream);
-    if (e == hipSuccess)
-        e = launch_mesh_count(c->T, c->Pl, dk, (uint32_t)nb, min_weight, table, dc, c->stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(cnt.data(), dc, nb * 4, hipMemcpyDeviceToHost, c->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-    if (e == hipSuccess) {
-        for (uint64_t i = 0; i < nb; i++) {
-            off[i] = total;
-            total += cnt[i];
-        }
-        *n_tri = total;
-    }
-    if (e == hipSuccess && tri && total <= cap && total) {
-        e = hipMalloc(&doff, nb * 8);
-        if (e == hipSuccess) e = hipMalloc(&dt, total * 36);
-        if (e == hipSuccess)
-            e = hipMemcpyAsync(doff, off.data(), nb * 8, hipMemcpyHostToDevice, c->stream);
-        if (e == hipSuccess)
-            e = launch_mesh_emit(c->T, c->Pl, dk, (uint32_t)nb, min_weight, table, c->R.vs, doff,
-                                 dt, c->stream);
-        if (e == hipSuccess) e = hipMemcpyAsync(tri, dt, total * 36, hipMemcpyDeviceToHost, c->stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-    }
-    for (void* p : {(void*)dk, (void*)dc, (void*)doff, (void*)dt})
-        if (p) (void)hipFree(p);
-    if (e != hipSuccess) return fail(c, TSDF_EHIP, "extract_mesh: %s", hipGetErrorString(e));
-    if (tri && total > cap)
-        return fail(c, TSDF_EOVERFLOW, "mesh has %llu triangles", (unsigned long long)total);
-    return TSDF_OK;
+    return mesh_impl(c, min_weight, table, nullptr, 0, tri, cap, n_tri);
 }
 
 int tsdf_import_bricks(tsdf_ctx* c, const int32_t* coords, const float* sdf, const float* weight,
                        uint64_t n) {
     if (!c) return TSDF_EINVAL;
+    if (border_busy(c)) return TSDF_EINVAL;
     if (!n) return TSDF_OK;
     if (!coords || !sdf || !weight) return fail(c, TSDF_EINVAL, "null argument");
     if (n >= 0xFFFFFFF0ull) return fail(c, TSDF_EINVAL, "too many bricks");
@@ -2455,16 +2572,40 @@ static int border_pack_impl(tsdf_ctx* c, const uint64_t* d_all_keys, const uint6
     return TSDF_OK;
 }
 
+static bool border_busy(tsdf_ctx* c) {
+    if (!c->brd_open) return false;
+    fail(c, TSDF_EINVAL, "a border reduce is open on this context: commit or abort it first "
+                         "(tsdf_border_commit_device)");
+    return true;
+}
+
 extern "C" {
 
+// ABI v9: the pack no longer resets the sent bricks -- their mass stays here until
+// tsdf_border_commit_device(ctx, 1) after the collective and every rank's merge succeeded; an
+// abort keeps it.  The call opens the context's border transaction when it packs rows.
 int tsdf_border_pack_device(tsdf_ctx* c, const uint64_t* d_all_keys, const uint64_t* counts,
                             uint64_t stride, uint32_t world, uint32_t rank, uint32_t* d_send,
                             uint64_t cap_rows, uint64_t* send_counts) {
     if (!c) return TSDF_EINVAL;
-    return border_pack_impl(c, d_all_keys, counts, stride, world, rank, d_send, cap_rows,
-                            send_counts, true, nullptr, nullptr);
+    if (c->brd_n_sent)
+        return fail(c, TSDF_EINVAL, "border pack: the open reduce has packed already (commit first)");
+    HIPCHK(c, hipSetDevice(c->device));
+    uint32_t* rows = nullptr;
+    uint64_t n = 0;
+    const int rc = border_pack_impl(c, d_all_keys, counts, stride, world, rank, d_send, cap_rows,
+                                    send_counts, false, d_send ? &rows : nullptr, &n);
+    if (rc) return rc;
+    if (d_send) {
+        c->brd_open = true;
+        c->brd_sent = rows;
+        c->brd_n_sent = n;
+    }
+    return TSDF_OK;
 }
 
+// The owner's merge of received tiles; the bricks it touches are snapshot first (ABI v9) so an
+// aborted reduce restores them.
 int tsdf_border_merge_device(tsdf_ctx* c, const uint32_t* d_recv, const uint64_t* recv_counts,
                              uint32_t world) {
     if (!c) return TSDF_EINVAL;
@@ -2472,10 +2613,15 @@ int tsdf_border_merge_device(tsdf_ctx* c, const uint32_t* d_recv, const uint64_t
         return fail(c, TSDF_EINVAL, "bad world or null counts");
     uint64_t total = 0;
     for (uint32_t r = 0; r < world; r++) total += recv_counts[r];
+    c->brd_open = true;  // a merge is part of the reduce even when this rank received nothing
     if (!total) return TSDF_OK;
     if (!d_recv) return fail(c, TSDF_EINVAL, "null tile buffer");
     int rc = drain(c);
     if (rc) return rc;
+    uint32_t* bk = nullptr;
+    HIPCHK(c, hipMalloc(&bk, total * TSDF_TILE_WORDS * 4));
+    c->brd_backup.push_back({bk, total});
+    HIPCHK(c, launch_border_snapshot(c->T, c->Pl, d_recv, total, bk, c->stream));
     uint64_t row = 0;
     for (uint32_t r = 0; r < world; r++) {  // sources in ascending rank order
         if (recv_counts[r])
@@ -2487,28 +2633,59 @@ int tsdf_border_merge_device(tsdf_ctx* c, const uint32_t* d_recv, const uint64_t
     return tsdf_sync(c);
 }
 
+// ABI v9: close the context's border transaction.  commit = 1 (the collective and EVERY rank's
+// merge succeeded): the bricks this rank sent are reset to the background -- their mass now lives
+// at their owners.  commit = 0 (abort): the bricks the merges touched are written back as they
+// were, the sent bricks keep their mass; the field is the one before the reduce, bit for bit.
+int tsdf_border_commit_device(tsdf_ctx* c, int32_t commit) {
+    if (!c) return TSDF_EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    hipError_t e = hipSuccess;
+    if (commit) {
+        if (c->brd_n_sent)
+            e = launch_border_reset(c->Pl, c->R.bg, c->brd_sent, (uint32_t)c->brd_n_sent, c->stream);
+    } else {
+        for (size_t k = c->brd_backup.size(); k-- > 0 && e == hipSuccess;)
+            e = launch_border_restore(c->T, c->Pl, c->brd_backup[k].first, c->brd_backup[k].second,
+                                      c->stream);
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess)  // the transaction stays open: the caller may retry
+        return fail(c, TSDF_EHIP, "border %s: %s", commit ? "commit" : "abort",
+                    hipGetErrorString(e));
+    if (c->brd_sent) (void)hipFree(c->brd_sent);
+    c->brd_sent = nullptr;
+    c->brd_n_sent = 0;
+    for (auto& b : c->brd_backup) (void)hipFree(b.first);
+    c->brd_backup.clear();
+    c->brd_open = false;
+    return TSDF_OK;
+}
+
 // ---- one process, several GPUs (SURVEY §8b's num_gpus / device_ids) ------------------------------
 
 int tsdf_create_sharded(const tsdf_params* p, uint32_t n, const int32_t* device_ids, tsdf_ctx** out) {
     if (!p || !out || n == 0 || n > TSDF_MAX_WORLD) return TSDF_EINVAL;
+    int dev0 = 0;
+    if (hipGetDevice(&dev0) != hipSuccess) dev0 = -1;  // the caller's device, restored at the end
     for (uint32_t k = 0; k < n; k++) out[k] = nullptr;
-    for (uint32_t k = 0; k < n; k++) {
+    int rc = TSDF_OK;
+    for (uint32_t k = 0; k < n && rc == TSDF_OK; k++) {
         tsdf_params q = *p;
         q.device_id = device_ids ? device_ids[k] : (int32_t)k;
         q.n_sectors = n > 1 ? n : 0;
         q.sector = k;
-        const int rc = tsdf_create(&q, &out[k]);
+        rc = tsdf_create(&q, &out[k]);
         if (rc) {
             for (uint32_t j = 0; j < k; j++) {
                 tsdf_destroy(out[j]);
                 out[j] = nullptr;
             }
-            return rc;
         }
     }
     // peer access between every pair of distinct devices that supports it, so the input fan-out
     // (tsdf_integrate_sectors) and the border reduce's tile copies go GPU to GPU over xGMI
-    for (uint32_t k = 0; k < n; k++) {
+    for (uint32_t k = 0; k < n && rc == TSDF_OK; k++) {
         tsdf_ctx* c = out[k];
         for (uint32_t j = 0; j < n; j++) {
             const int dk = c->device, dj = out[j]->device;
@@ -2524,127 +2701,305 @@ int tsdf_create_sharded(const tsdf_params* p, uint32_t n, const int32_t* device_
             (void)hipGetLastError();  // an already-enabled pair leaves its error code behind
         }
     }
-    return TSDF_OK;
+    if (dev0 >= 0) (void)hipSetDevice(dev0);  // the caller's device as it was
+    return rc;
 }
+
+}  // extern "C"
+
+// Tiles of `rows` rows from context src's device buffer to context dst's (xGMI peer copy, or a
+// device copy when both share a GPU)
+static hipError_t copy_tiles(tsdf_ctx* dst, uint32_t* d_dst, tsdf_ctx* src, const uint32_t* d_src,
+                             uint64_t rows) {
+    const size_t bytes = rows * TSDF_TILE_WORDS * 4;
+    if (!bytes) return hipSuccess;
+    return src->device == dst->device ? hipMemcpy(d_dst, d_src, bytes, hipMemcpyDeviceToDevice)
+                                      : hipMemcpyPeer(d_dst, dst->device, d_src, src->device, bytes);
+}
+
+// Device buffers of several contexts, freed on their devices at scope end.
+struct DevBufs {
+    std::vector<std::pair<int, void*>> v;
+    int get(tsdf_ctx* c, size_t bytes, void** p) {
+        HIPCHK(c, hipSetDevice(c->device));
+        HIPCHK(c, hipMalloc(p, std::max<size_t>(bytes, 16)));
+        v.push_back({c->device, *p});
+        return TSDF_OK;
+    }
+    ~DevBufs() {
+        for (auto& q : v) {
+            (void)hipSetDevice(q.first);
+            (void)hipFree(q.second);
+        }
+    }
+};
+
+// A failure in a multi-context call: the failing context holds the message, the first gets a copy
+static int first_error(tsdf_ctx* const* ctxs, uint32_t n, int rc) {
+    for (uint32_t k = 1; k < n && ctxs[0]->err.empty(); k++) ctxs[0]->err = ctxs[k]->err;
+    return rc;
+}
+
+extern "C" {
 
 // The border reduce of tsdf_brick_keys_device / tsdf_border_pack_device / tsdf_border_merge_device
 // among the contexts of one process: the keys meet on the host, and each source's tiles go to
 // their owner's GPU with one peer copy per (source, owner) pair (xGMI between GPUs; a device copy
-// when two contexts share a GPU).  Synchronous.
+// when two contexts share a GPU).  Transactional (ABI v9): every context packs without
+// resetting and every owner snapshots before it merges; only when every copy and merge succeeded
+// are the sent bricks reset (commit), otherwise every context is rolled back (abort), so a failed
+// reduce neither loses nor double-counts mass.  Synchronous.
 int tsdf_border_reduce_local(tsdf_ctx* const* ctxs, uint32_t n, uint64_t* bricks_moved) {
     if (!ctxs || n == 0 || n > TSDF_MAX_WORLD) return TSDF_EINVAL;
     for (uint32_t k = 0; k < n; k++)
         if (!ctxs[k]) return TSDF_EINVAL;
     if (bricks_moved) *bricks_moved = 0;
     if (n == 1) return TSDF_OK;
-    tsdf_ctx* c0 = ctxs[0];
-    std::vector<void*> dev_bufs;  // (device, pointer) freed at the end
-    std::vector<int> dev_of;
-    auto dalloc = [&](tsdf_ctx* c, size_t bytes, void** p) -> int {
-        HIPCHK(c, hipSetDevice(c->device));
-        HIPCHK(c, hipMalloc(p, std::max<size_t>(bytes, 16)));
-        dev_bufs.push_back(*p);
-        dev_of.push_back(c->device);
-        return TSDF_OK;
-    };
-    auto release = [&]() {
-        for (size_t i = 0; i < dev_bufs.size(); i++) {
-            (void)hipSetDevice(dev_of[i]);
-            (void)hipFree(dev_bufs[i]);
-        }
-    };
+    for (uint32_t k = 0; k < n; k++)
+        if (border_busy(ctxs[k])) return first_error(ctxs, n, TSDF_EINVAL);
+    int dev0 = 0;
+    if (hipGetDevice(&dev0) != hipSuccess) dev0 = -1;
     int rc = TSDF_OK;
-    // 1. every context's keys, gathered on the host
-    std::vector<uint64_t> counts(n, 0);
-    std::vector<std::vector<uint64_t>> hkeys(n);
-    for (uint32_t k = 0; k < n && !rc; k++) {
-        tsdf_ctx* c = ctxs[k];
-        uint64_t nb = 0;
-        rc = pool_bricks(c, &nb);
-        void* d = nullptr;
-        if (!rc) rc = dalloc(c, nb * 8, &d);
-        if (!rc) rc = tsdf_brick_keys_device(c, static_cast<uint64_t*>(d), nb, &counts[k]);
-        if (!rc) {
-            hkeys[k].resize(counts[k]);
-            if (counts[k] && hipMemcpy(hkeys[k].data(), d, counts[k] * 8, hipMemcpyDeviceToHost) != hipSuccess)
-                rc = fail(c, TSDF_EHIP, "border reduce: key read-back failed");
+    {
+        DevBufs bufs;
+        // 1. every context's keys, gathered on the host
+        std::vector<uint64_t> counts(n, 0);
+        std::vector<std::vector<uint64_t>> hkeys(n);
+        for (uint32_t k = 0; k < n && !rc; k++) {
+            tsdf_ctx* c = ctxs[k];
+            uint64_t nb = 0;
+            rc = pool_bricks(c, &nb);
+            void* d = nullptr;
+            if (!rc) rc = bufs.get(c, nb * 8, &d);
+            if (!rc) rc = tsdf_brick_keys_device(c, static_cast<uint64_t*>(d), nb, &counts[k]);
+            if (!rc) {
+                hkeys[k].resize(counts[k]);
+                if (counts[k] &&
+                    hipMemcpy(hkeys[k].data(), d, counts[k] * 8, hipMemcpyDeviceToHost) != hipSuccess)
+                    rc = fail(c, TSDF_EHIP, "border reduce: key read-back failed");
+            }
+        }
+        uint64_t stride = 1;
+        for (uint32_t k = 0; k < n; k++) stride = std::max(stride, counts[k]);
+        std::vector<uint64_t> all(stride * n, ~0ull);
+        for (uint32_t k = 0; k < n; k++)
+            std::copy(hkeys[k].begin(), hkeys[k].end(), all.begin() + k * stride);
+        // 2. each context packs the bricks a lower rank owns (no reset: the transaction)
+        std::vector<uint32_t*> send(n, nullptr);
+        std::vector<std::vector<uint64_t>> sc(n, std::vector<uint64_t>(n, 0));
+        for (uint32_t k = 0; k < n && !rc; k++) {
+            tsdf_ctx* c = ctxs[k];
+            void *dk = nullptr, *ds = nullptr;
+            rc = bufs.get(c, all.size() * 8, &dk);
+            if (!rc && hipMemcpy(dk, all.data(), all.size() * 8, hipMemcpyHostToDevice) != hipSuccess)
+                rc = fail(c, TSDF_EHIP, "border reduce: key upload failed");
+            if (!rc) rc = bufs.get(c, counts[k] * TSDF_TILE_WORDS * 4, &ds);
+            if (!rc)
+                rc = tsdf_border_pack_device(c, static_cast<uint64_t*>(dk), counts.data(), stride, n,
+                                             k, static_cast<uint32_t*>(ds), counts[k], sc[k].data());
+            send[k] = static_cast<uint32_t*>(ds);
+        }
+        // 3. every owner d receives block d of every source, sources ascending; 4. merge
+        uint64_t moved = 0;
+        for (uint32_t d = 0; d < n && !rc; d++) {
+            tsdf_ctx* c = ctxs[d];
+            std::vector<uint64_t> rcnt(n, 0);
+            uint64_t total = 0;
+            for (uint32_t r = 0; r < n; r++) {
+                rcnt[r] = sc[r][d];
+                total += rcnt[r];
+            }
+            if (!total) continue;
+            void* dr = nullptr;
+            rc = bufs.get(c, total * TSDF_TILE_WORDS * 4, &dr);
+            uint64_t row = 0;
+            for (uint32_t r = 0; r < n && !rc; r++) {
+                if (!rcnt[r]) continue;
+                uint64_t off = 0;
+                for (uint32_t q = 0; q < d; q++) off += sc[r][q];
+                const hipError_t e = copy_tiles(c, static_cast<uint32_t*>(dr) + row * TSDF_TILE_WORDS,
+                                                ctxs[r], send[r] + off * TSDF_TILE_WORDS, rcnt[r]);
+                if (e != hipSuccess)
+                    rc = fail(c, TSDF_EHIP, "border reduce: tile copy: %s", hipGetErrorString(e));
+                row += rcnt[r];
+            }
+            if (!rc) rc = tsdf_border_merge_device(c, static_cast<uint32_t*>(dr), rcnt.data(), n);
+            moved += total;
+        }
+        // 5. commit everywhere when everything succeeded, else roll every context back
+        const int commit = rc == TSDF_OK ? 1 : 0;
+        for (uint32_t k = 0; k < n; k++) {
+            const int crc = tsdf_border_commit_device(ctxs[k], commit);
+            if (crc && !rc) rc = crc;
+        }
+        if (!rc && bricks_moved) *bricks_moved = moved;
+    }
+    if (dev0 >= 0) (void)hipSetDevice(dev0);
+    return rc ? first_error(ctxs, n, rc) : TSDF_OK;
+}
+
+// ---- mesh halo (ABI v9): meshing a sector-sharded field, one owner per cube ---------------------
+
+// The keys of the bricks this context needs to mesh its own and does not observe: for every brick
+// holding an observed voxel, its 7 +x / +y / +z neighbours that hold none here (sorted, unique).
+int tsdf_halo_keys_device(tsdf_ctx* c, uint64_t* d_keys, uint64_t cap, uint64_t* n_out) {
+    if (!c || !n_out) return TSDF_EINVAL;
+    *n_out = 0;
+    uint64_t nb = 0;
+    int rc = drain(c);
+    if (!rc) rc = pool_bricks(c, &nb);
+    if (rc) return rc;
+    if (!nb) return TSDF_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    std::vector<uint64_t> keys(nb);
+    std::vector<uint32_t> obs(nb);
+    uint32_t* d_obs = nullptr;
+    hipError_t e = hipMalloc(&d_obs, nb * 4);
+    if (e == hipSuccess) e = launch_brick_observed(c->Pl, (uint32_t)nb, d_obs, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(obs.data(), d_obs, nb * 4, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(keys.data(), c->T.brick_keys, nb * 8, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (d_obs) (void)hipFree(d_obs);
+    if (e != hipSuccess) return fail(c, TSDF_EHIP, "halo keys: %s", hipGetErrorString(e));
+    std::vector<uint64_t> have;
+    for (uint64_t i = 0; i < nb; i++)
+        if (obs[i]) have.push_back(keys[i]);
+    std::sort(have.begin(), have.end());
+    std::vector<uint64_t> need;
+    for (uint64_t k : have) {
+        const int64_t bx = (int64_t)(k & 0x1FFFFF), by = (int64_t)((k >> 21) & 0x1FFFFF),
+                      bz = (int64_t)((k >> 42) & 0x1FFFFF);
+        for (int d = 1; d < 8; d++) {
+            const int64_t nx = bx + (d & 1), ny = by + ((d >> 1) & 1), nz = bz + (d >> 2);
+            if (nx > 0x1FFFFF || ny > 0x1FFFFF || nz > 0x1FFFFF) continue;
+            const uint64_t q = (uint64_t)nx | ((uint64_t)ny << 21) | ((uint64_t)nz << 42);
+            if (!std::binary_search(have.begin(), have.end(), q)) need.push_back(q);
         }
     }
-    uint64_t stride = 1;
-    for (uint32_t k = 0; k < n; k++) stride = std::max(stride, counts[k]);
-    std::vector<uint64_t> all(stride * n, ~0ull);
-    for (uint32_t k = 0; k < n; k++) std::copy(hkeys[k].begin(), hkeys[k].end(), all.begin() + k * stride);
-    // 2. each context packs the bricks a lower rank owns, WITHOUT resetting them: the sources
-    // keep their mass until every merge has succeeded (step 5), so a failed copy or merge loses
-    // nothing
-    std::vector<uint32_t*> send(n, nullptr);
-    std::vector<uint32_t*> sent_rows(n, nullptr);
-    std::vector<uint64_t> n_sent(n, 0);
-    std::vector<std::vector<uint64_t>> sc(n, std::vector<uint64_t>(n, 0));
-    for (uint32_t k = 0; k < n && !rc; k++) {
-        tsdf_ctx* c = ctxs[k];
-        void *dk = nullptr, *ds = nullptr;
-        rc = dalloc(c, all.size() * 8, &dk);
-        if (!rc && hipMemcpy(dk, all.data(), all.size() * 8, hipMemcpyHostToDevice) != hipSuccess)
-            rc = fail(c, TSDF_EHIP, "border reduce: key upload failed");
-        if (!rc) rc = dalloc(c, counts[k] * TSDF_TILE_WORDS * 4, &ds);
-        if (!rc)
-            rc = border_pack_impl(c, static_cast<uint64_t*>(dk), counts.data(), stride, n, k,
-                                  static_cast<uint32_t*>(ds), counts[k], sc[k].data(), false,
-                                  &sent_rows[k], &n_sent[k]);
-        if (sent_rows[k]) {  // freed with the other buffers
-            dev_bufs.push_back(sent_rows[k]);
-            dev_of.push_back(c->device);
-        }
-        send[k] = static_cast<uint32_t*>(ds);
-    }
-    // 3. every owner d receives block d of every source, sources ascending; 4. merge
-    uint64_t moved = 0;
-    for (uint32_t d = 0; d < n && !rc; d++) {
-        tsdf_ctx* c = ctxs[d];
-        std::vector<uint64_t> rcnt(n, 0);
-        uint64_t total = 0;
-        for (uint32_t r = 0; r < n; r++) {
-            rcnt[r] = sc[r][d];
-            total += rcnt[r];
-        }
-        if (!total) continue;
-        void* dr = nullptr;
-        rc = dalloc(c, total * TSDF_TILE_WORDS * 4, &dr);
-        uint64_t row = 0;
-        for (uint32_t r = 0; r < n && !rc; r++) {
-            if (!rcnt[r]) continue;
-            uint64_t off = 0;
-            for (uint32_t q = 0; q < d; q++) off += sc[r][q];
-            const size_t bytes = rcnt[r] * TSDF_TILE_WORDS * 4;
-            uint32_t* dst = static_cast<uint32_t*>(dr) + row * TSDF_TILE_WORDS;
-            const uint32_t* src = send[r] + off * TSDF_TILE_WORDS;
-            const hipError_t e = ctxs[r]->device == c->device
-                                     ? hipMemcpy(dst, src, bytes, hipMemcpyDeviceToDevice)
-                                     : hipMemcpyPeer(dst, c->device, src, ctxs[r]->device, bytes);
-            if (e != hipSuccess) rc = fail(c, TSDF_EHIP, "border reduce: tile copy: %s", hipGetErrorString(e));
-            row += rcnt[r];
-        }
-        if (!rc) rc = tsdf_border_merge_device(c, static_cast<uint32_t*>(dr), rcnt.data(), n);
-        moved += total;
-    }
-    // 5. every merge succeeded: the sent bricks' mass now lives at their owners, reset the sources
-    for (uint32_t k = 0; k < n && !rc; k++) {
-        if (!n_sent[k]) continue;
-        tsdf_ctx* c = ctxs[k];
-        hipError_t e = hipSetDevice(c->device);
-        if (e == hipSuccess)
-            e = launch_border_reset(c->Pl, c->R.bg, sent_rows[k], (uint32_t)n_sent[k], c->stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-        if (e != hipSuccess) rc = fail(c, TSDF_EHIP, "border reduce: reset: %s", hipGetErrorString(e));
-    }
-    release();
-    if (rc) {  // the failing context holds the message; the first context gets a copy
-        for (uint32_t k = 1; k < n && c0->err.empty(); k++) c0->err = ctxs[k]->err;
-        return rc;
-    }
-    if (bricks_moved) *bricks_moved = moved;
+    std::sort(need.begin(), need.end());
+    need.erase(std::unique(need.begin(), need.end()), need.end());
+    *n_out = need.size();
+    if (need.size() > cap)
+        return fail(c, TSDF_EOVERFLOW, "halo keys need %llu entries", (unsigned long long)need.size());
+    if (need.empty()) return TSDF_OK;
+    if (!d_keys) return fail(c, TSDF_EINVAL, "null key buffer");
+    HIPCHK(c, hipMemcpy(d_keys, need.data(), need.size() * 8, hipMemcpyHostToDevice));
     return TSDF_OK;
+}
+
+// The tiles of the requested bricks (device keys) that this context observes, into d_send (device,
+// cap_rows rows; row order unspecified); *n_rows = the tiles (TSDF_EOVERFLOW above cap_rows).
+int tsdf_halo_pack_device(tsdf_ctx* c, const uint64_t* d_req, uint64_t n_req, uint32_t* d_send,
+                          uint64_t cap_rows, uint64_t* n_rows) {
+    if (!c || !n_rows) return TSDF_EINVAL;
+    *n_rows = 0;
+    if (!n_req) return TSDF_OK;
+    if (!d_req || !d_send) return fail(c, TSDF_EINVAL, "null buffer");
+    if (n_req >= 0xFFFFFFFFull || cap_rows >= 0xFFFFFFFFull)
+        return fail(c, TSDF_EINVAL, "too many halo requests");
+    int rc = drain(c);
+    if (rc) return rc;
+    HIPCHK(c, hipSetDevice(c->device));
+    uint32_t* d_n = nullptr;
+    uint32_t nr = 0;
+    hipError_t e = hipMalloc(&d_n, 4);
+    if (e == hipSuccess) e = hipMemsetAsync(d_n, 0, 4, c->stream);
+    if (e == hipSuccess)
+        e = launch_halo_pack(c->T, c->Pl, d_req, (uint32_t)n_req, d_send, (uint32_t)cap_rows, d_n,
+                             c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(&nr, d_n, 4, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (d_n) (void)hipFree(d_n);
+    if (e != hipSuccess) return fail(c, TSDF_EHIP, "halo pack: %s", hipGetErrorString(e));
+    *n_rows = nr;
+    if (nr > cap_rows) return fail(c, TSDF_EOVERFLOW, "halo pack needs %u rows", nr);
+    return TSDF_OK;
+}
+
+// tsdf_extract_mesh_table over this context's bricks, with the halo tiles (device) looked up first
+// for their neighbours: after a border reduce, the union of every context's mesh is the mesh of
+// the union field, each cube meshed by the owner of its min voxel's brick.
+int tsdf_extract_mesh_halo(tsdf_ctx* c, float min_weight, int32_t table, const uint32_t* d_halo,
+                           uint64_t n_halo, float* tri, uint64_t cap, uint64_t* n_tri) {
+    return mesh_impl(c, min_weight, table, d_halo, n_halo, tri, cap, n_tri);
+}
+
+// The sharded mesh among the contexts of one process (2 cm + marching cubes on N
+// GPUs): border reduce, halo exchange with one peer copy per (holder, requester) pair, one mesh per
+// context; tri holds the contexts' soups one after another in context order (tri == NULL: count).
+int tsdf_extract_mesh_local(tsdf_ctx* const* ctxs, uint32_t n, float min_weight, int32_t table,
+                            float* tri, uint64_t cap, uint64_t* n_tri) {
+    if (!ctxs || n == 0 || n > TSDF_MAX_WORLD || !n_tri) return TSDF_EINVAL;
+    for (uint32_t k = 0; k < n; k++)
+        if (!ctxs[k]) return TSDF_EINVAL;
+    *n_tri = 0;
+    if (n == 1) return tsdf_extract_mesh_table(ctxs[0], min_weight, table, tri, cap, n_tri);
+    int rc = tsdf_border_reduce_local(ctxs, n, nullptr);
+    if (rc) return rc;
+    int dev0 = 0;
+    if (hipGetDevice(&dev0) != hipSuccess) dev0 = -1;
+    {
+        DevBufs bufs;
+        // every context's requests
+        std::vector<void*> req(n, nullptr);
+        std::vector<uint64_t> nreq(n, 0);
+        for (uint32_t k = 0; k < n && !rc; k++) {
+            rc = tsdf_halo_keys_device(ctxs[k], nullptr, 0, &nreq[k]);
+            if (rc == TSDF_EOVERFLOW) rc = TSDF_OK;
+            if (!rc) rc = bufs.get(ctxs[k], nreq[k] * 8, &req[k]);
+            uint64_t got = 0;
+            if (!rc) rc = tsdf_halo_keys_device(ctxs[k], static_cast<uint64_t*>(req[k]), nreq[k], &got);
+        }
+        // holder j packs for requester k on j's GPU; the tiles go to k's halo buffer
+        std::vector<void*> halo(n, nullptr);
+        std::vector<uint64_t> nh(n, 0);
+        for (uint32_t k = 0; k < n && !rc; k++) {
+            if (!nreq[k]) continue;
+            rc = bufs.get(ctxs[k], nreq[k] * TSDF_TILE_WORDS * 4, &halo[k]);
+            for (uint32_t j = 0; j < n && !rc; j++) {
+                if (j == k) continue;
+                void *dq = nullptr, *ds = nullptr;
+                rc = bufs.get(ctxs[j], nreq[k] * 8, &dq);
+                if (!rc) {
+                    const hipError_t e =
+                        ctxs[j]->device == ctxs[k]->device
+                            ? hipMemcpy(dq, req[k], nreq[k] * 8, hipMemcpyDeviceToDevice)
+                            : hipMemcpyPeer(dq, ctxs[j]->device, req[k], ctxs[k]->device, nreq[k] * 8);
+                    if (e != hipSuccess)
+                        rc = fail(ctxs[j], TSDF_EHIP, "halo: key copy: %s", hipGetErrorString(e));
+                }
+                if (!rc) rc = bufs.get(ctxs[j], nreq[k] * TSDF_TILE_WORDS * 4, &ds);
+                uint64_t rows = 0;
+                if (!rc)
+                    rc = tsdf_halo_pack_device(ctxs[j], static_cast<uint64_t*>(dq), nreq[k],
+                                               static_cast<uint32_t*>(ds), nreq[k] - nh[k], &rows);
+                if (!rc) {
+                    const hipError_t e = copy_tiles(
+                        ctxs[k], static_cast<uint32_t*>(halo[k]) + nh[k] * TSDF_TILE_WORDS, ctxs[j],
+                        static_cast<uint32_t*>(ds), rows);
+                    if (e != hipSuccess)
+                        rc = fail(ctxs[k], TSDF_EHIP, "halo: tile copy: %s", hipGetErrorString(e));
+                }
+                nh[k] += rows;
+            }
+        }
+        // one mesh per context, soups concatenated
+        uint64_t total = 0;
+        for (uint32_t k = 0; k < n && !rc; k++) {
+            uint64_t nt = 0;
+            float* out = tri && total <= cap ? tri + 9 * total : nullptr;
+            rc = mesh_impl(ctxs[k], min_weight, table, static_cast<uint32_t*>(halo[k]), nh[k], out,
+                           tri && total <= cap ? cap - total : 0, &nt);
+            if (rc == TSDF_EOVERFLOW) rc = TSDF_OK;  // the total decides below
+            total += nt;
+        }
+        *n_tri = total;
+        if (!rc && tri && total > cap)
+            rc = fail(ctxs[0], TSDF_EOVERFLOW, "mesh has %llu triangles", (unsigned long long)total);
+    }
+    if (dev0 >= 0) (void)hipSetDevice(dev0);
+    return rc ? first_error(ctxs, n, rc) : TSDF_OK;
 }
 
 }  // extern "C"

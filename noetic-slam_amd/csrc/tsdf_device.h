@@ -350,6 +350,22 @@ hipError_t launch_border_reset(const Pool& Pl, float bg, const uint32_t* d_rows,
 // max_w: the merged weight's cap (Voxblox max_weight; +inf for VDBFusion)
 hipError_t launch_border_merge(const Table& T, const Pool& Pl, const uint32_t* d_recv,
                                uint64_t n_rows, Globals* G, float max_w, hipStream_t st);
+// ABI v9 border transaction: the bricks of n_rows received tiles as they are before the merge
+// (tiles; key EMPTY_KEY when the brick is not held), and their restore on abort
+hipError_t launch_border_snapshot(const Table& T, const Pool& Pl, const uint32_t* d_recv,
+                                  uint64_t n_rows, uint32_t* d_backup, hipStream_t st);
+hipError_t launch_border_restore(const Table& T, const Pool& Pl, const uint32_t* d_backup,
+                                 uint64_t n_rows, hipStream_t st);
+// mesh halo (ABI v9): per pool slot, 1 when the brick holds an observed voxel
+hipError_t launch_brick_observed(const Pool& Pl, uint32_t n_bricks, uint32_t* d_obs,
+                                 hipStream_t st);
+// tiles of the requested bricks observed here (rows counted in *d_n_rows, atomic order)
+hipError_t launch_halo_pack(const Table& T, const Pool& Pl, const uint64_t* d_req, uint32_t n_req,
+                            uint32_t* d_send, uint32_t cap_rows, uint32_t* d_n_rows,
+                            hipStream_t st);
+// received halo tiles -> a hash table H (slot = row) and pool HP (the mesh's second lookup)
+hipError_t launch_halo_build(const Table& H, const Pool& HP, const uint32_t* d_tiles,
+                             uint32_t n_rows, uint32_t* d_ovf, hipStream_t st);
 // Voxblox MergedTsdfIntegrator's bundling pre-pass (tsdf_merged.hip): per batch, the points of
 // every scan bundled by voxel; xyz_out / w_out hold one ray per bundle at its first point's slot
 // (other slots: NaN point, weight 0), so the batch keeps its ray layout and block counts
@@ -390,11 +406,14 @@ hipError_t launch_os_xyz(const uint32_t* d_range, uint64_t n, const float* d_dir
 // both case tables (TSDF_MC_GENERATED, TSDF_MC_LORENSEN); `tab` selects one per launch
 constexpr int MC_TABLES = 3;  // include/tsdf_hip.h TSDF_MC_TABLES
 hipError_t upload_mc_table(const uint8_t tab[MC_TABLES][256][32], const uint8_t edge[12][2]);
-hipError_t launch_mesh_count(const Table& T, const Pool& Pl, const uint64_t* d_keys, uint32_t nb,
-                             float min_weight, int tab, uint32_t* d_counts, hipStream_t st);
-hipError_t launch_mesh_emit(const Table& T, const Pool& Pl, const uint64_t* d_keys, uint32_t nb,
-                            float min_weight, int tab, float vs, const uint64_t* d_offsets,
-                            float* d_tri, hipStream_t st);
+// H / HP: halo bricks looked up before the context's own table (ABI v9: bricks another rank
+// owns; H.keys == nullptr: none)
+hipError_t launch_mesh_count(const Table& T, const Pool& Pl, const Table& H, const Pool& HP,
+                             const uint64_t* d_keys, uint32_t nb, float min_weight, int tab,
+                             uint32_t* d_counts, hipStream_t st);
+hipError_t launch_mesh_emit(const Table& T, const Pool& Pl, const Table& H, const Pool& HP,
+                            const uint64_t* d_keys, uint32_t nb, float min_weight, int tab,
+                            float vs, const uint64_t* d_offsets, float* d_tri, hipStream_t st);
 hipError_t launch_fill_u32(uint32_t* p, uint32_t v, uint64_t n, hipStream_t st);
 hipError_t launch_fill_u64(uint64_t* p, uint64_t v, uint64_t n, hipStream_t st);
 

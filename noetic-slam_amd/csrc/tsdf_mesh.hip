@@ -25,32 +25,49 @@ __constant__ uint8_t c_edge[12][2];  // edge -> corners (a, b), b = a | axis bit
 constexpr int MESH_THREADS = 512;
 constexpr int TILE = 9;
 
-// Stage the 9^3 tile of brick `key`: s_ok[t] = observed (W > 0, W >= min_weight).
-__device__ void mesh_tile(const Table& T, const Pool& Pl, uint64_t key, float min_weight,
-                          float* s_S, uint8_t* s_ok, uint32_t* s_slot) {
+// Stage the 9^3 tile of brick `key`: s_ok[t] = observed (W > 0, W >= min_weight).  A neighbour is
+// looked up in the halo (H, HP) first -- bricks another rank owns after a border reduce, of which
+// this context may hold a reset copy -- then in the context's own table.
+__device__ void mesh_tile(const Table& T, const Pool& Pl, const Table& H, const Pool& HP,
+                          uint64_t key, float min_weight, float* s_S, uint8_t* s_ok,
+                          uint32_t* s_slot) {
     const int bx = (int)(key & 0x1FFFFFu) - BRICK_COORD_BIAS;
     const int by = (int)((key >> 21) & 0x1FFFFFu) - BRICK_COORD_BIAS;
     const int bz = (int)((key >> 42) & 0x1FFFFFu) - BRICK_COORD_BIAS;
     if (threadIdx.x < 8) {  // the brick and its 7 +x/+y/+z neighbours
         const int dx = threadIdx.x & 1, dy = (threadIdx.x >> 1) & 1, dz = threadIdx.x >> 2;
-        uint32_t slot = INVALID_SLOT;
+        uint32_t slot = INVALID_SLOT, src = 0u;
         const int nx = bx + dx, ny = by + dy, nz = bz + dz;
         if (nx < BRICK_COORD_BIAS && ny < BRICK_COORD_BIAS && nz < BRICK_COORD_BIAS) {
-            const int64_t h = table_find(T, pack_brick(nx, ny, nz));
-            if (h >= 0) slot = T.slots[h];
+            const uint64_t nk = pack_brick(nx, ny, nz);
+            if (H.keys) {
+                const int64_t h = table_find(H, nk);
+                if (h >= 0) {
+                    slot = H.slots[h];
+                    src = 1u << 31;
+                }
+            }
+            if (!src) {
+                const int64_t h = table_find(T, nk);
+                if (h >= 0) slot = T.slots[h];
+            }
         }
-        s_slot[threadIdx.x] = slot;
+        // bit 31: a halo slot (slots are < 2^31 in both pools)
+        s_slot[threadIdx.x] = slot < T.max_bricks || src ? slot | src : INVALID_SLOT;
     }
     __syncthreads();
     for (int t = threadIdx.x; t < TILE * TILE * TILE; t += MESH_THREADS) {
         const int tx = t % TILE, ty = (t / TILE) % TILE, tz = t / (TILE * TILE);
-        const uint32_t slot = s_slot[(tx >> 3) | ((ty >> 3) << 1) | ((tz >> 3) << 2)];
+        const uint32_t ss = s_slot[(tx >> 3) | ((ty >> 3) << 1) | ((tz >> 3) << 2)];
+        const bool halo = ss != INVALID_SLOT && (ss >> 31);
+        const uint32_t slot = ss & 0x7FFFFFFFu;
+        const Pool& P = halo ? HP : Pl;
         float S = 0.0f;
         uint8_t ok = 0;
-        if (slot < T.max_bricks) {
+        if (ss != INVALID_SLOT && slot < (halo ? H.max_bricks : T.max_bricks)) {
             const size_t i = (size_t)slot * BRICK_VOX + ((tz & 7) << 6) + ((ty & 7) << 3) + (tx & 7);
-            const float W = Pl.weight[i];
-            S = Pl.sdf[i];
+            const float W = P.weight[i];
+            S = P.sdf[i];
             ok = (W > 0.0f && W >= min_weight) ? 1 : 0;
         }
         s_S[t] = S;
@@ -72,7 +89,7 @@ __device__ __forceinline__ int mesh_case(const float* s_S, const uint8_t* s_ok, 
     return k;
 }
 
-__global__ __launch_bounds__(MESH_THREADS) void k_mesh_count(Table T, Pool Pl,
+__global__ __launch_bounds__(MESH_THREADS) void k_mesh_count(Table T, Pool Pl, Table H, Pool HP,
                                                             const uint64_t* __restrict__ keys,
                                                             uint32_t nb, float min_weight,
                                                             uint32_t* __restrict__ counts, int tab) {
@@ -82,7 +99,7 @@ __global__ __launch_bounds__(MESH_THREADS) void k_mesh_count(Table T, Pool Pl,
     __shared__ uint32_t s_sum;
     for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
         if (threadIdx.x == 0) s_sum = 0u;
-        mesh_tile(T, Pl, keys[b], min_weight, s_S, s_ok, s_slot);
+        mesh_tile(T, Pl, H, HP, keys[b], min_weight, s_S, s_ok, s_slot);
         float S[8];
         const int k = mesh_case(s_S, s_ok, threadIdx.x, S);
         const uint32_t nt = k >= 0 ? c_mc[tab][k][0] : 0u;
@@ -94,7 +111,7 @@ __global__ __launch_bounds__(MESH_THREADS) void k_mesh_count(Table T, Pool Pl,
     }
 }
 
-__global__ __launch_bounds__(MESH_THREADS) void k_mesh_emit(Table T, Pool Pl,
+__global__ __launch_bounds__(MESH_THREADS) void k_mesh_emit(Table T, Pool Pl, Table H, Pool HP,
                                                            const uint64_t* __restrict__ keys,
                                                            uint32_t nb, float min_weight, float vs,
                                                            const uint64_t* __restrict__ offsets, int tab,
@@ -106,7 +123,7 @@ __global__ __launch_bounds__(MESH_THREADS) void k_mesh_emit(Table T, Pool Pl,
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
         const uint64_t key = keys[b];
-        mesh_tile(T, Pl, key, min_weight, s_S, s_ok, s_slot);
+        mesh_tile(T, Pl, H, HP, key, min_weight, s_S, s_ok, s_slot);
         float S[8];
         const int l = threadIdx.x;
         const int k = mesh_case(s_S, s_ok, l, S);
@@ -151,21 +168,23 @@ hipError_t upload_mc_table(const uint8_t tab[MC_TABLES][256][32], const uint8_t 
     return e;
 }
 
-hipError_t launch_mesh_count(const Table& T, const Pool& Pl, const uint64_t* d_keys, uint32_t nb,
-                             float min_weight, int tab, uint32_t* d_counts, hipStream_t st) {
+hipError_t launch_mesh_count(const Table& T, const Pool& Pl, const Table& H, const Pool& HP,
+                             const uint64_t* d_keys, uint32_t nb, float min_weight, int tab,
+                             uint32_t* d_counts, hipStream_t st) {
     if (nb == 0) return hipSuccess;
     const uint32_t grid = nb < 4096u ? nb : 4096u;
-    k_mesh_count<<<grid, MESH_THREADS, 0, st>>>(T, Pl, d_keys, nb, min_weight, d_counts, tab);
+    k_mesh_count<<<grid, MESH_THREADS, 0, st>>>(T, Pl, H, HP, d_keys, nb, min_weight, d_counts,
+                                                tab);
     return hipGetLastError();
 }
 
-hipError_t launch_mesh_emit(const Table& T, const Pool& Pl, const uint64_t* d_keys, uint32_t nb,
-                            float min_weight, int tab, float vs, const uint64_t* d_offsets,
-                            float* d_tri, hipStream_t st) {
+hipError_t launch_mesh_emit(const Table& T, const Pool& Pl, const Table& H, const Pool& HP,
+                            const uint64_t* d_keys, uint32_t nb, float min_weight, int tab,
+                            float vs, const uint64_t* d_offsets, float* d_tri, hipStream_t st) {
     if (nb == 0) return hipSuccess;
     const uint32_t grid = nb < 4096u ? nb : 4096u;
-    k_mesh_emit<<<grid, MESH_THREADS, 0, st>>>(T, Pl, d_keys, nb, min_weight, vs, d_offsets, tab,
-                                               d_tri);
+    k_mesh_emit<<<grid, MESH_THREADS, 0, st>>>(T, Pl, H, HP, d_keys, nb, min_weight, vs,
+                                               d_offsets, tab, d_tri);
     return hipGetLastError();
 }
 

@@ -9,7 +9,7 @@ from ._lib import HIP_LIB, load_hip_library  # noqa: F401
 from .volume import (HipTSDFVolume, MergedTsdfIntegrator, SimpleTsdfIntegrator,  # noqa: F401
                      TSDFVolume,
                      TsdfError, TsdfIntegratorConfig, border_reduce_local, bricks_to_voxels,
-                     integrate_sectors,
+                     extract_mesh_local, integrate_sectors, integrate_sectors_cloud,
                      sector_ids, select_sector)
 
 MAP_BACKENDS = {

@@ -16,7 +16,7 @@ STATUS_NAMES = {
     TSDF_EHIP: "TSDF_EHIP", TSDF_ENODEV: "TSDF_ENODEV", TSDF_EOVERFLOW: "TSDF_EOVERFLOW",
 }
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 TILE_WORDS = 1028  # TSDF_TILE_WORDS: u32 words of one border-brick tile
 MAX_WORLD = 64
 SEM_VDBFUSION = 0
@@ -148,6 +148,16 @@ SIGNATURES = {
     "tsdf_border_pack_device": (C.c_int, [P, P, U64P, C.c_uint64, C.c_uint32, C.c_uint32, P,
                                           C.c_uint64, U64P]),
     "tsdf_border_merge_device": (C.c_int, [P, P, U64P, C.c_uint32]),
+    # ABI v9
+    "tsdf_border_commit_device": (C.c_int, [P, C.c_int32]),
+    "tsdf_integrate_sectors_origin": (C.c_int, [C.POINTER(P), C.c_uint32, P, C.c_uint64,
+                                                C.c_uint32, C.c_uint32, C.c_int32, D3]),
+    "tsdf_halo_keys_device": (C.c_int, [P, P, C.c_uint64, U64P]),
+    "tsdf_halo_pack_device": (C.c_int, [P, P, C.c_uint64, P, C.c_uint64, U64P]),
+    "tsdf_extract_mesh_halo": (C.c_int, [P, C.c_float, C.c_int32, P, C.c_uint64, FP, C.c_uint64,
+                                         U64P]),
+    "tsdf_extract_mesh_local": (C.c_int, [C.POINTER(P), C.c_uint32, C.c_float, C.c_int32, FP,
+                                          C.c_uint64, U64P]),
     "tsdf_extract_mesh": (C.c_int, [P, C.c_float, FP, C.c_uint64, U64P]),
     "tsdf_mc_table": (C.c_int, [C.POINTER(C.c_uint8)]),
     "tsdf_extract_mesh_table": (C.c_int, [P, C.c_float, C.c_int32, FP, C.c_uint64, U64P]),

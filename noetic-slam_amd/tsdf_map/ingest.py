@@ -109,8 +109,11 @@ def cloud_xyz_layout(cloud):
 
 def ingest_bag(volume, path, cloud_topic=DLIO_CLOUD, pose_topic=DLIO_POSE, max_gap_ms=50.0):
     """Integrate every cloud of `cloud_topic` (world frame) from the pose track's pose at its stamp
-    (position: the ray origin; orientation: the sensor axes).  Returns (integrated, skipped)
-    cloud counts."""
+    (position: the ray origin; orientation: the sensor axes).  `volume` may be a list of sector
+    volumes (volume k = sector k of len(volume)): each cloud then goes to all of them through
+    tsdf_integrate_sectors (the N-GPU node's path).  Returns (integrated, skipped) cloud counts."""
+    from .volume import integrate_sectors_cloud
+    sectors = isinstance(volume, (list, tuple))
     bag = rosbag.BagReader(path)
     track = load_poses(bag, pose_topic)
     done = skipped = 0
@@ -123,7 +126,11 @@ def ingest_bag(volume, path, cloud_topic=DLIO_CLOUD, pose_topic=DLIO_POSE, max_g
         off, f64 = cloud_xyz_layout(c)
         # the full pose (x, y, z, qx, qy, qz, qw): the position is the ray origin, the
         # orientation gives Voxblox's sensor z axis (tsdf_integrate_pose)
-        volume.integrate_cloud(c.data, c.width * c.height, c.point_step, off,
-                               np.concatenate([pose[0], pose[1]]), xyz_is_f64=f64)
+        if sectors:
+            integrate_sectors_cloud(volume, c.data, c.width * c.height, c.point_step, off,
+                                    np.concatenate([pose[0], pose[1]]), xyz_is_f64=f64)
+        else:
+            volume.integrate_cloud(c.data, c.width * c.height, c.point_step, off,
+                                   np.concatenate([pose[0], pose[1]]), xyz_is_f64=f64)
         done += 1
     return done, skipped

@@ -140,6 +140,8 @@ class TSDFVolume:
             raise ValueError("method must be one of %s" % sorted(_abi.VB_METHODS))
         p.voxblox_method = _abi.VB_METHODS[method]
         # tsdf_integrate_sectors' transfer (ABI v8): "fanout", "h2d" or "split"
+        if sector_input not in _abi.SECTOR_INPUTS:
+            raise ValueError("sector_input must be one of %s" % sorted(_abi.SECTOR_INPUTS))
         p.sector_input = _abi.SECTOR_INPUTS[sector_input]
         return p
 
@@ -224,21 +226,30 @@ class TSDFVolume:
                                                w.ctypes.data_as(_abi.FP)), "query_dense")
         return s, w
 
-    def extract_triangle_mesh(self, fill_holes=True, min_weight=0.0, table="generated"):
+    def extract_triangle_mesh(self, fill_holes=True, min_weight=0.0, table="generated",
+                              halo=None):
         """VDBVolume.extract_triangle_mesh: (vertices (3T, 3) float32, triangles (T, 3) int64) —
         marching cubes over every cube of 8 observed voxels (W > 0, W >= min_weight), as a soup
         (each triangle owns its 3 vertices).  fill_holes is accepted for API compatibility; cubes
         with an unobserved voxel are never meshed.  table: "generated" (face-consistent, the
-        default) or "lorensen" (the classic table's ambiguity rule, VDBFusion's)."""
+        default) or "lorensen" (the published Lorensen / Bourke table, VDBFusion's).
+        halo: (d_tiles_ptr, n_tiles) of neighbour bricks another rank owns (tsdf_extract_mesh_halo,
+        in `tensor_device` memory): after a border reduce each rank meshes its own cubes."""
         tab = _abi.MC_TABLES[table]
         n = C.c_uint64()
-        self._check(self._lib.tsdf_extract_mesh_table(self._ctx, float(min_weight), tab, None, 0,
-                                                      C.byref(n)), "extract_mesh")
+
+        def call(out, cap):
+            if halo is None:
+                return self._lib.tsdf_extract_mesh_table(self._ctx, float(min_weight), tab, out,
+                                                         cap, C.byref(n))
+            return self._lib.tsdf_extract_mesh_halo(self._ctx, float(min_weight), tab,
+                                                    C.c_void_p(int(halo[0])), int(halo[1]), out,
+                                                    cap, C.byref(n))
+
+        self._check(call(None, 0), "extract_mesh")
         t = np.empty((n.value, 9), np.float32)
         if n.value:
-            self._check(self._lib.tsdf_extract_mesh_table(self._ctx, float(min_weight), tab,
-                                                          t.ctypes.data_as(_abi.FP), n.value,
-                                                          C.byref(n)), "extract_mesh")
+            self._check(call(t.ctypes.data_as(_abi.FP), n.value), "extract_mesh")
         return t.reshape(-1, 3), np.arange(3 * t.shape[0], dtype=np.int64).reshape(-1, 3)
 
     def num_bricks(self):
@@ -301,7 +312,8 @@ class TSDFVolume:
         return n.value
 
     def border_pack(self, d_all_keys_ptr, counts, stride, world, rank, d_send_ptr, cap_rows):
-        """Pack (and reset) the bricks a lower rank owns; returns the rows per destination."""
+        """Pack the bricks a lower rank owns (they keep their mass until border_commit); returns
+        the rows per destination."""
         cnt = np.ascontiguousarray(counts, np.uint64)
         out = np.zeros(int(world), np.uint64)
         self._check(self._lib.tsdf_border_pack_device(
@@ -316,6 +328,30 @@ class TSDFVolume:
             self._ctx, C.c_void_p(int(d_recv_ptr)), cnt.ctypes.data_as(_abi.U64P), cnt.shape[0]),
             "border_merge")
 
+    def border_commit(self, commit=True):
+        """Close the border reduce: commit (every rank merged) resets the sent bricks, abort
+        restores the merged ones; either way the context takes scans again."""
+        self._check(self._lib.tsdf_border_commit_device(self._ctx, 1 if commit else 0),
+                    "border_commit")
+
+    def halo_keys_into(self, d_keys_ptr, cap):
+        """The neighbour bricks this volume needs to mesh its own and does not observe
+        (tsdf_halo_keys_device): returns the count; writes them when cap suffices."""
+        n = C.c_uint64()
+        rc = self._lib.tsdf_halo_keys_device(self._ctx, C.c_void_p(int(d_keys_ptr or 0)), int(cap),
+                                             C.byref(n))
+        if rc != _abi.TSDF_EOVERFLOW or cap:
+            self._check(rc, "halo_keys")
+        return n.value
+
+    def halo_pack(self, d_req_ptr, n_req, d_send_ptr, cap_rows):
+        """Tiles of the requested bricks this volume observes; returns the rows written."""
+        n = C.c_uint64()
+        self._check(self._lib.tsdf_halo_pack_device(self._ctx, C.c_void_p(int(d_req_ptr)),
+                                                    int(n_req), C.c_void_p(int(d_send_ptr)),
+                                                    int(cap_rows), C.byref(n)), "halo_pack")
+        return n.value
+
     # -- stats ----------------------------------------------------------------------------------
     def stats(self):
         st = _abi.TsdfStats()
@@ -328,20 +364,23 @@ class TSDFVolume:
 
 def integrate_sectors(volumes, points, extrinsic):
     """tsdf_integrate_sectors: one host cloud for the sector-sharded contexts `volumes` (volume k
-    created with n_sectors = len(volumes), sector = k, one per GPU): classified and split on the
-    host, each volume receives only its sector's points (live N-GPU input)."""
+    created with n_sectors = len(volumes), sector = k, one per GPU; DESIGN.md §7, live N-GPU
+    input).  A (7,) pose or (4,4) extrinsic carries the sensor orientation; a bare (3,) origin
+    goes to tsdf_integrate_sectors_origin and, like `integrate`, carries none (Voxblox's constant
+    weight), so the sharded field equals the unsharded one for every semantics."""
     pts = np.ascontiguousarray(points)
     if pts.ndim != 2 or pts.shape[1] != 3 or pts.dtype not in (np.float32, np.float64):
         raise ValueError("points must be np.ndarray(n, 3) of float32 / float64")
-    pose = _pose_of(extrinsic)
-    if pose is None:
-        pose = np.concatenate([_origin_of(extrinsic), [0.0, 0.0, 0.0, 1.0]])
     v0 = volumes[0]
     ctxs = (C.c_void_p * len(volumes))(*[v._ctx.value for v in volumes])
     is64 = pts.dtype == np.float64
-    rc = v0._lib.tsdf_integrate_sectors(ctxs, len(volumes), pts.ctypes.data_as(C.c_void_p),
-                                        pts.shape[0], 24 if is64 else 12, 0, 1 if is64 else 0,
-                                        _d3(np.ascontiguousarray(pose, np.float64)))
+    pose = _pose_of(extrinsic)
+    if pose is None:
+        fn, arg = v0._lib.tsdf_integrate_sectors_origin, _origin_of(extrinsic)
+    else:
+        fn, arg = v0._lib.tsdf_integrate_sectors, np.ascontiguousarray(pose, np.float64)
+    rc = fn(ctxs, len(volumes), pts.ctypes.data_as(C.c_void_p), pts.shape[0], 24 if is64 else 12,
+            0, 1 if is64 else 0, _d3(arg))
     v0._check(rc, "integrate_sectors")
 
 
@@ -354,6 +393,40 @@ def border_reduce_local(volumes):
     v0._check(v0._lib.tsdf_border_reduce_local(ctxs, len(volumes), C.byref(moved)),
               "border_reduce_local")
     return moved.value
+
+
+def integrate_sectors_cloud(volumes, data, n, point_step, xyz_offset, extrinsic, xyz_is_f64=False):
+    """integrate_sectors on PointCloud2-style raw records (e.g. dlio::Point, point_step 32)."""
+    buf = np.frombuffer(data, dtype=np.uint8)
+    if buf.size < n * point_step:
+        raise ValueError("buffer smaller than n * point_step")
+    v0 = volumes[0]
+    ctxs = (C.c_void_p * len(volumes))(*[v._ctx.value for v in volumes])
+    pose = _pose_of(extrinsic)
+    if pose is None:
+        fn, arg = v0._lib.tsdf_integrate_sectors_origin, _origin_of(extrinsic)
+    else:
+        fn, arg = v0._lib.tsdf_integrate_sectors, np.ascontiguousarray(pose, np.float64)
+    v0._check(fn(ctxs, len(volumes), buf.ctypes.data_as(C.c_void_p), int(n), int(point_step),
+                 int(xyz_offset), 1 if xyz_is_f64 else 0, _d3(arg)), "integrate_sectors_cloud")
+
+
+def extract_mesh_local(volumes, min_weight=0.0, table="generated"):
+    """tsdf_extract_mesh_local: the mesh of sector volumes of this process (border reduce, halo
+    exchange, one mesh per volume); returns (vertices (3T, 3), triangles (T, 3)) with the volumes'
+    soups in volume order, and the triangles per volume."""
+    v0 = volumes[0]
+    ctxs = (C.c_void_p * len(volumes))(*[v._ctx.value for v in volumes])
+    tab = _abi.MC_TABLES[table]
+    n = C.c_uint64()
+    v0._check(v0._lib.tsdf_extract_mesh_local(ctxs, len(volumes), float(min_weight), tab, None, 0,
+                                              C.byref(n)), "extract_mesh_local")
+    t = np.empty((n.value, 9), np.float32)
+    if n.value:
+        v0._check(v0._lib.tsdf_extract_mesh_local(ctxs, len(volumes), float(min_weight), tab,
+                                                  t.ctypes.data_as(_abi.FP), n.value, C.byref(n)),
+                  "extract_mesh_local")
+    return t.reshape(-1, 3), np.arange(3 * t.shape[0], dtype=np.int64).reshape(-1, 3)
 
 
 def bricks_to_voxels(coords, sdf, weight):

@@ -23,9 +23,9 @@ LIB_PATH = os.path.join(HERE, "build", "libtsdf_oracle.so")
 MODE_SCAN_FUSED = 0
 MODE_SEQUENTIAL = 1
 MODE_VDB_LITERAL = 2  # VDBFusion's own precisions (double sdf, Ray<float> DDA), per-sample update
-HOST_ONLY = ("tsdf_integrate_device", "tsdf_integrate_batch_device", "tsdf_integrate_sectors",
+HOST_ONLY = ("tsdf_integrate_device", "tsdf_integrate_batch_device",
              "tsdf_integrate_batch_device_pose", "tsdf_set_profiling",
-             "tsdf_set_metrics_log", "tsdf_create_sharded", "tsdf_border_reduce_local",
+             "tsdf_set_metrics_log",
              "tsdf_os_packet_bytes", "tsdf_os_decode_device", "tsdf_os_cartesian_device")
 
 _lib = None

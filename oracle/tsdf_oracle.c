@@ -96,7 +96,16 @@ struct tsdf_ctx {
     int mg_on;
     struct tsdf_ctx** sub;
     struct mt_bucket* bk; /* n_thr x n_thr: samples of ray-thread t for partition p at [t n_thr + p] */
+    /* border-reduce transaction (ABI v9; the GPU library's brd_*): the bricks the open reduce's pack
+     * sent (reset at commit), and the voxels its merges touched as they were (restored at abort) */
+    int brd_open;
+    int32_t* brd_sent; /* brick coordinates, 3 per brick */
+    uint64_t brd_n_sent;
+    struct brd_vox* brd_bk;
+    uint64_t brd_n_bk, brd_cap_bk;
 };
+
+struct brd_vox { int32_t x, y, z; float S, W; };
 
 typedef struct { int32_t x, y, z; float s, w; } mt_sample;
 struct mt_bucket { mt_sample* v; uint64_t n, cap; };
@@ -288,6 +297,8 @@ void tsdf_destroy(tsdf_ctx* c) {
     free(c->bk);
     free(c->tab);
     free(c->touched);
+    free(c->brd_sent);
+    free(c->brd_bk);
     free(c);
 }
 
@@ -977,6 +988,8 @@ int tsdf_integrate_pose(tsdf_ctx* c, const void* pts, uint64_t n, uint32_t point
 static int integrate_scan(tsdf_ctx* c, const void* pts, uint64_t n, uint32_t point_step,
                           uint32_t xyz_offset, int32_t xyz_is_f64, const double origin[3]) {
     if (!c || (!pts && n) || !origin) return set_err(c, TSDF_EINVAL, "null argument");
+    if (c->brd_open)
+        return set_err(c, TSDF_EINVAL, "a border reduce is open on this context: commit or abort it first");
     const uint32_t need = xyz_is_f64 ? 24u : 12u;
     if (point_step < need || xyz_offset > point_step - need)
         return set_err(c, TSDF_EINVAL, "point_step/xyz_offset inconsistent");
@@ -1152,9 +1165,19 @@ int tsdf_export_bricks(tsdf_ctx* c, int32_t* coords, float* sdf, float* weight, 
     return TSDF_OK;
 }
 
+static int import_impl(tsdf_ctx* c, const int32_t* coords, const float* sdf, const float* weight,
+                       uint64_t n);
+
 int tsdf_import_bricks(tsdf_ctx* c, const int32_t* coords, const float* sdf, const float* weight,
                        uint64_t n) {
     if (!c || (n && (!coords || !sdf || !weight))) return TSDF_EINVAL;
+    if (c->brd_open)
+        return set_err(c, TSDF_EINVAL, "a border reduce is open on this context: commit or abort it first");
+    return import_impl(c, coords, sdf, weight, n);
+}
+
+static int import_impl(tsdf_ctx* c, const int32_t* coords, const float* sdf, const float* weight,
+                       uint64_t n) {
     if (c->n_thr > 1) return set_err(c, TSDF_EINVAL, "import is not supported in the threaded mode");
     for (uint64_t i = 0; i < n; i++)
         for (int l = 0; l < 512; l++) {
@@ -1338,6 +1361,7 @@ int tsdf_border_pack_device(tsdf_ctx* c, const uint64_t* all_keys, const uint64_
     if (!c || !counts || !send_counts || world == 0 || world > TSDF_MAX_WORLD || rank >= world)
         return set_err(c, TSDF_EINVAL, "bad world/rank or null counts");
     if (c->n_thr > 1) return set_err(c, TSDF_EINVAL, "border reduce needs the serial mode");
+    if (c->brd_n_sent) return set_err(c, TSDF_EINVAL, "border pack: the open reduce has packed already");
     for (uint32_t r = 0; r < world; r++) {
         if (counts[r] > stride) return set_err(c, TSDF_EINVAL, "counts[r] > stride");
         send_counts[r] = 0;
@@ -1363,8 +1387,11 @@ int tsdf_border_pack_device(tsdf_ctx* c, const uint64_t* all_keys, const uint64_
     int rc = TSDF_OK;
     if (send && rows > cap_rows) rc = set_err(c, TSDF_EOVERFLOW, "send buffer too small");
     if (send && rc == TSDF_OK) {
+        /* ABI v9: packed WITHOUT resetting; the sent bricks are reset at commit */
+        c->brd_sent = (int32_t*)malloc((rows ? rows : 1) * 3 * sizeof(int32_t));
+        if (!c->brd_sent) rc = TSDF_ENOMEM;
         uint64_t row = 0;
-        for (uint32_t d = 0; d < rank; d++)
+        for (uint32_t d = 0; d < rank && rc == TSDF_OK; d++)
             for (uint64_t i = 0; i < nb; i++) {
                 if (owner[i] != d) continue;
                 uint32_t* t = send + row * TILE_WORDS;
@@ -1373,20 +1400,37 @@ int tsdf_border_pack_device(tsdf_ctx* c, const uint64_t* all_keys, const uint64_
                 for (int l = 0; l < 512; l++) {
                     const int32_t x = e[i].b[0] * 8 + (l & 7), y = e[i].b[1] * 8 + ((l >> 3) & 7),
                                   z = e[i].b[2] * 8 + (l >> 6);
-                    int64_t k = -1;
                     const vox_t* v = vox_find(c, x, y, z);
-                    if (v) k = v - c->tab;
                     ts[l] = v ? v->S : c->bg;
                     tw[l] = v ? v->W : 0.0f;
-                    if (k >= 0) { c->tab[k].S = c->bg; c->tab[k].W = 0.0f; } /* mass moves out */
                 }
                 const uint64_t key = pack_key(e[i].b);
                 t[1024] = (uint32_t)key; t[1025] = (uint32_t)(key >> 32); t[1026] = 0; t[1027] = 0;
+                memcpy(c->brd_sent + 3 * row, e[i].b, 3 * sizeof(int32_t));
                 row++;
             }
+        if (rc == TSDF_OK) {
+            c->brd_n_sent = rows;
+            c->brd_open = 1;
+        }
     }
     free(e); free(owner); free(sorted);
     return rc;
+}
+
+static void key_brick(uint64_t key, int32_t b[3]) {
+    b[0] = (int32_t)(key & 0x1FFFFF) - (1 << 20);
+    b[1] = (int32_t)((key >> 21) & 0x1FFFFF) - (1 << 20);
+    b[2] = (int32_t)((key >> 42) & 0x1FFFFF) - (1 << 20);
+}
+
+/* a brick holds an observed voxel here */
+static int brick_observed(const tsdf_ctx* c, const int32_t b[3]) {
+    for (int l = 0; l < 512; l++) {
+        const vox_t* v = vox_find(c, b[0] * 8 + (l & 7), b[1] * 8 + ((l >> 3) & 7), b[2] * 8 + (l >> 6));
+        if (v && v->W > 0.0f) return 1;
+    }
+    return 0;
 }
 
 int tsdf_border_merge_device(tsdf_ctx* c, const uint32_t* recv, const uint64_t* recv_counts,
@@ -1396,23 +1440,238 @@ int tsdf_border_merge_device(tsdf_ctx* c, const uint32_t* recv, const uint64_t* 
     if (c->n_thr > 1) return set_err(c, TSDF_EINVAL, "border reduce needs the serial mode");
     uint64_t total = 0;
     for (uint32_t r = 0; r < world; r++) total += recv_counts[r];
+    c->brd_open = 1;
+    /* ABI v9: every received brick as it is before the merge (restored at abort) */
+    if (c->brd_n_bk + 512 * total > c->brd_cap_bk) {
+        const uint64_t nc = c->brd_n_bk + 512 * total + 512;
+        struct brd_vox* q = (struct brd_vox*)realloc(c->brd_bk, nc * sizeof *q);
+        if (!q) return TSDF_ENOMEM;
+        c->brd_bk = q;
+        c->brd_cap_bk = nc;
+    }
+    for (uint64_t row = 0; row < total; row++) {
+        const uint32_t* t = recv + row * TILE_WORDS;
+        int32_t b[3];
+        key_brick((uint64_t)t[1024] | ((uint64_t)t[1025] << 32), b);
+        for (int l = 0; l < 512; l++) {
+            struct brd_vox* o = &c->brd_bk[c->brd_n_bk++];
+            o->x = b[0] * 8 + (l & 7); o->y = b[1] * 8 + ((l >> 3) & 7); o->z = b[2] * 8 + (l >> 6);
+            const vox_t* v = vox_find(c, o->x, o->y, o->z);
+            o->S = v ? v->S : c->bg;
+            o->W = v ? v->W : 0.0f;
+        }
+    }
     for (uint64_t row = 0; row < total; row++) { /* rows are grouped by source, ascending */
         const uint32_t* t = recv + row * TILE_WORDS;
-        const uint64_t key = (uint64_t)t[1024] | ((uint64_t)t[1025] << 32);
-        const int32_t b[3] = {(int32_t)(key & 0x1FFFFF) - (1 << 20),
-                              (int32_t)((key >> 21) & 0x1FFFFF) - (1 << 20),
-                              (int32_t)((key >> 42) & 0x1FFFFF) - (1 << 20)};
-        int held = 0;
-        for (int l = 0; l < 512 && !held; l++) {
-            const vox_t* v = vox_find(c, b[0] * 8 + (l & 7), b[1] * 8 + ((l >> 3) & 7),
-                                      b[2] * 8 + (l >> 6));
-            held = v && v->W > 0.0f;
-        }
-        if (!held) return set_err(c, TSDF_EINVAL, "border merge: a tile's brick is not held here");
-        const int rc = tsdf_import_bricks(c, b, (const float*)t, (const float*)(t + 512), 1);
+        int32_t b[3];
+        key_brick((uint64_t)t[1024] | ((uint64_t)t[1025] << 32), b);
+        if (!brick_observed(c, b))
+            return set_err(c, TSDF_EINVAL, "border merge: a tile's brick is not held here");
+        const int rc = import_impl(c, b, (const float*)t, (const float*)(t + 512), 1);
         if (rc != TSDF_OK) return rc;
     }
     return TSDF_OK;
+}
+
+int tsdf_border_commit_device(tsdf_ctx* c, int32_t commit) {
+    if (!c) return TSDF_EINVAL;
+    if (commit) {
+        for (uint64_t i = 0; i < c->brd_n_sent; i++) {
+            const int32_t* b = c->brd_sent + 3 * i;
+            for (int l = 0; l < 512; l++) {
+                const vox_t* v = vox_find(c, b[0] * 8 + (l & 7), b[1] * 8 + ((l >> 3) & 7), b[2] * 8 + (l >> 6));
+                if (v) { vox_t* w = &c->tab[v - c->tab]; w->S = c->bg; w->W = 0.0f; } /* mass moved out */
+            }
+        }
+    } else {
+        for (uint64_t i = c->brd_n_bk; i-- > 0;) { /* the earliest snapshot of a voxel is written last */
+            const struct brd_vox* o = &c->brd_bk[i];
+            const vox_t* v = vox_find(c, o->x, o->y, o->z);
+            if (v) { vox_t* w = &c->tab[v - c->tab]; w->S = o->S; w->W = o->W; }
+        }
+    }
+    free(c->brd_sent);
+    c->brd_sent = NULL;
+    c->brd_n_sent = 0;
+    c->brd_n_bk = 0;
+    c->brd_open = 0;
+    return TSDF_OK;
+}
+
+/* ---- several contexts in one process (the GPU library's tsdf_create_sharded & co., host-side) */
+
+int tsdf_create_sharded(const tsdf_params* p, uint32_t n, const int32_t* device_ids, tsdf_ctx** out) {
+    (void)device_ids;
+    if (!p || !out || n == 0 || n > TSDF_MAX_WORLD) return TSDF_EINVAL;
+    for (uint32_t k = 0; k < n; k++) out[k] = NULL;
+    for (uint32_t k = 0; k < n; k++) {
+        tsdf_params q = *p;
+        q.n_sectors = n > 1 ? n : 0;
+        q.sector = k;
+        const int rc = tsdf_create(&q, &out[k]);
+        if (rc) {
+            for (uint32_t j = 0; j < k; j++) { tsdf_destroy(out[j]); out[j] = NULL; }
+            return rc;
+        }
+    }
+    return TSDF_OK;
+}
+
+static int sectors_check(tsdf_ctx* const* ctxs, uint32_t n_ctx) {
+    if (!ctxs || n_ctx == 0 || n_ctx > TSDF_MAX_WORLD) return TSDF_EINVAL;
+    for (uint32_t k = 0; k < n_ctx; k++) {
+        const tsdf_ctx* c = ctxs[k];
+        if (!c) return TSDF_EINVAL;
+        const int sharded = n_ctx == 1 ? c->p.n_sectors <= 1 : c->p.n_sectors == n_ctx;
+        if (!sharded || (n_ctx > 1 && (c->p.sector != k || c->p.sector_yaw0 != ctxs[0]->p.sector_yaw0)))
+            return set_err(ctxs[0], TSDF_EINVAL, "a context is not its sector of n (same sector_yaw0)");
+        if (c->brd_open)
+            return set_err(ctxs[0], TSDF_EINVAL, "a border reduce is open on a context");
+    }
+    return TSDF_OK;
+}
+
+/* every context integrates the whole cloud and keeps its sector's rays: the fields the GPU
+ * library's fan-out / split give, bit for bit */
+int tsdf_integrate_sectors(tsdf_ctx* const* ctxs, uint32_t n_ctx, const void* pts, uint64_t n,
+                           uint32_t point_step, uint32_t xyz_offset, int32_t xyz_is_f64,
+                           const double pose[7]) {
+    int rc = sectors_check(ctxs, n_ctx);
+    for (uint32_t k = 0; k < n_ctx && rc == TSDF_OK; k++) {
+        rc = tsdf_integrate_pose(ctxs[k], pts, n, point_step, xyz_offset, xyz_is_f64, pose);
+        if (rc && k) snprintf(ctxs[0]->err, sizeof ctxs[0]->err, "%s", ctxs[k]->err);
+    }
+    return rc;
+}
+
+int tsdf_integrate_sectors_origin(tsdf_ctx* const* ctxs, uint32_t n_ctx, const void* pts,
+                                  uint64_t n, uint32_t point_step, uint32_t xyz_offset,
+                                  int32_t xyz_is_f64, const double origin[3]) {
+    int rc = sectors_check(ctxs, n_ctx);
+    for (uint32_t k = 0; k < n_ctx && rc == TSDF_OK; k++) {
+        rc = tsdf_integrate(ctxs[k], pts, n, point_step, xyz_offset, xyz_is_f64, origin);
+        if (rc && k) snprintf(ctxs[0]->err, sizeof ctxs[0]->err, "%s", ctxs[k]->err);
+    }
+    return rc;
+}
+
+/* the GPU library's tsdf_border_reduce_local on host buffers: keys, pack, merge per owner (sources
+ * ascending), then commit everywhere, or abort everywhere on any failure */
+int tsdf_border_reduce_local(tsdf_ctx* const* ctxs, uint32_t n, uint64_t* bricks_moved) {
+    if (!ctxs || n == 0 || n > TSDF_MAX_WORLD) return TSDF_EINVAL;
+    for (uint32_t k = 0; k < n; k++)
+        if (!ctxs[k]) return TSDF_EINVAL;
+    if (bricks_moved) *bricks_moved = 0;
+    if (n == 1) return TSDF_OK;
+    int rc = TSDF_OK;
+    uint64_t counts[TSDF_MAX_WORLD] = {0}, stride = 1;
+    for (uint32_t k = 0; k < n && rc == TSDF_OK; k++) {
+        if (ctxs[k]->brd_open) rc = set_err(ctxs[0], TSDF_EINVAL, "a border reduce is open on a context");
+        else rc = tsdf_num_bricks(ctxs[k], &counts[k]);
+        if (counts[k] > stride) stride = counts[k];
+    }
+    if (rc) return rc;
+    uint64_t* all = (uint64_t*)malloc(stride * n * sizeof(uint64_t));
+    uint32_t* send[TSDF_MAX_WORLD] = {0};
+    uint64_t sc[TSDF_MAX_WORLD][TSDF_MAX_WORLD];
+    memset(sc, 0, sizeof sc);
+    if (!all) return TSDF_ENOMEM;
+    for (uint64_t i = 0; i < stride * n; i++) all[i] = ~0ull;
+    for (uint32_t k = 0; k < n && rc == TSDF_OK; k++)
+        rc = tsdf_brick_keys_device(ctxs[k], all + k * stride, stride, &counts[k]);
+    for (uint32_t k = 0; k < n && rc == TSDF_OK; k++) {
+        send[k] = (uint32_t*)malloc((counts[k] ? counts[k] : 1) * TILE_WORDS * 4);
+        if (!send[k]) { rc = TSDF_ENOMEM; break; }
+        rc = tsdf_border_pack_device(ctxs[k], all, counts, stride, n, k, send[k], counts[k], sc[k]);
+    }
+    uint64_t moved = 0;
+    for (uint32_t d = 0; d < n && rc == TSDF_OK; d++) {
+        uint64_t rcnt[TSDF_MAX_WORLD] = {0}, total = 0;
+        for (uint32_t r = 0; r < n; r++) { rcnt[r] = sc[r][d]; total += rcnt[r]; }
+        if (!total) continue;
+        uint32_t* recv = (uint32_t*)malloc(total * TILE_WORDS * 4);
+        if (!recv) { rc = TSDF_ENOMEM; break; }
+        uint64_t row = 0;
+        for (uint32_t r = 0; r < n; r++) {
+            uint64_t off = 0;
+            for (uint32_t q = 0; q < d; q++) off += sc[r][q];
+            memcpy(recv + row * TILE_WORDS, send[r] + off * TILE_WORDS, rcnt[r] * TILE_WORDS * 4);
+            row += rcnt[r];
+        }
+        rc = tsdf_border_merge_device(ctxs[d], recv, rcnt, n);
+        if (rc && d) snprintf(ctxs[0]->err, sizeof ctxs[0]->err, "%s", ctxs[d]->err);
+        free(recv);
+        moved += total;
+    }
+    for (uint32_t k = 0; k < n; k++) {
+        const int crc = tsdf_border_commit_device(ctxs[k], rc == TSDF_OK);
+        if (crc && rc == TSDF_OK) rc = crc;
+        free(send[k]);
+    }
+    free(all);
+    if (rc == TSDF_OK && bricks_moved) *bricks_moved = moved;
+    return rc;
+}
+
+/* ---- mesh halo (the GPU library's tsdf_halo_* on host buffers) ---------------------------- */
+
+int tsdf_halo_keys_device(tsdf_ctx* c, uint64_t* keys, uint64_t cap, uint64_t* n_out) {
+    if (!c || !n_out) return TSDF_EINVAL;
+    uint64_t nb = 0;
+    brick_ent* e = list_bricks(c, &nb);
+    if (!e) return TSDF_ENOMEM;
+    uint64_t* have = (uint64_t*)malloc((nb ? nb : 1) * sizeof(uint64_t));
+    uint64_t* need = (uint64_t*)malloc((nb ? 7 * nb : 1) * sizeof(uint64_t));
+    if (!have || !need) { free(e); free(have); free(need); return TSDF_ENOMEM; }
+    for (uint64_t i = 0; i < nb; i++) have[i] = pack_key(e[i].b);
+    qsort(have, nb, sizeof(uint64_t), cmp_u64);
+    uint64_t m = 0;
+    for (uint64_t i = 0; i < nb; i++)
+        for (int d = 1; d < 8; d++) {
+            const int32_t q[3] = {e[i].b[0] + (d & 1), e[i].b[1] + ((d >> 1) & 1), e[i].b[2] + (d >> 2)};
+            if (q[0] >= (1 << 20) || q[1] >= (1 << 20) || q[2] >= (1 << 20)) continue;
+            const uint64_t k = pack_key(q);
+            if (!bsearch(&k, have, nb, sizeof(uint64_t), cmp_u64)) need[m++] = k;
+        }
+    qsort(need, m, sizeof(uint64_t), cmp_u64);
+    uint64_t u = 0;
+    for (uint64_t i = 0; i < m; i++)
+        if (u == 0 || need[u - 1] != need[i]) need[u++] = need[i];
+    *n_out = u;
+    int rc = TSDF_OK;
+    if (u > cap) rc = set_err(c, TSDF_EOVERFLOW, "halo key buffer too small");
+    else if (u && !keys) rc = set_err(c, TSDF_EINVAL, "null key buffer");
+    else if (u) memcpy(keys, need, u * sizeof(uint64_t));
+    free(e); free(have); free(need);
+    return rc;
+}
+
+/* tiles of the requested bricks observed here, in request order */
+int tsdf_halo_pack_device(tsdf_ctx* c, const uint64_t* req, uint64_t n_req, uint32_t* send,
+                          uint64_t cap_rows, uint64_t* n_rows) {
+    if (!c || !n_rows) return TSDF_EINVAL;
+    *n_rows = 0;
+    if (!n_req) return TSDF_OK;
+    if (!req || !send) return set_err(c, TSDF_EINVAL, "null buffer");
+    uint64_t row = 0;
+    for (uint64_t i = 0; i < n_req; i++) {
+        if (req[i] == ~0ull) continue;
+        int32_t b[3];
+        key_brick(req[i], b);
+        if (!brick_observed(c, b)) continue;
+        if (row < cap_rows) {
+            uint32_t* t = send + row * TILE_WORDS;
+            for (int l = 0; l < 512; l++) {
+                const vox_t* v = vox_find(c, b[0] * 8 + (l & 7), b[1] * 8 + ((l >> 3) & 7), b[2] * 8 + (l >> 6));
+                ((float*)t)[l] = v ? v->S : c->bg;
+                ((float*)t)[512 + l] = v ? v->W : 0.0f;
+            }
+            t[1024] = (uint32_t)req[i]; t[1025] = (uint32_t)(req[i] >> 32); t[1026] = 0; t[1027] = 0;
+        }
+        row++;
+    }
+    *n_rows = row;
+    return row > cap_rows ? set_err(c, TSDF_EOVERFLOW, "halo send buffer too small") : TSDF_OK;
 }
 
 /* ---- marching cubes (mesh extraction over the field) --------------------
@@ -1534,16 +1793,53 @@ int tsdf_extract_mesh(tsdf_ctx* c, float min_weight, float* tri, uint64_t cap, u
     return tsdf_extract_mesh_table(c, min_weight, TSDF_MC_GENERATED, tri, cap, n_tri);
 }
 
-int tsdf_extract_mesh_table(tsdf_ctx* c, float min_weight, int32_t table, float* tri,
-                            uint64_t cap, uint64_t* n_tri) {
+/* halo tiles (ABI v9) sorted by key for the corner lookups of mesh_impl */
+typedef struct { uint64_t key; const uint32_t* tile; } halo_ent;
+
+static int cmp_halo(const void* a, const void* b) {
+    const uint64_t x = ((const halo_ent*)a)->key, y = ((const halo_ent*)b)->key;
+    return x < y ? -1 : (x > y);
+}
+
+/* voxel (x, y, z): from its brick's halo tile when there is one, else the context's own voxel */
+static int corner(const tsdf_ctx* c, const halo_ent* h, uint64_t nh, int32_t x, int32_t y, int32_t z,
+                  float* S, float* W) {
+    if (nh) {
+        const int32_t b[3] = {fdiv8(x), fdiv8(y), fdiv8(z)};
+        const halo_ent q = {pack_key(b), NULL};
+        const halo_ent* f = (const halo_ent*)bsearch(&q, h, nh, sizeof(halo_ent), cmp_halo);
+        if (f) {
+            const int l = ((z - 8 * b[2]) << 6) | ((y - 8 * b[1]) << 3) | (x - 8 * b[0]);
+            *S = ((const float*)f->tile)[l];
+            *W = ((const float*)f->tile)[512 + l];
+            return 1;
+        }
+    }
+    const vox_t* v = vox_find(c, x, y, z);
+    if (!v) return 0;
+    *S = v->S;
+    *W = v->W;
+    return 1;
+}
+
+static int mesh_impl(tsdf_ctx* c, float min_weight, int32_t table, const uint32_t* halo,
+                     uint64_t n_halo, float* tri, uint64_t cap, uint64_t* n_tri) {
     if (!c || !n_tri) return TSDF_EINVAL;
     if (table < 0 || table >= TSDF_MC_TABLES)
         return set_err(c, TSDF_EINVAL, "unknown marching-cubes table");
+    if (n_halo && !halo) return set_err(c, TSDF_EINVAL, "null halo tiles");
     if (!mc_ready) mc_build();
     const uint8_t(*mc_tab)[32] = mc_tabs[table];
+    halo_ent* h = (halo_ent*)malloc((n_halo ? n_halo : 1) * sizeof(halo_ent));
+    if (!h) return TSDF_ENOMEM;
+    for (uint64_t i = 0; i < n_halo; i++) {
+        h[i].tile = halo + i * TILE_WORDS;
+        h[i].key = (uint64_t)h[i].tile[1024] | ((uint64_t)h[i].tile[1025] << 32);
+    }
+    qsort(h, n_halo, sizeof(halo_ent), cmp_halo);
     uint64_t nb = 0;
     brick_ent* e = list_bricks(c, &nb);
-    if (!e) return TSDF_ENOMEM;
+    if (!e) { free(h); return TSDF_ENOMEM; }
     const float vs = c->vs;
     uint64_t nt = 0;
     for (uint64_t b = 0; b < nb; b++) {
@@ -1553,10 +1849,11 @@ int tsdf_extract_mesh_table(tsdf_ctx* c, float min_weight, int32_t table, float*
             float S[8];
             int ok = 1, k = 0;
             for (int q = 0; q < 8 && ok; q++) {
-                const vox_t* v = vox_find(c, x + (q & 1), y + ((q >> 1) & 1), z + ((q >> 2) & 1));
-                if (!v || !(v->W > 0.0f) || !(v->W >= min_weight)) { ok = 0; break; }
-                S[q] = v->S;
-                if (v->S < 0.0f) k |= 1 << q;
+                float sv = 0.0f, wv = 0.0f;
+                if (!corner(c, h, n_halo, x + (q & 1), y + ((q >> 1) & 1), z + ((q >> 2) & 1), &sv, &wv) ||
+                    !(wv > 0.0f) || !(wv >= min_weight)) { ok = 0; break; }
+                S[q] = sv;
+                if (sv < 0.0f) k |= 1 << q;
             }
             if (!ok) continue;
             const int ntc = mc_tab[k][0];
@@ -1581,6 +1878,58 @@ int tsdf_extract_mesh_table(tsdf_ctx* c, float min_weight, int32_t table, float*
         }
     }
     free(e);
+    free(h);
     *n_tri = nt;
     return (tri && nt > cap) ? TSDF_EOVERFLOW : TSDF_OK;  /* tri == NULL: count only */
+}
+
+int tsdf_extract_mesh_table(tsdf_ctx* c, float min_weight, int32_t table, float* tri,
+                            uint64_t cap, uint64_t* n_tri) {
+    return mesh_impl(c, min_weight, table, NULL, 0, tri, cap, n_tri);
+}
+
+int tsdf_extract_mesh_halo(tsdf_ctx* c, float min_weight, int32_t table, const uint32_t* halo,
+                           uint64_t n_halo, float* tri, uint64_t cap, uint64_t* n_tri) {
+    return mesh_impl(c, min_weight, table, halo, n_halo, tri, cap, n_tri);
+}
+
+/* the GPU library's tsdf_extract_mesh_local: reduce, halo exchange, one mesh per context,
+ * soups concatenated in context order */
+int tsdf_extract_mesh_local(tsdf_ctx* const* ctxs, uint32_t n, float min_weight, int32_t table,
+                            float* tri, uint64_t cap, uint64_t* n_tri) {
+    if (!ctxs || n == 0 || n > TSDF_MAX_WORLD || !n_tri) return TSDF_EINVAL;
+    for (uint32_t k = 0; k < n; k++)
+        if (!ctxs[k]) return TSDF_EINVAL;
+    *n_tri = 0;
+    if (n == 1) return tsdf_extract_mesh_table(ctxs[0], min_weight, table, tri, cap, n_tri);
+    int rc = tsdf_border_reduce_local(ctxs, n, NULL);
+    uint64_t total = 0;
+    for (uint32_t k = 0; k < n && rc == TSDF_OK; k++) {
+        uint64_t nr = 0;
+        rc = tsdf_halo_keys_device(ctxs[k], NULL, 0, &nr);
+        if (rc == TSDF_EOVERFLOW) rc = TSDF_OK;
+        uint64_t* req = (uint64_t*)malloc((nr ? nr : 1) * sizeof(uint64_t));
+        uint32_t* halo = (uint32_t*)malloc((nr ? nr : 1) * TILE_WORDS * 4);
+        if (!req || !halo) rc = TSDF_ENOMEM;
+        uint64_t got = 0, nh = 0;
+        if (rc == TSDF_OK) rc = tsdf_halo_keys_device(ctxs[k], req, nr, &got);
+        for (uint32_t j = 0; j < n && rc == TSDF_OK; j++) {
+            if (j == k) continue;
+            uint64_t rows = 0;
+            rc = tsdf_halo_pack_device(ctxs[j], req, nr, halo + nh * TILE_WORDS, nr - nh, &rows);
+            nh += rows;
+        }
+        uint64_t nt = 0;
+        if (rc == TSDF_OK) {
+            rc = mesh_impl(ctxs[k], min_weight, table, halo, nh, tri && total <= cap ? tri + 9 * total : NULL,
+                           tri && total <= cap ? cap - total : 0, &nt);
+            if (rc == TSDF_EOVERFLOW) rc = TSDF_OK;
+        }
+        total += nt;
+        free(req);
+        free(halo);
+    }
+    *n_tri = total;
+    if (rc == TSDF_OK && tri && total > cap) rc = set_err(ctxs[0], TSDF_EOVERFLOW, "mesh buffer too small");
+    return rc;
 }

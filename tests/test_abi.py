@@ -37,7 +37,7 @@ def test_hip_library_exports_every_declared_symbol():
     missing = [f for f in header_functions() if f not in syms]
     assert not missing, missing
     lib = load_hip_library()
-    assert lib.tsdf_abi_version() == 8
+    assert lib.tsdf_abi_version() == 9
 
 
 def test_hip_library_is_gfx950_code():

@@ -73,3 +73,111 @@ def test_sector_sharded_merge_gloo(world, tmp_path):
     assert np.array_equal(mw, rw)
     assert np.max(np.abs(ms - rs)) <= 1e-5
     assert np.mean(ms.view(np.uint32) == rs.view(np.uint32)) > 0.5
+
+
+def _fault_worker(rank, world, port, out_dir, fault_rank, step):
+    import sys
+    for p in (os.path.join(REPO, "noetic-slam_amd"), os.path.join(REPO, "oracle")):
+        sys.path.insert(0, p)
+    import torch.distributed as dist
+    import oracle
+    from tsdf_map.distributed import BorderReduceAborted, border_reduce
+    from tsdf_map.scan_gen import OusterSim
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sim = OusterSim()
+    vol = oracle.OracleTSDFVolume(0.05, 0.15, n_sectors=world, sector=rank, sector_yaw0=0.3)
+    for k in (0, 3):
+        pts, org = sim.scan(k)
+        vol.integrate(np.ascontiguousarray(pts[::8]), org)
+    before = vol.export_voxels()
+    outcome = "ok"
+    try:
+        border_reduce(vol, _fault=step if rank == fault_rank else None)
+    except BorderReduceAborted:
+        outcome = "aborted"
+    except RuntimeError as e:
+        outcome = "fault" if "injected" in str(e) else "error: %s" % e
+    after = vol.export_voxels()
+    same = all(np.array_equal(a.view(np.uint32) if a.dtype == np.float32 else a,
+                              b.view(np.uint32) if b.dtype == np.float32 else b)
+               for a, b in zip(before, after))
+    # the context takes scans again after the roll-back, and a clean reduce still works
+    pts, org = sim.scan(6)
+    vol.integrate(np.ascontiguousarray(pts[::8]), org)
+    border_reduce(vol)
+    with open(os.path.join(out_dir, "rank%d.txt" % rank), "w") as f:
+        f.write("%s %d %d" % (outcome, int(same), before[0].shape[0]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,step", [(2, "merge"), (3, "merge"), (3, "pack"), (2, "keys")])
+def test_border_reduce_failure_leaves_fields_unchanged(world, step, tmp_path):
+    """a rank failing between pack and merge (or earlier) makes every rank roll back:
+    the faulty rank raises its error, the others BorderReduceAborted, and every rank's field is bit
+    for bit the one before the reduce (no mass lost at the sources, none double-counted at the
+    owners); the contexts take scans and reduce again afterwards."""
+    fault_rank = world - 1
+    mp.start_processes(_fault_worker, args=(world, _free_port(), str(tmp_path), fault_rank, step),
+                       nprocs=world, join=True, start_method="spawn")
+    for r in range(world):
+        outcome, same, nvox = (tmp_path / ("rank%d.txt" % r)).read_text().split()
+        assert outcome == ("fault" if r == fault_rank else "aborted"), (r, outcome)
+        assert same == "1", r
+        assert int(nvox) > 1000
+
+
+def _mesh_worker(rank, world, port, out_dir):
+    import sys
+    for p in (os.path.join(REPO, "noetic-slam_amd"), os.path.join(REPO, "oracle")):
+        sys.path.insert(0, p)
+    import torch.distributed as dist
+    import oracle
+    from tsdf_map.distributed import mesh
+    from tsdf_map.scan_gen import OusterSim
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sim = OusterSim()
+    vol = oracle.OracleTSDFVolume(0.05, 0.15, n_sectors=world, sector=rank, sector_yaw0=0.3)
+    for k in (0, 3):
+        pts, org = sim.scan(k)
+        vol.integrate(np.ascontiguousarray(pts[::4]), org)
+    out = {}
+    for table in ("generated", "lorensen"):
+        v, _ = mesh(vol, table=table, reduce=table == "generated")
+        out[table] = v
+    c, s, w = vol.export_bricks()
+    np.savez(os.path.join(out_dir, "rank%d.npz" % rank), coords=c, sdf=s, weight=w, **out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def tri_set(v):
+    """A triangle soup as a sorted array of its triangles (9 floats each, as raw bits)."""
+    t = np.ascontiguousarray(v, np.float32).reshape(-1, 9).view(np.uint32)
+    return t[np.lexsort(t.T[::-1])]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_mesh_gloo(world, tmp_path):
+    """VERDICT r4 #3 on CPU: after the border reduce each rank meshes its own cubes with a one-brick
+    halo exchanged over the collective; the union of the ranks' soups is, triangle for triangle,
+    the mesh of the union field, for both case tables."""
+    mp.start_processes(_mesh_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+                       join=True, start_method="spawn")
+    import oracle
+    parts = [np.load(str(tmp_path / ("rank%d.npz" % r))) for r in range(world)]
+    union = oracle.OracleTSDFVolume(0.05, 0.15)
+    for p in parts:
+        keep = (p["weight"].reshape(len(p["coords"]), -1) > 0).any(1)
+        union.import_bricks(p["coords"][keep], p["sdf"][keep], p["weight"][keep])
+    for table in ("generated", "lorensen"):
+        got = tri_set(np.concatenate([p[table] for p in parts]))
+        want = tri_set(union.extract_triangle_mesh(table=table)[0])
+        assert got.shape[0] > 1000
+        assert np.array_equal(got, want), table

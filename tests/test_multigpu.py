@@ -88,6 +88,8 @@ def emulated_reduce(vols, dev):
                                                                           device=dev)
         torch.cuda.synchronize()
         v.border_merge(recv.data_ptr(), rc)
+    for v in vols:  # every rank merged: commit (ABI v9)
+        v.border_commit(True)
     return splits
 
 
@@ -114,6 +116,8 @@ def emulated_reduce_host(vols):
             rc.append(splits[r][d])
         recv = np.ascontiguousarray(np.concatenate(parts)) if sum(rc) else np.empty((1, TILE), np.int32)
         v.border_merge(recv.ctypes.data, rc)
+    for v in vols:  # every rank merged: commit (ABI v9)
+        v.border_commit(True)
     return splits
 
 
@@ -204,7 +208,10 @@ def _worker(rank, world, port, out_dir):
     for k in (0, 3):
         vol.integrate(*sim.scan(k))
     c, s, w = merged_bricks(vol, device="cpu")
-    np.savez(os.path.join(out_dir, "rank%d.npz" % rank), coords=c, sdf=s, weight=w)
+    # the sharded mesh over the collective (halo tiles through host memory here; RCCL on a node)
+    from tsdf_map.distributed import mesh
+    mv, _ = mesh(vol, comm_device="cpu", reduce=False)
+    np.savez(os.path.join(out_dir, "rank%d.npz" % rank), coords=c, sdf=s, weight=w, mesh=mv)
     dist.barrier()
     dist.destroy_process_group()
 
@@ -226,6 +233,83 @@ def test_border_reduce_two_processes(tmp_path, sim):
     ri, rs, rw = ref.export_voxels()
     assert np.array_equal(mi, ri) and np.array_equal(mw, rw)
     assert np.max(np.abs(ms - rs)) <= 1e-5
+    # the ranks' meshes together: the mesh of the union field, triangle for triangle
+    from test_distributed import tri_set
+    union = ora()
+    for p in parts:
+        union.import_bricks(p["coords"], p["sdf"], p["weight"])
+    got = tri_set(np.concatenate([p["mesh"] for p in parts]))
+    assert got.shape[0] > 1000
+    assert np.array_equal(got, tri_set(union.extract_triangle_mesh()[0]))
+
+
+def test_border_abort_restores_bitwise(sim):
+    """ABI v9 on the GPU: pack, merge, then abort (tsdf_border_commit_device(0)) -- the snapshot
+    kernels write the merged bricks back and the sent bricks never lost their mass: every
+    context's field is the one before, bit for bit; integration is refused while the reduce is
+    open and accepted after."""
+    world, yaw0 = 3, 0.25
+    dev = torch.device("cuda", 0)
+    g = [hip(n_sectors=world, sector=r, sector_yaw0=yaw0) for r in range(world)]
+    for k in (0, 1):
+        pts, org = sim.scan(k)
+        for v in g:
+            v.integrate(np.ascontiguousarray(pts[::2]), org)
+    before = [v.export_voxels() for v in g]
+    keys, counts = [], []
+    for v in g:
+        k = torch.empty(max(v.num_bricks(), 1), dtype=torch.int64, device=dev)
+        torch.cuda.synchronize()
+        counts.append(v.brick_keys_into(k.data_ptr(), k.numel()))
+        keys.append(k)
+    stride = max(counts)
+    allk = torch.full((world, stride), -1, dtype=torch.int64, device=dev)
+    for r in range(world):
+        allk[r, :counts[r]] = keys[r][:counts[r]]
+    sends, splits = [], []
+    for r, v in enumerate(g):
+        s_ = torch.empty((max(counts[r], 1), TILE), dtype=torch.int32, device=dev)
+        torch.cuda.synchronize()
+        splits.append(v.border_pack(allk.data_ptr(), counts, stride, world, r, s_.data_ptr(),
+                                    s_.shape[0]))
+        sends.append(s_)
+    assert sum(map(sum, splits)) > 100
+    for d, v in enumerate(g):
+        parts = [sends[r][sum(splits[r][:d]):sum(splits[r][:d]) + splits[r][d]] for r in range(world)]
+        rc = [splits[r][d] for r in range(world)]
+        recv = torch.cat(parts).contiguous() if sum(rc) else torch.empty((1, TILE), dtype=torch.int32,
+                                                                          device=dev)
+        torch.cuda.synchronize()
+        v.border_merge(recv.data_ptr(), rc)
+    pts, org = sim.scan(3)
+    with pytest.raises(Exception, match="border reduce is open"):
+        g[0].integrate(np.ascontiguousarray(pts[::2]), org)
+    assert not voxels_equal_bitwise(g[0].export_voxels(), before[0])  # the owner merged
+    for v in g:
+        v.border_commit(False)
+    for v, b in zip(g, before):
+        assert voxels_equal_bitwise(v.export_voxels(), b)
+    g[0].integrate(np.ascontiguousarray(pts[::2]), org)
+
+
+def test_sectors_bare_origin_voxblox_depth_weight(sim):
+    """integrate_sectors with a bare (3,) origin takes
+    tsdf_integrate_sectors_origin -- no orientation, so Voxblox's constant weight, exactly what
+    integrate(points, origin) gives -- bit for bit against the oracle's sector volumes."""
+    from tsdf_map import integrate_sectors
+    n, yaw0 = 3, 0.5
+    kw = dict(semantics="voxblox", use_const_weight=False, max_range=100.0)
+    g = [hip(n_sectors=n, sector=r, sector_yaw0=yaw0, max_batch=2, **kw) for r in range(n)]
+    o = [ora(n_sectors=n, sector=r, sector_yaw0=yaw0, **kw) for r in range(n)]
+    for k in (0, 4):
+        pts, org = sim.scan(k)
+        pts = np.ascontiguousarray(pts[::2])
+        integrate_sectors(g, pts, org)
+        for v in o:
+            v.integrate(pts, org)
+    for r in range(n):
+        g[r].sync()
+        assert voxels_equal_bitwise(g[r].export_voxels(), o[r].export_voxels()), r
 
 
 @pytest.mark.parametrize("n,f64,mode", [(3, False, "split"), (4, True, "split"),
