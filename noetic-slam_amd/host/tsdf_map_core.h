@@ -98,6 +98,9 @@ class PoseTrack {
 };
 
 // The node's per-scan slot: clouds paired with the pose track, integrated through the C-ABI.
+// One context, or N azimuth-sector contexts of tsdf_create_sharded (the node's ~num_gpus): each
+// cloud then goes to all of them through tsdf_integrate_sectors (packed once, fanned out GPU to
+// GPU; every context keeps its sector's rays).
 class MapCore {
    public:
     struct Counts {
@@ -105,7 +108,9 @@ class MapCore {
     };
 
     MapCore(tsdf_ctx* ctx, double max_gap_ms = 50.0, size_t max_pending = 16)
-        : ctx_(ctx), max_gap_ms_(max_gap_ms), max_pending_(max_pending) {}
+        : ctxs_(1, ctx), max_gap_ms_(max_gap_ms), max_pending_(max_pending) {}
+    MapCore(std::vector<tsdf_ctx*> ctxs, double max_gap_ms = 50.0, size_t max_pending = 16)
+        : ctxs_(std::move(ctxs)), max_gap_ms_(max_gap_ms), max_pending_(max_pending) {}
 
     // A pose sample (PoseStamped / Odometry / a Path entry); releases the clouds it covers.
     int on_pose(const Pose& s) {
@@ -163,7 +168,11 @@ class MapCore {
                 pending_.pop_front();
                 continue;
             }
-            const int rc = tsdf_integrate_pose(ctx_, c.data, c.n, c.step, c.xoff, c.f64, pose);
+            const int rc =
+                ctxs_.size() == 1
+                    ? tsdf_integrate_pose(ctxs_[0], c.data, c.n, c.step, c.xoff, c.f64, pose)
+                    : tsdf_integrate_sectors(ctxs_.data(), (uint32_t)ctxs_.size(), c.data, c.n,
+                                             c.step, c.xoff, c.f64, pose);
             pending_.pop_front();
             if (rc != TSDF_OK) return rc;
             counts_.integrated++;
@@ -171,7 +180,7 @@ class MapCore {
         return TSDF_OK;
     }
 
-    tsdf_ctx* ctx_;
+    std::vector<tsdf_ctx*> ctxs_;
     double max_gap_ms_;
     size_t max_pending_;
     PoseTrack track_;

@@ -17,7 +17,17 @@
 //
 // On shutdown the map is written like dliomapping's destructor writes its PLY (dliomapping.cpp:53-61):
 // ~map_path (bricks: u64 n, i32 coords[3 n], f32 sdf[512 n], f32 weight[512 n]) and, with
-// ~mesh_path set, a binary PLY triangle soup from tsdf_extract_mesh.
+// ~mesh_path set, a binary PLY triangle soup from tsdf_extract_mesh_table with ~mesh_table
+// ("lorensen", the default: the published Lorensen / Bourke table VDBFusion's and voxblox's
+// marching cubes compile in; "generated": this library's face-consistent table).
+//
+// Several GPUs (north_star: "scans shard by azimuth sector across up to 8 GPUs"; SURVEY §5's
+// ~num_gpus): ~num_gpus = N > 1 creates N sector contexts with tsdf_create_sharded on ~device_ids
+// ("0,1,2,3"; default 0 .. N-1) from ~sector_yaw0, each cloud goes to all of them through
+// tsdf_integrate_sectors (packed once, one H2D copy, xGMI copies to the others, each GPU keeps its
+// azimuth sector), and before the map or mesh is written tsdf_border_reduce_local moves every border
+// brick's mass to one owner; the map file then holds every observed brick once and the mesh is
+// tsdf_extract_mesh_local's (a one-brick halo exchanged between the GPUs, each cube meshed once).
 #include <geometry_msgs/PoseStamped.h>
 #include <nav_msgs/Path.h>
 #include <ros/ros.h>
@@ -25,7 +35,9 @@
 #include <sensor_msgs/PointField.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <memory>
+#include <sstream>
 #include <string>
 #include <vector>
 
@@ -104,20 +116,61 @@ class TsdfMapNode {
             ros::shutdown();
             return;
         }
-        if (tsdf_create(&p, &ctx_) != TSDF_OK) {
-            ROS_FATAL("tsdf_create failed (see stderr)");
+        // ~num_gpus sector contexts (one per GPU of ~device_ids), or one context on ~device_id
+        int num_gpus = 1;
+        pnh.param("num_gpus", num_gpus, num_gpus);
+        std::string ids;
+        pnh.param<std::string>("device_ids", ids, "");
+        pnh.param("sector_yaw0", p.sector_yaw0, 0.0);
+        if (num_gpus < 1 || num_gpus > TSDF_MAX_WORLD) {
+            ROS_FATAL("num_gpus must be 1 .. %d", TSDF_MAX_WORLD);
             ros::shutdown();
             return;
         }
+        std::vector<int32_t> dev_ids;
+        {
+            std::stringstream ss(ids);
+            std::string tok;
+            while (std::getline(ss, tok, ',')) dev_ids.push_back((int32_t)std::atoi(tok.c_str()));
+        }
+        if (dev_ids.empty())
+            for (int k = 0; k < num_gpus; k++) dev_ids.push_back(num_gpus == 1 ? device : k);
+        if ((int)dev_ids.size() != num_gpus) {
+            ROS_FATAL("device_ids lists %zu devices for num_gpus %d", dev_ids.size(), num_gpus);
+            ros::shutdown();
+            return;
+        }
+        ctxs_.assign((size_t)num_gpus, nullptr);
+        const int crc = num_gpus == 1
+                            ? (p.device_id = dev_ids[0], tsdf_create(&p, &ctxs_[0]))
+                            : tsdf_create_sharded(&p, (uint32_t)num_gpus, dev_ids.data(), ctxs_.data());
+        if (crc != TSDF_OK) {
+            ROS_FATAL("tsdf_create%s failed (see stderr)", num_gpus > 1 ? "_sharded" : "");
+            ctxs_.clear();
+            ros::shutdown();
+            return;
+        }
+        ctx_ = ctxs_[0];
         double max_gap_ms = 50.0;
         pnh.param("max_pose_gap_ms", max_gap_ms, max_gap_ms);
-        core_ = new tsdf_map::MapCore(ctx_, max_gap_ms);
+        core_ = new tsdf_map::MapCore(ctxs_, max_gap_ms);
         std::string metrics;
         pnh.param<std::string>("metrics_log", metrics, "");
         if (!metrics.empty() && tsdf_set_metrics_log(ctx_, metrics.c_str()) != TSDF_OK)
             ROS_WARN("metrics log: %s", tsdf_last_error(ctx_));
         pnh.param<std::string>("map_path", map_path_, "tsdf_map.bricks");
         pnh.param<std::string>("mesh_path", mesh_path_, "");
+        std::string table;
+        pnh.param<std::string>("mesh_table", table, "lorensen");
+        if (table == "lorensen") {
+            mesh_table_ = TSDF_MC_LORENSEN;
+        } else if (table == "generated") {
+            mesh_table_ = TSDF_MC_GENERATED;
+        } else {
+            ROS_FATAL("unknown mesh_table '%s' (lorensen, generated)", table.c_str());
+            ros::shutdown();
+            return;
+        }
         std::string cloud_topic, pose_topic, path_topic;
         pnh.param<std::string>("cloud_topic", cloud_topic, "robot/dlio/odom_node/pointcloud/deskewed");
         pnh.param<std::string>("pose_topic", pose_topic, "robot/dlio/odom_node/pose");
@@ -132,7 +185,7 @@ class TsdfMapNode {
         core_->flush();
         save();
         delete core_;
-        tsdf_destroy(ctx_);
+        for (tsdf_ctx* c : ctxs_) tsdf_destroy(c);
     }
 
     void on_pose(const geometry_msgs::PoseStampedConstPtr& m) {
@@ -174,26 +227,52 @@ class TsdfMapNode {
     }
 
     void save() {
-        uint64_t nb = 0;
-        if (tsdf_num_bricks(ctx_, &nb) != TSDF_OK) return;
-        std::vector<int32_t> c(3 * nb);
-        std::vector<float> s(512 * nb), w(512 * nb);
-        uint64_t got = 0;
-        if (tsdf_export_bricks(ctx_, c.data(), s.data(), w.data(), nb, &got) == TSDF_OK) {
-            if (FILE* f = std::fopen(map_path_.c_str(), "wb")) {
-                std::fwrite(&got, 8, 1, f);
-                std::fwrite(c.data(), 4, 3 * got, f);
-                std::fwrite(s.data(), 4, 512 * got, f);
-                std::fwrite(w.data(), 4, 512 * got, f);
-                std::fclose(f);
-                ROS_INFO("saved %llu bricks to %s", (unsigned long long)got, map_path_.c_str());
+        const uint32_t n = (uint32_t)ctxs_.size();
+        // several GPUs: every border brick's mass to one owner first, so each observed brick is
+        // written once (the other contexts hold it reset, W = 0, and are skipped below)
+        if (n > 1) {
+            uint64_t moved = 0;
+            if (tsdf_border_reduce_local(ctxs_.data(), n, &moved) != TSDF_OK) {
+                ROS_ERROR("tsdf border reduce: %s", tsdf_last_error(ctx_));
+                return;
+            }
+            ROS_INFO("border reduce: %llu bricks moved", (unsigned long long)moved);
+        }
+        std::vector<int32_t> c;
+        std::vector<float> s, w;
+        for (tsdf_ctx* k : ctxs_) {
+            uint64_t nb = 0, got = 0;
+            if (tsdf_num_bricks(k, &nb) != TSDF_OK) return;
+            std::vector<int32_t> ck(3 * nb);
+            std::vector<float> sk(512 * nb), wk(512 * nb);
+            if (tsdf_export_bricks(k, ck.data(), sk.data(), wk.data(), nb, &got) != TSDF_OK) return;
+            for (uint64_t b = 0; b < got; b++) {
+                bool obs = false;
+                for (int l = 0; l < 512 && !obs; l++) obs = wk[512 * b + l] > 0.0f;
+                if (n > 1 && !obs) continue;
+                c.insert(c.end(), ck.begin() + 3 * b, ck.begin() + 3 * b + 3);
+                s.insert(s.end(), sk.begin() + 512 * b, sk.begin() + 512 * b + 512);
+                w.insert(w.end(), wk.begin() + 512 * b, wk.begin() + 512 * b + 512);
             }
         }
+        const uint64_t got = c.size() / 3;
+        if (FILE* f = std::fopen(map_path_.c_str(), "wb")) {
+            std::fwrite(&got, 8, 1, f);
+            std::fwrite(c.data(), 4, 3 * got, f);
+            std::fwrite(s.data(), 4, 512 * got, f);
+            std::fwrite(w.data(), 4, 512 * got, f);
+            std::fclose(f);
+            ROS_INFO("saved %llu bricks to %s", (unsigned long long)got, map_path_.c_str());
+        }
         if (mesh_path_.empty()) return;
+        auto mesh = [&](float* tri, uint64_t cap, uint64_t* nt) {
+            return n > 1 ? tsdf_extract_mesh_local(ctxs_.data(), n, 0.0f, mesh_table_, tri, cap, nt)
+                         : tsdf_extract_mesh_table(ctx_, 0.0f, mesh_table_, tri, cap, nt);
+        };
         uint64_t nt = 0;
-        if (tsdf_extract_mesh(ctx_, 0.0f, nullptr, 0, &nt) != TSDF_OK) return;
+        if (mesh(nullptr, 0, &nt) != TSDF_OK) return;
         std::vector<float> tri(9 * nt);
-        if (tsdf_extract_mesh(ctx_, 0.0f, tri.data(), nt, &nt) != TSDF_OK) return;
+        if (mesh(tri.data(), nt, &nt) != TSDF_OK) return;
         if (FILE* f = std::fopen(mesh_path_.c_str(), "wb")) {  // binary PLY triangle soup
             std::fprintf(f,
                          "ply\nformat binary_little_endian 1.0\nelement vertex %llu\n"
@@ -212,7 +291,9 @@ class TsdfMapNode {
         }
     }
 
-    tsdf_ctx* ctx_ = nullptr;
+    tsdf_ctx* ctx_ = nullptr;            // ctxs_[0]: errors, metrics
+    std::vector<tsdf_ctx*> ctxs_;        // one per GPU (sector k of num_gpus)
+    int32_t mesh_table_ = TSDF_MC_LORENSEN;
     tsdf_map::MapCore* core_ = nullptr;
     ros::Subscriber sub_cloud_, sub_pose_, sub_path_;
     std::string map_path_, mesh_path_;
@@ -224,6 +305,6 @@ int main(int argc, char** argv) {
     ros::init(argc, argv, "tsdf_map_node");
     ros::NodeHandle nh, pnh("~");
     TsdfMapNode node(nh, pnh);
-    ros::spin();  // single-threaded: one context, one thread (include/tsdf_hip.h)
+    ros::spin();  // single-threaded: the contexts are used by this one thread (include/tsdf_hip.h)
     return 0;
 }

@@ -274,3 +274,27 @@ def test_import_merges_as_weighted_mean(scan0):
     i2, s2, w2 = ref.export_voxels()
     assert np.array_equal(i1, i2) and np.array_equal(w1, w2)
     assert np.max(np.abs(s1 - s2)) <= 1e-6
+
+
+@pytest.mark.parametrize("semantics", ["vdbfusion_f64", "vdbfusion"])
+@pytest.mark.parametrize("origin", [(3.1, -7.3, 0.7), (2.0, -1.5, 0.25)])
+def test_zero_range_point_is_origin_ray(semantics, origin):
+    """an Ouster r = 0 pixel becomes the sensor origin rounded to float
+    (cartesian.h:64-65 after the pose).  fp32 restatement: that point minus (float)origin is zero,
+    the ray has no length and is dropped.  VDBFusion at its precisions: the point minus the DOUBLE
+    origin is a rounding error, unless the origin is a float, so a non-float origin keeps a
+    micrometre ray whose band surrounds the origin (as upstream's Integrate would); DLIO's crop box
+    (min_range 1 m) drops it in both modes."""
+    o = np.array(origin, np.float64)
+    p = o.astype(np.float32).reshape(1, 3)
+    exact = bool(np.all(p[0].astype(np.float64) == o))
+    for min_range, keep in ((0.0, semantics == "vdbfusion_f64" and not exact), (1.0, False)):
+        v = vol(semantics=semantics, min_range=min_range)
+        v.integrate(p, o)
+        assert v.stats()["n_rays_total"] == (1 if keep else 0), (min_range, exact)
+        ijk, s, w = v.export_voxels()
+        if keep:  # the band of a ray of ~0 length: voxels around the origin, all within tau
+            c = (ijk.astype(np.float64) + 0.5) * VS
+            assert len(ijk) > 0 and np.all(np.linalg.norm(c - o, axis=1) <= TAU + VS)
+        else:
+            assert len(ijk) == 0

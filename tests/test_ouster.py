@@ -15,6 +15,7 @@ import os
 import numpy as np
 import pytest
 
+import oracle
 import ouster_ref as R
 from conftest import GOLDEN
 
@@ -144,10 +145,16 @@ def test_destaggered_cloud_layout_and_order():
 
 
 @pytest.mark.gpu
-def test_gpu_destaggered_48b_cloud_bitwise():
+@pytest.mark.parametrize("semantics,min_range", [("vdbfusion_f64", 1.0), ("vdbfusion_f64", 0.0),
+                                                 ("vdbfusion", 0.0)])
+def test_gpu_destaggered_48b_cloud_bitwise(semantics, min_range):
     """An organized 48-B cloud of the pinned OS-2-128 frame (destaggered, world frame) integrates
     through tsdf_integrate(point_step 48) to the same field, bit for bit, as the staggered packed
-    xyz: the per-scan fuse sums each voxel's samples exactly, so point order does not matter."""
+    xyz: the per-scan fuse sums each voxel's samples exactly, so point order does not matter.
+    In the default mode (vdbfusion_f64) with DLIO's crop box as min_range (odom.cc:114-116: what
+    the node receives) and without it, and in the fp32 restatement.  The r = 0 pixels are the
+    sensor origin rounded to float: test_oracle_kat.py::test_zero_range_point_is_origin_ray pins
+    which modes keep that ray."""
     from tsdf_map import HipTSDFVolume
     from tsdf_map.ouster import destaggered_cloud
     js = [f for f in FIXTURES if "OS-2-128" in f][0]
@@ -162,12 +169,10 @@ def test_gpu_destaggered_48b_cloud_bitwise():
     x = xyz.cpu().numpy()
     cloud = destaggered_cloud(x, ref["RANGE"], ref["SIGNAL"], ref["REFLECTIVITY"], ref["NEAR_IR"],
                               meta["data_format"]["pixel_shift_by_row"])
-    # the fp32 restatement: an r = 0 pixel is the sensor origin to the bit there, so its ray drops
-    # (in vdbfusion_f64 the float point sits a rounding error from the double origin and its
-    # zero-length-ish ray is kept, as upstream would; DLIO's crop box removes it either way)
-    a = HipTSDFVolume(0.05, 0.15, max_points=1 << 18, semantics="vdbfusion")
+    kw = dict(max_points=1 << 18, semantics=semantics, min_range=min_range)
+    a = HipTSDFVolume(0.05, 0.15, **kw)
     a.integrate_cloud(cloud.tobytes(), cloud.shape[0], 48, 0, P[:3, 3])
-    b = HipTSDFVolume(0.05, 0.15, max_points=1 << 18, semantics="vdbfusion")
+    b = HipTSDFVolume(0.05, 0.15, **kw)
     b.integrate(x, P[:3, 3])
     a.sync()
     b.sync()
@@ -176,4 +181,17 @@ def test_gpu_destaggered_48b_cloud_bitwise():
     assert ai.shape[0] > 10000
     assert np.array_equal(ai, bi) and np.array_equal(aw, bw)
     assert np.array_equal(as_.view(np.uint32), bs.view(np.uint32))
-    assert a.stats()["n_rays_total"] == np.count_nonzero(ref["RANGE"])  # r = 0 pixels drop
+    o = oracle.OracleTSDFVolume(0.05, 0.15, semantics=semantics, min_range=min_range)
+    o.integrate(x, P[:3, 3])
+    oi, os_, ow = o.export_voxels()
+    assert np.array_equal(ai, oi) and np.array_equal(aw, ow)
+    assert np.array_equal(as_.view(np.uint32), os_.view(np.uint32))
+    # which rays count: every pixel at least min_range from the origin; an r = 0 pixel (the origin
+    # rounded to float) is dropped by the crop, and kept without it only in the double-precision
+    # mode, where it sits a rounding error from the double origin (the KAT's rule)
+    nz = int(np.count_nonzero(ref["RANGE"]))
+    zero_kept = semantics == "vdbfusion_f64" and min_range == 0.0
+    d = np.linalg.norm(x.astype(np.float64) - P[:3, 3], axis=1).astype(np.float32)
+    far = int(np.count_nonzero(d >= min_range))
+    want = x.shape[0] if zero_kept else (nz if min_range == 0.0 else far)
+    assert a.stats()["n_rays_total"] == b.stats()["n_rays_total"] == want
