@@ -71,6 +71,12 @@ def parse():
                     help="fusion rule (tsdf_params.semantics); the headline is vdbfusion_f64, "
                          "VDBFusion at upstream's own precisions (the mode that meets SURVEY §8c's "
                          "per-voxel bar against literal VDBFusion, DESIGN.md §2c)")
+    ap.add_argument("--method", default="simple", choices=("simple", "merged"),
+                    help="with --semantics voxblox: voxblox's integrator (tsdf_params.voxblox_method;"
+                         " voxblox_ros' default is merged, DESIGN.md §2d)")
+    ap.add_argument("--const-weight", action="store_true",
+                    help="with --semantics voxblox: use_const_weight (w = 1); the default is "
+                         "voxblox's 1/z^2 weight from each scan's pose")
     ap.add_argument("--rank-rehearsal", type=int, default=0, metavar="N",
                     help="one process plays rank 0 of an N-GPU run (sector 0 of N, N x batch full "
                          "scans per step): its time per step is one rank's; value = N x batch "
@@ -140,7 +146,8 @@ def bench_parity(args, steps, make_volume):
     g.close()
     share = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
     threads = max(1, min(args.cpu_threads, share or 1))
-    ov = oracle.OracleTSDFVolume(args.voxel, args.trunc, semantics=args.semantics, threads=threads)
+    ov = oracle.OracleTSDFVolume(args.voxel, args.trunc, semantics=args.semantics, threads=threads,
+                                 method=args.method, use_const_weight=args.const_weight)
     n_scans = 0
     for i in sel:
         x, offs, org = steps[i]
@@ -155,8 +162,10 @@ def bench_parity(args, steps, make_volume):
     out = {"scans": n_scans, "voxels": int(gi.shape[0]), "oracle_voxels": int(oi.shape[0]),
            "bitwise": bool(same_set and w_eq and s_eq), "same_voxels": same_set,
            "weights_equal": w_eq, "sdf_bits_equal": s_eq,
-           "settings": "fresh context, semantics %s, pipeline %d, %d-scan device batches" % (
-               args.semantics, args.pipeline, args.batch),
+           "settings": "fresh context, semantics %s%s, pipeline %d, %d-scan device batches" % (
+               args.semantics, (" %s %s" % (args.method, "const weight" if args.const_weight
+                                            else "1/z^2")) if args.semantics == "voxblox" else "",
+               args.pipeline, args.batch),
            "oracle": "oracle/tsdf_oracle.c scan-fused, %d threads" % threads,
            "seconds": round(time.perf_counter() - t0, 2)}
     if same_set and not (w_eq and s_eq):
@@ -247,7 +256,7 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
 
     from tsdf_map import HipTSDFVolume
-    from tsdf_map.scan_gen import TorchOusterSim
+    from tsdf_map.scan_gen import TorchOusterSim, pose_on_circle
 
     # ---- synthesize every (full) scan of every step, resident in HBM ----------------------------
     sim = TorchOusterSim(dev, beams=args.sensor, hz=args.hz)
@@ -263,6 +272,11 @@ def main():
             pts, org = sim.scan(k)
             parts.append(pts)
             offs.append(offs[-1] + pts.shape[0])
+            if args.semantics == "voxblox":
+                # the full pose (x, y, z, qx, qy, qz, qw): Voxblox's 1/z^2 weight needs the sensor
+                # axes (the yaw of pose_on_circle; tsdf_integrate_batch_device_pose)
+                yaw = pose_on_circle(k, hz=args.hz)[1]
+                org = np.concatenate([org, [0.0, 0.0, math.sin(yaw / 2), math.cos(yaw / 2)]])
             origins.append(org)
         steps.append((torch.cat(parts).contiguous(), np.array(offs, np.uint64),
                       np.stack(origins)))
@@ -276,6 +290,7 @@ def main():
                              max_batch=min(scans_per_step, 512),  # one launch per step (all shards)
                              pipeline=args.pipeline if pipeline is None else pipeline,
                              semantics=args.semantics,
+                             method=args.method, use_const_weight=args.const_weight,
                              n_sectors=n_shards,  # this rank's azimuth sector of every scan
                              sector=(args.rehearsal_sector % n_shards if world == 1 and n_shards > 1
                                      else rank),
@@ -412,7 +427,8 @@ def main():
 
         def oracle_leg(threads):
             ov = oracle.OracleTSDFVolume(args.voxel, args.trunc, semantics=args.semantics,
-                                         threads=threads)
+                                         threads=threads, method=args.method,
+                                         use_const_weight=args.const_weight)
             n_done, tc, busy = 0, time.perf_counter(), 0.0
             for i in range(args.warmup, n_steps):  # the timed steps' scans, in order, until the budget
                 x, offs, org = steps[i]
@@ -481,6 +497,8 @@ def main():
                        "points_per_scan": int(round(rays_per_scan * n_shards)),
                     "scans_per_gpu_batch": args.batch, "pipelined_batches": args.pipeline,
                        "semantics": args.semantics,
+                       "voxblox": ({"method": args.method, "weight": "const" if args.const_weight
+                                    else "1/z^2"} if args.semantics == "voxblox" else None),
                        "parallelism": ("azimuth-sector x%d" % world if world > 1 else
                                        "rank-%d rehearsal of azimuth-sector x%d" % (
                                            args.rehearsal_sector % n_shards, n_shards)

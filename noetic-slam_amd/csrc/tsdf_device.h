@@ -60,6 +60,12 @@ constexpr int MAX_IN_BRICK = 22;       // a line visits at most 8+8+8-2 voxels o
 #define TSDF_PLC_STAGE 5600
 #endif
 constexpr int PLC_STAGE = TSDF_PLC_STAGE;
+// Voxblox with 1/z^2 weights (sem 3) stages a weight per sample too: 10 B a sample, so the
+// capacity that keeps three k_place workgroups per CU is smaller
+#ifndef TSDF_PLC_STAGE3
+#define TSDF_PLC_STAGE3 3700
+#endif
+constexpr int PLC_STAGE3 = TSDF_PLC_STAGE3;
 constexpr int PLC_WORDS = (PLC_STAGE + 31) / 32;
 constexpr int PLAN_STRIDE = ((PLC_WORDS + (PLC_WORDS + 1) / 2 + 1) + 15) & ~15;
 // single-walk front end (tsdf_walk.hip): rays per k_walk workgroup (one per lane; half an RPB

@@ -32,6 +32,11 @@ constexpr int INT_THREADS = 256;
 #endif
 constexpr int INT_PER = TSDF_INT_PER;                // register-cached samples per thread
 constexpr uint32_t INT_CAP = INT_PER * INT_THREADS;  // samples (>= live cells) per window
+// Voxblox with per-sample weights (sem 3): 16-B cells (u64 weight sums) and a weight register per
+// cached sample, so a window holds fewer samples to keep five workgroups per CU
+#ifndef TSDF_INT_PER3
+#define TSDF_INT_PER3 5
+#endif
 // LDS: 12 B per cell + ~9.5 KB per workgroup; residency as LDS allows
 constexpr int INT_BLOCKS_PER_CU = (160 * 1024) / (INT_CAP * 12 + 10 * 1024);
 #ifndef TSDF_INT_WIN
@@ -88,12 +93,14 @@ constexpr uint32_t NO_SPAN = 0xFFFFFFFFu;
 template <int SEM, int MAXS, bool FUSED>
 __global__ __launch_bounds__(INT_THREADS, TSDF_INT_WAVES) void k_integrate(BatchRef D, Table T, Work Wk, Pool Pl,
                                                           Globals* G, int parity, RayConst R) {
-    constexpr int NSLOT = FUSED ? INT_SPT * SPAN : INT_PER;  // register-cached samples per thread
+    constexpr int PER = SEM == 3 ? TSDF_INT_PER3 : INT_PER;  // register-cached samples per thread
+    constexpr uint32_t CAP = PER * INT_THREADS;                // samples (>= live cells) per window
+    constexpr int NSLOT = FUSED ? INT_SPT * SPAN : PER;  // register-cached samples per thread
     constexpr bool VB = SEM == 1 || SEM == 3;  // Voxblox fuse (3: per-sample weights in Work::smw)
     constexpr int NW = SEM == 3 ? NSLOT : 1;    // register-cached sample weights per thread
     typedef typename std::conditional<VB, unsigned long long, uint32_t>::type CellB;
-    __shared__ unsigned long long cA[INT_CAP];  // live cell: sum of trunc(s w * 2^32)
-    __shared__ CellB cB[INT_CAP];               // live cell: sample count / sum of trunc(w 2^32)
+    __shared__ unsigned long long cA[CAP];  // live cell: sum of trunc(s w * 2^32)
+    __shared__ CellB cB[CAP];               // live cell: sample count / sum of trunc(w 2^32)
     const float tau = R.tau;
     __shared__ MaskT sMask[BRICK_VOX];          // voxel: scans (bit t - t0) observed in the window
     __shared__ uint32_t sBase[BRICK_VOX];       // voxel: first live cell
@@ -123,7 +130,7 @@ __global__ __launch_bounds__(INT_THREADS, TSDF_INT_WAVES) void k_integrate(Batch
     uint32_t nb = 0, nwin = 0;
 #endif
     // Software pipeline over the workgroup's bricks: while brick a is processed, brick a + G's
-    // cell row, (S, W) and first INT_CAP samples are in flight to registers (BrickRegs), and
+    // cell row, (S, W) and first CAP samples are in flight to registers (BrickRegs), and
     // brick a + 2G's active record is loading.  A brick then starts with its data at hand.
     typedef typename std::conditional<FUSED, unsigned long long, uint32_t>::type CellT;
     const CellT* cells = reinterpret_cast<const CellT*>(T.cell);
@@ -161,7 +168,7 @@ __global__ __launch_bounds__(INT_THREADS, TSDF_INT_WAVES) void k_integrate(Batch
             load_span_samples(SP, B.c);
         } else {
 #pragma unroll
-            for (int j = 0; j < INT_PER; j++) {
+            for (int j = 0; j < PER; j++) {
                 const uint32_t i = tid + j * INT_THREADS;
                 // base + i >= max_smp: capacity overflow (reported by k_compact)
                 B.c[j] = (i < n && base + i < Wk.max_smp) ? Wk.smp[base + i] : make_uint2(0u, ~0u);
@@ -220,7 +227,7 @@ __global__ __launch_bounds__(INT_THREADS, TSDF_INT_WAVES) void k_integrate(Batch
         for (int j = 0; j < NSLOT; j++) c[j] = B.c[j];
 #pragma unroll
         for (int j = 0; j < NW; j++) cw[j] = B.cw[j];
-        // samples [cq, cq + INT_CAP) (FUSED: spans [cq, cq + INT_SCH)) are in c[] (uniform)
+        // samples [cq, cq + CAP) (FUSED: spans [cq, cq + INT_SCH)) are in c[] (uniform)
         uint32_t cq = FUSED ? base : 0u;
         const uint32_t pend = FUSED ? base + n : 0u;  // FUSED: the brick's span end
         auto load_chunk = [&](uint32_t q) {
@@ -231,7 +238,7 @@ __global__ __launch_bounds__(INT_THREADS, TSDF_INT_WAVES) void k_integrate(Batch
                 load_span_samples(sp, c);
             } else {
 #pragma unroll
-                for (int j = 0; j < INT_PER; j++) {
+                for (int j = 0; j < PER; j++) {
                     const uint32_t i = q + tid + j * INT_THREADS;
                     c[j] = (i < n && base + i < Wk.max_smp) ? Wk.smp[base + i] : make_uint2(0u, ~0u);
                     if constexpr (SEM == 3) cw[j] = (i < n && base + i < Wk.max_smp) ? Wk.smw[base + i] : 0.0f;
@@ -266,19 +273,19 @@ __global__ __launch_bounds__(INT_THREADS, TSDF_INT_WAVES) void k_integrate(Batch
         __syncthreads();  // s_cs, sS, sW visible
         PHASE(1);
         for (uint32_t t0 = 0; t0 < ns;) {
-            // window [t0, t1): as many scans as keep its samples <= INT_CAP (at least one)
+            // window [t0, t1): as many scans as keep its samples <= CAP (at least one)
             // (the extension test is monotone in the scan: one lane per candidate, one ballot)
             const uint32_t q0 = s_cs[t0];
             const uint32_t p0 = FUSED ? s_ps[t0] : 0u;
             const uint32_t tt = t0 + 1 + lane;
-            const bool ext = tt < ns && tt - t0 < INT_MAX_WIN && s_cs[min(tt + 1, ns)] - q0 <= INT_CAP &&
+            const bool ext = tt < ns && tt - t0 < INT_MAX_WIN && s_cs[min(tt + 1, ns)] - q0 <= CAP &&
                              (!FUSED || s_ps[min(tt + 1, ns)] - p0 <= INT_SCH);
             const uint32_t t1 = t0 + 1 + (uint32_t)__popcll(__ballot(ext));
             const uint32_t q1 = s_cs[t1], nw = t1 - t0;
             const uint32_t p1 = FUSED ? s_ps[t1] : 0u;
-            // the window's chunks: samples [q0, q1) in INT_CAP steps, FUSED spans [p0, p1) in INT_SCH
+            // the window's chunks: samples [q0, q1) in CAP steps, FUSED spans [p0, p1) in INT_SCH
             const uint32_t ck0 = FUSED ? p0 : q0, ck1 = FUSED ? p1 : q1;
-            constexpr uint32_t CK = FUSED ? INT_SCH : INT_CAP;
+            constexpr uint32_t CK = FUSED ? INT_SCH : CAP;
             if (q0 == q1) {  // uniform: no sample of this brick in the window
                 t0 = t1;
                 continue;
@@ -286,7 +293,7 @@ __global__ __launch_bounds__(INT_THREADS, TSDF_INT_WAVES) void k_integrate(Batch
 #ifdef TSDF_PHASE_TIMING
             nwin++;
 #endif
-            // P1: scan masks (a one-scan window may exceed INT_CAP samples: chunked)
+            // P1: scan masks (a one-scan window may exceed CAP samples: chunked)
             for (uint32_t qc = ck0; qc < ck1; qc += CK) {
                 if (cq != qc) {
                     load_chunk(qc);
@@ -429,13 +436,13 @@ __global__ __launch_bounds__(INT_THREADS, TSDF_INT_WAVES) void k_integrate(Batch
                         typedef const volatile __attribute__((address_space(3))) uint32_t lds_u32r;
                         lds_u64r* rA = (lds_u64r*)(cA);
                         lds_u32r* rB = (lds_u32r*)(cB);
-                        uint64_t a0 = rA[cell], a1 = rA[min(cell + 1u, INT_CAP - 1u)];
-                        uint32_t b0 = rB[cell], b1 = rB[min(cell + 1u, INT_CAP - 1u)];
+                        uint64_t a0 = rA[cell], a1 = rA[min(cell + 1u, CAP - 1u)];
+                        uint32_t b0 = rB[cell], b1 = rB[min(cell + 1u, CAP - 1u)];
                         for (uint32_t k = 0; k < rem; k += 2) {
-                            const uint64_t na0 = rA[min(cell + k + 2, INT_CAP - 1u)];
-                            const uint32_t nb0 = rB[min(cell + k + 2, INT_CAP - 1u)];
-                            const uint64_t na1 = rA[min(cell + k + 3, INT_CAP - 1u)];
-                            const uint32_t nb1 = rB[min(cell + k + 3, INT_CAP - 1u)];
+                            const uint64_t na0 = rA[min(cell + k + 2, CAP - 1u)];
+                            const uint32_t nb0 = rB[min(cell + k + 2, CAP - 1u)];
+                            const uint64_t na1 = rA[min(cell + k + 3, CAP - 1u)];
+                            const uint32_t nb1 = rB[min(cell + k + 3, CAP - 1u)];
                             const float fa0 = (float)((double)(long long)a0 * (1.0 / 4294967296.0));
                             const float fa1 = (float)((double)(long long)a1 * (1.0 / 4294967296.0));
                             float nwt = wt + (float)b0;
@@ -456,7 +463,7 @@ __global__ __launch_bounds__(INT_THREADS, TSDF_INT_WAVES) void k_integrate(Batch
                         continue;
                     }
                     // two cells in flight: a step's operand was read one step earlier
-                    float2 va = cF[cell], vb = cF[min(cell + 1u, INT_CAP - 1u)];
+                    float2 va = cF[cell], vb = cF[min(cell + 1u, CAP - 1u)];
                     // branch-free body (one basic block, so the reads stay ahead of their use);
                     // the second step of a pair is dropped past the chain's end
                     typedef const volatile __attribute__((address_space(3))) uint64_t lds_u64;
@@ -473,11 +480,11 @@ __global__ __launch_bounds__(INT_THREADS, TSDF_INT_WAVES) void k_integrate(Batch
                         w_ = ok ? (nw < R.max_weight ? nw : R.max_weight) : w_;
                     };
                     for (uint32_t k = 0; k < rem; k += 2) {
-                        const uint64_t na = cV[min(cell + k + 2, INT_CAP - 1u)];
+                        const uint64_t na = cV[min(cell + k + 2, CAP - 1u)];
                         uint64_t nb;
                         if constexpr (VB) {
                             vb_fuse(va, s, wt);
-                            nb = cV[min(cell + k + 3, INT_CAP - 1u)];
+                            nb = cV[min(cell + k + 3, CAP - 1u)];
                             float s2 = s, w2 = wt;
                             vb_fuse(vb, s2, w2);
                             const bool more = k + 1 < rem;
@@ -487,7 +494,7 @@ __global__ __launch_bounds__(INT_THREADS, TSDF_INT_WAVES) void k_integrate(Batch
                             float nwt = wt + va.y;
                             s = (s * wt + va.x) / nwt;
                             wt = nwt;
-                            nb = cV[min(cell + k + 3, INT_CAP - 1u)];
+                            nb = cV[min(cell + k + 3, CAP - 1u)];
                             nwt = wt + vb.y;
                             const float s2 = (s * wt + vb.x) / nwt;
                             const bool more = k + 1 < rem;

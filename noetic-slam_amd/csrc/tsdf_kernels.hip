@@ -1033,14 +1033,19 @@ template <int SEM>
 __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) void k_place(const float* __restrict__ xyz, BatchRef D,
                                                       RayConst R, Table T, Work Wk,
                                                       const Globals* __restrict__ G, int parity) {
+    // staging capacity: Voxblox 1/z^2 (sem 3) stages a weight beside every sample (10 B instead of
+    // 6), so it stages fewer to keep three workgroups per CU (the plan's positions below STG are
+    // a prefix of k_count's; later samples are stored directly)
+    constexpr int STG = SEM == 3 ? PLC_STAGE3 : PLC_STAGE;
+    static_assert(STG <= PLC_STAGE, "k_count's plan covers the staging");
     __shared__ uint32_t s_base[HCAP];      // run -> first sample of the run in the brick segment
     __shared__ uint16_t s_loff[HCAP];      // run -> offset in the workgroup's sample order
     __shared__ uint16_t s_ord[HCAP];       // staged runs in staging order
     __shared__ uint32_t s_bits[PLC_WORDS]; // staging positions where a run starts
     __shared__ uint16_t s_wpre[(PLC_WORDS + 1) & ~1]; // run starts in the words before
-    __shared__ float st_s[PLC_STAGE];      // staged samples
-    __shared__ uint16_t st_l[PLC_STAGE];
-    __shared__ float st_w[SEM == 3 ? PLC_STAGE : 1];  // Voxblox 1/z^2: the samples' weights
+    __shared__ float st_s[STG];      // staged samples
+    __shared__ uint16_t st_l[STG];
+    __shared__ float st_w[SEM == 3 ? STG : 1];  // Voxblox 1/z^2: the samples' weights
     __shared__ uint32_t s_vote[2][PLC_THREADS / 64];  // block_any: sector test, second pass
 #ifdef TSDF_ABLATE_PL_EMPTY
     __shared__ uint32_t s_nst;             // staged samples (end of the last staged run)
@@ -1115,7 +1120,7 @@ __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) v
     auto fill = [&](uint32_t j, const uint4& e) {
         const uint32_t slot = e.w >> 16;
         // runs starting past the staging capacity are stored directly (0xFFFF: not staged)
-        const bool stg = e.z < (uint32_t)PLC_STAGE;
+        const bool stg = e.z < (uint32_t)STG;
         s_loff[slot] = stg ? (uint16_t)e.z : (uint16_t)0xFFFFu;
         if (stg) s_ord[j] = (uint16_t)slot;
     };
@@ -1142,7 +1147,7 @@ __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) v
     if (threadIdx.x == 0) pt[3] = clock64();
 #endif
     // a pair code -> its samples' global position (when `with_pos`: s_base is filled), staging
-    // position (lpos < PLC_STAGE), count
+    // position (lpos < STG), count
     auto resolve = [&](uint32_t code, bool with_pos, uint32_t& pos, uint32_t& lpos, uint32_t& cnt) {
         pos = NO_PAIR;
         lpos = NO_PAIR;
@@ -1185,10 +1190,10 @@ __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) v
             if (maxp > 2) code.z = pc[2];
         }
         // pair queue: global position P, and (staging position | count << 16) Q; a staging
-        // position of 0xFFFF (>= PLC_STAGE) means not staged
+        // position of 0xFFFF (>= STG) means not staged
         uint32_t P0 = NO_PAIR, P1 = NO_PAIR, P2 = NO_PAIR, P3 = NO_PAIR;
         uint32_t Q0 = 0xFFFFu, Q1 = 0xFFFFu, Q2 = 0xFFFFu, Q3 = 0xFFFFu;
-        static_assert(PLC_STAGE < 0xFFFF, "staging positions are 16-bit");
+        static_assert(STG < 0xFFFF, "staging positions are 16-bit");
         auto resolve_q = [&](uint32_t c, uint32_t& P, uint32_t& Q) {
             uint32_t lp, n;
             resolve(c, WITH_POS, P, lp, n);
@@ -1227,7 +1232,7 @@ __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) v
                 w = nb ? 0u : w;
                 const uint32_t lpos = lq & 0xFFFFu, cnt = lq >> 16;
                 const bool st = g && w < cnt;
-                const bool staged = lpos + w < (uint32_t)PLC_STAGE;
+                const bool staged = lpos + w < (uint32_t)STG;
                 if (STAGE && st && staged) {
                     st_s[lpos + w] = s;
                     st_l[lpos + w] = (uint16_t)l;
@@ -1271,7 +1276,7 @@ __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) v
                     }
                     if (w < cnt) {
                         const uint32_t l = ((r.vz & 7) << 6) | ((r.vy & 7) << 3) | (r.vx & 7);
-                        if (lpos != NO_PAIR && lpos + w < (uint32_t)PLC_STAGE) {
+                        if (lpos != NO_PAIR && lpos + w < (uint32_t)STG) {
                             st_s[lpos + w] = s;
                             st_l[lpos + w] = (uint16_t)l;
                             if constexpr (SEM == 3) st_w[lpos + w] = vb_weight(R, r.w0, s);
@@ -1310,7 +1315,7 @@ __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) v
 #ifdef TSDF_ABLATE_PL_NOCOPY
     const uint32_t nst = 0;
 #else
-    const uint32_t nst = plan_nst;
+    const uint32_t nst = min(plan_nst, (uint32_t)STG);
 #endif
     for (uint32_t j = threadIdx.x; j < nst; j += PLC_THREADS) {
         const uint32_t wd = j >> 5;
