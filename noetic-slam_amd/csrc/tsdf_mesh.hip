@@ -27,7 +27,8 @@ constexpr int TILE = 9;
 
 // Stage the 9^3 tile of brick `key`: s_ok[t] = observed (W > 0, W >= min_weight).  A neighbour is
 // looked up in the halo (H, HP) first -- bricks another rank owns after a border reduce, of which
-// this context may hold a reset copy -- then in the context's own table.
+// this context may hold a reset copy -- then in the context's own table; the brick itself only in
+// the own table.
 __device__ void mesh_tile(const Table& T, const Pool& Pl, const Table& H, const Pool& HP,
                           uint64_t key, float min_weight, float* s_S, uint8_t* s_ok,
                           uint32_t* s_slot) {
@@ -40,7 +41,9 @@ __device__ void mesh_tile(const Table& T, const Pool& Pl, const Table& H, const 
         const int nx = bx + dx, ny = by + dy, nz = bz + dz;
         if (nx < BRICK_COORD_BIAS && ny < BRICK_COORD_BIAS && nz < BRICK_COORD_BIAS) {
             const uint64_t nk = pack_brick(nx, ny, nz);
-            if (H.keys) {
+            // the brick itself always from the own table: a reset copy of a brick owned elsewhere
+            // is meshed by its owner (its halo copy would mesh its cubes twice)
+            if (H.keys && threadIdx.x != 0) {
                 const int64_t h = table_find(H, nk);
                 if (h >= 0) {
                     slot = H.slots[h];

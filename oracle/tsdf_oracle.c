@@ -1623,7 +1623,15 @@ int tsdf_halo_keys_device(tsdf_ctx* c, uint64_t* keys, uint64_t cap, uint64_t* n
     uint64_t* have = (uint64_t*)malloc((nb ? nb : 1) * sizeof(uint64_t));
     uint64_t* need = (uint64_t*)malloc((nb ? 7 * nb : 1) * sizeof(uint64_t));
     if (!have || !need) { free(e); free(have); free(need); return TSDF_ENOMEM; }
-    for (uint64_t i = 0; i < nb; i++) have[i] = pack_key(e[i].b);
+    /* observed bricks only: a reset copy of a brick owned elsewhere (W = 0 after a border reduce)
+       is requested like an absent one */
+    uint64_t nh = 0;
+    for (uint64_t i = 0; i < nb; i++)
+        if (brick_observed(c, e[i].b)) {
+            e[nh] = e[i];
+            have[nh++] = pack_key(e[i].b);
+        }
+    nb = nh;
     qsort(have, nb, sizeof(uint64_t), cmp_u64);
     uint64_t m = 0;
     for (uint64_t i = 0; i < nb; i++)
@@ -1801,9 +1809,14 @@ static int cmp_halo(const void* a, const void* b) {
     return x < y ? -1 : (x > y);
 }
 
-/* voxel (x, y, z): from its brick's halo tile when there is one, else the context's own voxel */
-static int corner(const tsdf_ctx* c, const halo_ent* h, uint64_t nh, int32_t x, int32_t y, int32_t z,
-                  float* S, float* W) {
+/* voxel (x, y, z): from its brick's halo tile when there is one, else the context's own voxel;
+   voxels of the brick being meshed (own = its key) always from the context itself */
+static int corner(const tsdf_ctx* c, const halo_ent* h, uint64_t nh, uint64_t own, int32_t x,
+                  int32_t y, int32_t z, float* S, float* W) {
+    if (nh) {
+        const int32_t b[3] = {fdiv8(x), fdiv8(y), fdiv8(z)};
+        if (pack_key(b) == own) nh = 0;
+    }
     if (nh) {
         const int32_t b[3] = {fdiv8(x), fdiv8(y), fdiv8(z)};
         const halo_ent q = {pack_key(b), NULL};
@@ -1850,7 +1863,8 @@ static int mesh_impl(tsdf_ctx* c, float min_weight, int32_t table, const uint32_
             int ok = 1, k = 0;
             for (int q = 0; q < 8 && ok; q++) {
                 float sv = 0.0f, wv = 0.0f;
-                if (!corner(c, h, n_halo, x + (q & 1), y + ((q >> 1) & 1), z + ((q >> 2) & 1), &sv, &wv) ||
+                if (!corner(c, h, n_halo, pack_key(e[b].b), x + (q & 1), y + ((q >> 1) & 1),
+                            z + ((q >> 2) & 1), &sv, &wv) ||
                     !(wv > 0.0f) || !(wv >= min_weight)) { ok = 0; break; }
                 S[q] = sv;
                 if (sv < 0.0f) k |= 1 << q;
