@@ -237,11 +237,6 @@ struct tsdf_ctx {
     // the end of the last batch of each parity: the ring event of that batch's slot (one marker
     // per batch; every marker in the stream costs the GPU a few microseconds)
     hipEvent_t ev_integ[2] = {nullptr, nullptr};
-    // role streams (TSDF_ROLE_STREAMS, experiment): the front end (upload, count, compact) of every
-    // batch on bst[1], the back end (place, integrate, finish) on bst[0], so the two can carry
-    // different HIP stream priorities; ev_fe[b & 1]: batch b's front end done
-    int role = 0;
-    hipEvent_t ev_fe[2] = {nullptr, nullptr};
     BatchDesc pend{};  // pending host scans (points in stage2[pend_stage])
     // Device staging ownership (independent of batch parity, which replays can shift): the pending
     // batch's buffer, and per buffer the last batch that read it (its id and completion event).
@@ -418,10 +413,7 @@ static int launch(tsdf_ctx* c, const float* d_xyz, BatchDesc& D) {
 #else
     const bool cross = true;
 #endif
-    // role streams: st (front end) and bk (back end); otherwise one stream per batch parity
-    const bool role = cross && c->role;
-    hipStream_t st = role ? c->bst[1] : c->bst[cross ? par : 0];
-    hipStream_t bk = role ? c->bst[0] : st;
+    hipStream_t st = c->bst[cross ? par : 0];
     Table T = c->T;
     T.cell = c->cell2[par];
     const Work& W = c->W2[par];
@@ -433,15 +425,7 @@ static int launch(tsdf_ctx* c, const float* d_xyz, BatchDesc& D) {
         HIPCHK(c, hipEventRecord(c->ev_main, c->stream));
         HIPCHK(c, hipStreamWaitEvent(st, c->ev_main, 0));
     }
-    if (role) {
-        // the front stream orders batch b after b-1's front end; batch b-2, the last user of this
-        // parity's work buffers, cells and counters, must have finished (pipeline 1), or batch
-        // b-1's place (pipeline 2, which implies it: the back stream is in batch order)
-        if (c->p.pipeline == 2 && c->batch_id > 0)
-            HIPCHK(c, hipStreamWaitEvent(st, c->ev_compact[par ^ 1], 0));
-        else if (c->batch_id > 1)
-            HIPCHK(c, hipStreamWaitEvent(st, c->ev_integ[par], 0));
-    } else if (c->batch_id > 0 && cross)  // pipelined: after the previous batch's compact; else after all of it
+    if (c->batch_id > 0 && cross)  // pipelined: after the previous batch's compact; else after all of it
         HIPCHK(c, hipStreamWaitEvent(st, c->p.pipeline ? c->ev_compact[par ^ 1]
                                                        : c->ev_integ[par ^ 1], 0));
     c->ht.lap(1);
@@ -504,14 +488,8 @@ static int launch(tsdf_ctx* c, const float* d_xyz, BatchDesc& D) {
     // batch b-1's end, so only k_count / k_compact of b+1 overlap k_integrate of b and k_place
     // always runs alone
     const bool lean = c->p.pipeline == 2;
-    if (role) {  // the back end after this batch's front end (and, in stream order, after b-1)
-        HIPCHK(c, hipEventRecord(c->ev_fe[par], st));
-        HIPCHK(c, hipStreamWaitEvent(bk, c->ev_fe[par], 0));
-        st = bk;
-    } else {
     if (cross && c->p.pipeline && !lean) HIPCHK(c, hipEventRecord(c->ev_compact[par], st));
     if (lean && c->batch_id > 0) HIPCHK(c, hipStreamWaitEvent(st, c->ev_integ[par ^ 1], 0));
-    }
     if (D.n_blocks) {
         if (tm && c->fused) tm->next(KIND_COMPACT, k_back, st);
         if (c->fused) HIPCHK(c, launch_spans(B, c->R, T, W, c->G, par, c->nstep, st));
@@ -520,8 +498,7 @@ static int launch(tsdf_ctx* c, const float* d_xyz, BatchDesc& D) {
         if (tm && c->fused) tm->end(k_back, st);
     }
     if (lean) HIPCHK(c, hipEventRecord(c->ev_compact[par], st));  // batch b+1's front-end wait
-    if (c->batch_id > 0 && cross && !lean && !role)
-        HIPCHK(c, hipStreamWaitEvent(st, c->ev_integ[par ^ 1], 0));
+    if (c->batch_id > 0 && cross && !lean) HIPCHK(c, hipStreamWaitEvent(st, c->ev_integ[par ^ 1], 0));
     if (D.n_blocks) {
         if (tm && c->fused) tm->begin(KIND_INTEGRATE, st);
         if (small) {
@@ -1162,7 +1139,6 @@ void tsdf_destroy(tsdf_ctx* c) {
     for (int q = 0; q < 2; q++) {
         if (c->bst[q]) (void)hipStreamDestroy(c->bst[q]);
         if (c->ev_compact[q]) (void)hipEventDestroy(c->ev_compact[q]);
-        if (c->ev_fe[q]) (void)hipEventDestroy(c->ev_fe[q]);
         if (c->stage_ev[q]) (void)hipEventDestroy(c->stage_ev[q]);
     }
     if (c->ev_main) (void)hipEventDestroy(c->ev_main);
@@ -1185,19 +1161,8 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
     c->device = p->device_id;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    // TSDF_ROLE_STREAMS (experiment): 1 role streams at equal priority, 2 the back
-    // end (place, integrate) at high and the front end at low priority, 3 the reverse
-    if (const char* e = std::getenv("TSDF_ROLE_STREAMS")) c->role = std::atoi(e);
-    int prio_lo = 0, prio_hi = 0;
-    HIPCHK(c, hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
     for (int q = 0; q < 2; q++) {
-        const bool hi = (c->role == 2 && q == 0) || (c->role == 3 && q == 1);
-        const bool lo = (c->role == 2 && q == 1) || (c->role == 3 && q == 0);
-        if (hi || lo)
-            HIPCHK(c, hipStreamCreateWithPriority(&c->bst[q], hipStreamNonBlocking, hi ? prio_hi : prio_lo));
-        else
-            HIPCHK(c, hipStreamCreateWithFlags(&c->bst[q], hipStreamNonBlocking));
-        HIPCHK(c, hipEventCreateWithFlags(&c->ev_fe[q], hipEventDisableTiming));
+        HIPCHK(c, hipStreamCreateWithFlags(&c->bst[q], hipStreamNonBlocking));
         HIPCHK(c, hipEventCreateWithFlags(&c->ev_compact[q], hipEventDisableTiming));
         HIPCHK(c, hipEventCreateWithFlags(&c->stage_ev[q], hipEventDisableTiming));
     }

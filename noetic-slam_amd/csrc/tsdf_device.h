@@ -60,14 +60,20 @@ constexpr int MAX_IN_BRICK = 22;       // a line visits at most 8+8+8-2 voxels o
 #define TSDF_PLC_STAGE 5600
 #endif
 constexpr int PLC_STAGE = TSDF_PLC_STAGE;
-// Voxblox with 1/z^2 weights (sem 3) stages a weight per sample too: 10 B a sample, so the
-// capacity that keeps three k_place workgroups per CU is smaller
+// Voxblox with 1/z^2 weights (sem 3): the sample's ray is staged beside it (8 B a sample; the
+// weight is formed at copy-out from a per-ray LDS table), and its rays carry more samples, so it
+// stages more: two workgroups per CU with nearly a whole half block staged beat three with less
+// (round 5: 4352 / 4096 / 5600 / 7744 samples).  k_count<3>'s plan covers it.
 #ifndef TSDF_PLC_STAGE3
-#define TSDF_PLC_STAGE3 3700
+#define TSDF_PLC_STAGE3 7744
 #endif
 constexpr int PLC_STAGE3 = TSDF_PLC_STAGE3;
-constexpr int PLC_WORDS = (PLC_STAGE + 31) / 32;
-constexpr int PLAN_STRIDE = ((PLC_WORDS + (PLC_WORDS + 1) / 2 + 1) + 15) & ~15;
+// staging capacity and plan bitmap words of semantics SEM
+__host__ __device__ constexpr int plan_cap(int sem) { return sem == 3 ? PLC_STAGE3 : PLC_STAGE; }
+__host__ __device__ constexpr int plan_words(int sem) { return (plan_cap(sem) + 31) / 32; }
+constexpr int PLC_WORDS = plan_words(0);
+constexpr int PLC_WORDS_MAX = plan_words(0) > plan_words(3) ? plan_words(0) : plan_words(3);
+constexpr int PLAN_STRIDE = ((PLC_WORDS_MAX + (PLC_WORDS_MAX + 1) / 2 + 1) + 15) & ~15;
 // single-walk front end (tsdf_walk.hip): rays per k_walk workgroup (one per lane; half an RPB
 // block) and samples per span record
 constexpr int WLK_THREADS = RPB / 2;

@@ -32,18 +32,11 @@ constexpr int INT_THREADS = 256;
 #endif
 constexpr int INT_PER = TSDF_INT_PER;                // register-cached samples per thread
 constexpr uint32_t INT_CAP = INT_PER * INT_THREADS;  // samples (>= live cells) per window
-// Voxblox with per-sample weights (sem 3): 16-B cells (u64 weight sums) and a weight register per
-// cached sample, so a window holds fewer samples to keep five workgroups per CU
+// Voxblox with per-sample weights (sem 3): register-cached samples per thread (A/B knob; 5 keeps
+// five workgroups per CU with 16-B cells but measured slower than 6: DESIGN.md §10)
 #ifndef TSDF_INT_PER3
-#define TSDF_INT_PER3 5
+#define TSDF_INT_PER3 TSDF_INT_PER
 #endif
-// VDBFusion cells (sem 0, 2): a window whose samples are few enough that no cell's fixed-point sum
-// can reach 2^47 (|trunc(s 2^32)| <= tau 2^32 per sample) carries the sample count in the top 16
-// bits of the same 64-bit cell, so P3 issues one LDS atomic per sample instead of two
-#ifndef TSDF_INT_PACKCNT
-#define TSDF_INT_PACKCNT 1
-#endif
-constexpr uint32_t PACK_SHIFT = 48;
 // LDS: 12 B per cell + ~9.5 KB per workgroup; residency as LDS allows
 constexpr int INT_BLOCKS_PER_CU = (160 * 1024) / (INT_CAP * 12 + 10 * 1024);
 #ifndef TSDF_INT_WIN
@@ -125,8 +118,6 @@ __global__ __launch_bounds__(INT_THREADS, TSDF_INT_WAVES) void k_integrate(Batch
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const uint32_t n_active = min(C->n_active, Wk.max_active);
     const uint32_t ns = D.n_scans;
-    // the most samples a packed window may hold: n tau 2^32 < 2^47 (with margin), n < 2^16
-    const uint32_t pack_max = (uint32_t)fminf(65535.0f, 32000.0f / fmaxf(R.tau, 1e-6f));
     // a batch that overflowed (or follows one) is replayed after the host grows the buffers: its
     // field writes are skipped, everything else (cell clean-up) runs
     const bool commit = !(G->retry && (C->ovf || G->failed));
@@ -291,8 +282,6 @@ __global__ __launch_bounds__(INT_THREADS, TSDF_INT_WAVES) void k_integrate(Batch
                              (!FUSED || s_ps[min(tt + 1, ns)] - p0 <= INT_SCH);
             const uint32_t t1 = t0 + 1 + (uint32_t)__popcll(__ballot(ext));
             const uint32_t q1 = s_cs[t1], nw = t1 - t0;
-            // packed cells: every cell sum stays below 2^47 in magnitude and its count below 2^16
-            const bool pk = TSDF_INT_PACKCNT && !VB && q1 - q0 <= pack_max;
             const uint32_t p1 = FUSED ? s_ps[t1] : 0u;
             // the window's chunks: samples [q0, q1) in CAP steps, FUSED spans [p0, p1) in INT_SCH
             const uint32_t ck0 = FUSED ? p0 : q0, ck1 = FUSED ? p1 : q1;
@@ -363,7 +352,7 @@ __global__ __launch_bounds__(INT_THREADS, TSDF_INT_WAVES) void k_integrate(Batch
                 // the window's cells start at zero (the previous window's P4 is past a barrier)
                 for (uint32_t j = tid; j < (tot & 0xFFFFu); j += INT_THREADS) {
                     cA[j] = 0ull;
-                    if (!pk) cB[j] = 0;
+                    cB[j] = 0;
                 }
             }
             __syncthreads();
@@ -394,12 +383,8 @@ __global__ __launch_bounds__(INT_THREADS, TSDF_INT_WAVES) void k_integrate(Batch
                             if (fx == 12345)
 #endif
                             {
-                                if (pk) {
-                                    atomicAdd(&cA[cell], (unsigned long long)fx + (1ull << PACK_SHIFT));
-                                } else {
-                                    atomicAdd(&cA[cell], (unsigned long long)fx);
-                                    atomicAdd(&cB[cell], 1u);
-                                }
+                                atomicAdd(&cA[cell], (unsigned long long)fx);
+                                atomicAdd(&cB[cell], 1u);
                             }
                         }
                     }
@@ -421,21 +406,12 @@ __global__ __launch_bounds__(INT_THREADS, TSDF_INT_WAVES) void k_integrate(Batch
             if constexpr (!inline_cvt) {
                 const uint32_t ncell = s_ncell;
                 for (uint32_t j = tid; j < ncell; j += INT_THREADS) {
-                    unsigned long long raw = cA[j];
-                    uint32_t cnt = 0;
-                    if (!VB) {
-                        if (pk) {
-                            cnt = (uint32_t)((raw + (1ull << (PACK_SHIFT - 1))) >> PACK_SHIFT);
-                            raw -= (unsigned long long)cnt << PACK_SHIFT;
-                        } else {
-                            cnt = (uint32_t)cB[j];
-                        }
-                    }
-                    const float af = (float)((double)(long long)raw * (1.0 / 4294967296.0));
+                    const long long av = (long long)cA[j];
+                    const float af = (float)((double)av * (1.0 / 4294967296.0));
                     if constexpr (VB)
                         cF[j] = make_float2(af, (float)((double)(long long)cB[j] * (1.0 / 4294967296.0)));
                     else
-                        cF[j] = make_float2(af, (float)cnt);
+                        cF[j] = make_float2(af, (float)cB[j]);
                 }
             }
             if constexpr (!inline_cvt) __syncthreads();
@@ -460,25 +436,13 @@ __global__ __launch_bounds__(INT_THREADS, TSDF_INT_WAVES) void k_integrate(Batch
                         typedef const volatile __attribute__((address_space(3))) uint32_t lds_u32r;
                         lds_u64r* rA = (lds_u64r*)(cA);
                         lds_u32r* rB = (lds_u32r*)(cB);
-                        // packed window: the count is the cell's top bits (no cB reads)
-                        auto rd = [&](uint32_t i, uint64_t& a, uint32_t& b) {
-                            a = rA[i];
-                            if (pk) {
-                                b = (uint32_t)((a + (1ull << (PACK_SHIFT - 1))) >> PACK_SHIFT);
-                                a -= (uint64_t)b << PACK_SHIFT;
-                            } else {
-                                b = rB[i];
-                            }
-                        };
-                        uint64_t a0, a1;
-                        uint32_t b0, b1;
-                        rd(cell, a0, b0);
-                        rd(min(cell + 1u, CAP - 1u), a1, b1);
+                        uint64_t a0 = rA[cell], a1 = rA[min(cell + 1u, CAP - 1u)];
+                        uint32_t b0 = rB[cell], b1 = rB[min(cell + 1u, CAP - 1u)];
                         for (uint32_t k = 0; k < rem; k += 2) {
-                            uint64_t na0, na1;
-                            uint32_t nb0, nb1;
-                            rd(min(cell + k + 2, CAP - 1u), na0, nb0);
-                            rd(min(cell + k + 3, CAP - 1u), na1, nb1);
+                            const uint64_t na0 = rA[min(cell + k + 2, CAP - 1u)];
+                            const uint32_t nb0 = rB[min(cell + k + 2, CAP - 1u)];
+                            const uint64_t na1 = rA[min(cell + k + 3, CAP - 1u)];
+                            const uint32_t nb1 = rB[min(cell + k + 3, CAP - 1u)];
                             const float fa0 = (float)((double)(long long)a0 * (1.0 / 4294967296.0));
                             const float fa1 = (float)((double)(long long)a1 * (1.0 / 4294967296.0));
                             float nwt = wt + (float)b0;

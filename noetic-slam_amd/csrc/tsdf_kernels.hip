@@ -137,6 +137,7 @@ __global__ __launch_bounds__(NT, SEM == 2 && (NT == CNT_THREADS || G == 2) ? TSD
     static_assert(G == 1 || G == 2, "one or two blocks per workgroup");
     static_assert(G == 1 || RPB % NT == 0, "a pass over the rays stays inside one block");
     using CntT = typename std::conditional<G == 2, unsigned long long, uint32_t>::type;
+    constexpr int PCAP = plan_cap(SEM), PW = plan_words(SEM);  // k_place<SEM>'s staging plan
 #ifdef TSDF_CNT_SPLIT
     // variant build: the global phase (find-or-insert, cell atomic) runs in k_resolve
     constexpr bool SPLIT = G == 1;
@@ -151,7 +152,7 @@ __global__ __launch_bounds__(NT, SEM == 2 && (NT == CNT_THREADS || G == 2) ? TSD
     __shared__ unsigned long long red[2][NT / 64];
     __shared__ unsigned long long s_wsum[G][NT / 64];
     __shared__ uint32_t s_wcnt[G][NT / 64];
-    __shared__ uint32_t s_bm[NSUB][PLC_WORDS];  // per sub-run list: staging positions where a run starts
+    __shared__ uint32_t s_bm[NSUB][PW];  // per sub-run list: staging positions where a run starts
     Counters* C = &G_->ctr[parity];  // zeroed by the previous batch of this parity (k_finish)
     // sector sharding: every GPU sees every scan, and a block of 1024 consecutive rays (~3 degrees
     // of azimuth) usually lies wholly in one sector; the workgroups take the blocks k_sector_flags
@@ -175,7 +176,7 @@ __global__ __launch_bounds__(NT, SEM == 2 && (NT == CNT_THREADS || G == 2) ? TSD
         s_key[j] = EMPTY_KEY;
         s_cnt[j] = 0u;
     }
-    for (int j = threadIdx.x; j < NSUB * PLC_WORDS; j += NT) (&s_bm[0][0])[j] = 0u;
+    for (int j = threadIdx.x; j < NSUB * PW; j += NT) (&s_bm[0][0])[j] = 0u;
     __syncthreads();
     CPH(0);  // LDS init
     const uint32_t maxp = Wk.maxp;
@@ -425,9 +426,9 @@ __global__ __launch_bounds__(NT, SEM == 2 && (NT == CNT_THREADS || G == 2) ? TSD
                 Wk.blk_n[2 * b + 1] = totc >> 16;
                 // each half's staged sample count: its samples, up to the staging capacity
                 Wk.plan[(size_t)(2 * b) * PLAN_STRIDE + PLAN_STRIDE - 1] =
-                    min((uint32_t)tot, (uint32_t)PLC_STAGE);
+                    min((uint32_t)tot, (uint32_t)PCAP);
                 Wk.plan[(size_t)(2 * b + 1) * PLAN_STRIDE + PLAN_STRIDE - 1] =
-                    min((uint32_t)(tot >> 32), (uint32_t)PLC_STAGE);
+                    min((uint32_t)(tot >> 32), (uint32_t)PCAP);
             }
         }
     }
@@ -447,14 +448,14 @@ __global__ __launch_bounds__(NT, SEM == 2 && (NT == CNT_THREADS || G == 2) ? TSD
             uint4* bt = Wk.blk + (size_t)(2 * bx) * HCAP;
             if (n0) {
                 reinterpret_cast<uint2*>(bt + idx[0])[1] = make_uint2(off[0], n0 | ((uint32_t)slot << 16));
-                if (off[0] < (uint32_t)PLC_STAGE) atomicOr(&s_bm[0][off[0] >> 5], 1u << (off[0] & 31));
+                if (off[0] < (uint32_t)PCAP) atomicOr(&s_bm[0][off[0] >> 5], 1u << (off[0] & 31));
                 w |= idx[0]++;
                 off[0] += n0;
             }
             if (n1) {
                 reinterpret_cast<uint2*>(bt + HCAP + idx[NSUB - 1])[1] =
                     make_uint2(off[NSUB - 1], n1 | ((uint32_t)slot << 16));
-                if (off[NSUB - 1] < (uint32_t)PLC_STAGE)
+                if (off[NSUB - 1] < (uint32_t)PCAP)
                     atomicOr(&s_bm[NSUB - 1][off[NSUB - 1] >> 5], 1u << (off[NSUB - 1] & 31));
                 w |= idx[NSUB - 1]++ << 11;
                 off[NSUB - 1] += n1;
@@ -503,7 +504,7 @@ __global__ __launch_bounds__(NT, SEM == 2 && (NT == CNT_THREADS || G == 2) ? TSD
         for (int s = 0; s < NSUB; s++) {
             const uint32_t n = (uint32_t)(c >> (16 * s)) & 0xFFFFu;
             if (n) {
-                if (boff[s] < (uint32_t)PLC_STAGE) atomicOr(&s_bm[s][boff[s] >> 5], 1u << (boff[s] & 31));
+                if (boff[s] < (uint32_t)PCAP) atomicOr(&s_bm[s][boff[s] >> 5], 1u << (boff[s] & 31));
                 boff[s] += n;
             }
         }
@@ -543,22 +544,22 @@ __global__ __launch_bounds__(NT, SEM == 2 && (NT == CNT_THREADS || G == 2) ? TSD
         static_assert(NT / 64 >= NSUB, "one wave per sub-run list");
         if (wv < NSUB) {
             // WPL consecutive bitmap words per lane; the prefix is one u16 per word
-            constexpr int WPL = (PLC_WORDS + 63) / 64;
+            constexpr int WPL = (PW + 63) / 64;
             static_assert(WPL >= 1 && WPL <= 4, "bitmap words per lane");
             uint32_t* pl = Wk.plan + (size_t)(2 * (G * bx + (wv >> 1)) + (wv & 1)) * PLAN_STRIDE;
-            uint16_t* pp = reinterpret_cast<uint16_t*>(pl + PLC_WORDS);
+            uint16_t* pp = reinterpret_cast<uint16_t*>(pl + PW);
             uint32_t b[WPL], cs = 0;
 #pragma unroll
             for (int q = 0; q < WPL; q++) {
                 const int wd = WPL * ln + q;
-                b[q] = wd < PLC_WORDS ? s_bm[wv][wd] : 0u;
+                b[q] = wd < PW ? s_bm[wv][wd] : 0u;
                 cs += (uint32_t)__popc(b[q]);
             }
             uint32_t pre = wave_incl_scan(cs) - cs;
 #pragma unroll
             for (int q = 0; q < WPL; q++) {
                 const int wd = WPL * ln + q;
-                if (wd < PLC_WORDS) {
+                if (wd < PW) {
                     pl[wd] = b[q];
                     pp[wd] = (uint16_t)pre;
                 }
@@ -1033,19 +1034,20 @@ template <int SEM>
 __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) void k_place(const float* __restrict__ xyz, BatchRef D,
                                                       RayConst R, Table T, Work Wk,
                                                       const Globals* __restrict__ G, int parity) {
-    // staging capacity: Voxblox 1/z^2 (sem 3) stages a weight beside every sample (10 B instead of
-    // 6), so it stages fewer to keep three workgroups per CU (the plan's positions below STG are
-    // a prefix of k_count's; later samples are stored directly)
-    constexpr int STG = SEM == 3 ? PLC_STAGE3 : PLC_STAGE;
-    static_assert(STG <= PLC_STAGE, "k_count's plan covers the staging");
+    // staging capacity (tsdf_device.h plan_cap: Voxblox 1/z^2 stages more, at 8 B a sample);
+    // samples past it are stored directly
+    constexpr int STG = plan_cap(SEM), PW = plan_words(SEM);  // k_count<SEM> plans as much
     __shared__ uint32_t s_base[HCAP];      // run -> first sample of the run in the brick segment
     __shared__ uint16_t s_loff[HCAP];      // run -> offset in the workgroup's sample order
     __shared__ uint16_t s_ord[HCAP];       // staged runs in staging order
-    __shared__ uint32_t s_bits[PLC_WORDS]; // staging positions where a run starts
-    __shared__ uint16_t s_wpre[(PLC_WORDS + 1) & ~1]; // run starts in the words before
+    __shared__ uint32_t s_bits[PW]; // staging positions where a run starts
+    __shared__ uint16_t s_wpre[(PW + 1) & ~1]; // run starts in the words before
     __shared__ float st_s[STG];      // staged samples
-    __shared__ uint16_t st_l[STG];
-    __shared__ float st_w[SEM == 3 ? STG : 1];  // Voxblox 1/z^2: the samples' weights
+    // the staged sample's voxel; Voxblox 1/z^2 (sem 3): | its ray (lane) << 9, whose 1/z^2 weight
+    // s_w0 holds (the sample's weight is formed at copy-out: 8 B of staging a sample, not 10)
+    typedef typename std::conditional<SEM == 3, uint32_t, uint16_t>::type StL;
+    __shared__ StL st_l[STG];
+    __shared__ float s_w0[SEM == 3 ? PLC_THREADS : 1];
     __shared__ uint32_t s_vote[2][PLC_THREADS / 64];  // block_any: sector test, second pass
 #ifdef TSDF_ABLATE_PL_EMPTY
     __shared__ uint32_t s_nst;             // staged samples (end of the last staged run)
@@ -1092,10 +1094,10 @@ __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) v
     const uint4 e0 = bt[threadIdx.x];
     // k_count's staging plan: bitmap words, their prefix (u16 pairs) and the staged count
     const uint32_t* pl = Wk.plan + (size_t)wb * PLAN_STRIDE;
-    static_assert(PLC_WORDS <= PLC_THREADS, "one bitmap word per lane");
-    const uint32_t plan_bits = threadIdx.x < (uint32_t)PLC_WORDS ? pl[threadIdx.x] : 0u;
+    static_assert(PW <= PLC_THREADS, "one bitmap word per lane");
+    const uint32_t plan_bits = threadIdx.x < (uint32_t)PW ? pl[threadIdx.x] : 0u;
     const uint32_t plan_pre =
-        threadIdx.x < (uint32_t)((PLC_WORDS + 1) / 2) ? pl[PLC_WORDS + threadIdx.x] : 0u;
+        threadIdx.x < (uint32_t)((PW + 1) / 2) ? pl[PW + threadIdx.x] : 0u;
     const uint32_t plan_nst = pl[PLAN_STRIDE - 1];
     // a run's absolute sample position is its (brick, scan) cell (absolute after k_compact) + its
     // rank.  The gather is issued here; for short rays (maxp <= 4) its value is first needed after
@@ -1109,8 +1111,9 @@ __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) v
     const bool ok = i < r1 && Walk<SEM>::init(R, D, t, i, px, py, pz, r);
     // sector sharding: a half block without a ray of this GPU's sector has no samples to place
     if (R.sec_on && !block_any<PLC_THREADS>(ok, s_vote[0])) return;
-    if (threadIdx.x < (uint32_t)PLC_WORDS) s_bits[threadIdx.x] = plan_bits;
-    if (threadIdx.x < (uint32_t)((PLC_WORDS + 1) / 2))
+    if constexpr (SEM == 3) s_w0[threadIdx.x] = ok ? r.w0 : 0.0f;
+    if (threadIdx.x < (uint32_t)PW) s_bits[threadIdx.x] = plan_bits;
+    if (threadIdx.x < (uint32_t)((PW + 1) / 2))
         reinterpret_cast<uint32_t*>(s_wpre)[threadIdx.x] = plan_pre;
 #ifdef TSDF_PLC_PHASE
     if (threadIdx.x == 0) pt[1] = clock64();
@@ -1235,8 +1238,7 @@ __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) v
                 const bool staged = lpos + w < (uint32_t)STG;
                 if (STAGE && st && staged) {
                     st_s[lpos + w] = s;
-                    st_l[lpos + w] = (uint16_t)l;
-                    if constexpr (SEM == 3) st_w[lpos + w] = vb_weight(R, rs.w0, s);
+                    st_l[lpos + w] = (StL)(SEM == 3 ? l | (threadIdx.x << 9) : l);
                 } else if (st && !staged) {
                     if constexpr (DIRECT) {
                         if (pos != NO_PAIR && pos + w < Wk.max_smp) {
@@ -1278,8 +1280,7 @@ __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) v
                         const uint32_t l = ((r.vz & 7) << 6) | ((r.vy & 7) << 3) | (r.vx & 7);
                         if (lpos != NO_PAIR && lpos + w < (uint32_t)STG) {
                             st_s[lpos + w] = s;
-                            st_l[lpos + w] = (uint16_t)l;
-                            if constexpr (SEM == 3) st_w[lpos + w] = vb_weight(R, r.w0, s);
+                            st_l[lpos + w] = (StL)(SEM == 3 ? l | (threadIdx.x << 9) : l);
                         } else if (pos != NO_PAIR && pos + w < Wk.max_smp) {
                             Wk.smp[pos + w] = make_uint2(__float_as_uint(s), (t << 9) | l);
                             if constexpr (SEM == 3) Wk.smw[pos + w] = vb_weight(R, r.w0, s);
@@ -1325,8 +1326,11 @@ __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) v
         if (b != NO_PAIR) {
             const uint32_t dst = b + (j - s_loff[slot]);
             if (dst < Wk.max_smp) {
-                Wk.smp[dst] = make_uint2(__float_as_uint(st_s[j]), (t << 9) | st_l[j]);
-                if constexpr (SEM == 3) Wk.smw[dst] = st_w[j];
+                const uint32_t sl = st_l[j];
+                Wk.smp[dst] = make_uint2(__float_as_uint(st_s[j]), (t << 9) | (sl & 511u));
+#ifndef TSDF_ABLATE_PL_NOSMW  // diagnostic build: no per-sample weight stores (wrong results)
+                if constexpr (SEM == 3) Wk.smw[dst] = vb_weight(R, s_w0[sl >> 9], st_s[j]);
+#endif
             }
         }
     }
@@ -1438,9 +1442,10 @@ static int grid_for(uint64_t items, int per_block, int cap) {
 hipError_t launch_count(const float* d_xyz, const BatchRef& D, const RayConst& R, const Table& T,
                         const Work& Wk, Globals* G, int parity, hipStream_t st, const KTime& kt,
                         bool wide, bool paired) {
-    // sem 3 (Voxblox 1/z^2) counts with Walk<1>: the weight only matters where it is stored
+    // sem 3 (Voxblox 1/z^2) walks as Walk<1> (Walk<3> derives from it); its own instantiation
+    // plans k_place<3>'s larger staging
     if (wide) {  // a batch too small to fill the chip: 1024-lane workgroups
-        auto k = R.sem == 1 || R.sem == 3 ? k_count<1, 1024> : R.sem == 2 ? k_count<2, 1024> : k_count<0, 1024>;
+        auto k = R.sem == 3 ? k_count<3, 1024> : R.sem == 1 ? k_count<1, 1024> : R.sem == 2 ? k_count<2, 1024> : k_count<0, 1024>;
 #ifndef TSDF_CNT_SPLIT
         tlaunch(k, D.n_blocks, 1024, st, kt.start, kt.stop, d_xyz, D, R, T, Wk, G, parity);
 #else
@@ -1448,10 +1453,10 @@ hipError_t launch_count(const float* d_xyz, const BatchRef& D, const RayConst& R
 #endif
     } else if (paired) {  // two blocks per 512-lane workgroup (no sector sharding)
         constexpr int NT2 = 2 * CNT_THREADS;
-        auto k = R.sem == 1 || R.sem == 3 ? k_count<1, NT2, 2> : R.sem == 2 ? k_count<2, NT2, 2> : k_count<0, NT2, 2>;
+        auto k = R.sem == 3 ? k_count<3, NT2, 2> : R.sem == 1 ? k_count<1, NT2, 2> : R.sem == 2 ? k_count<2, NT2, 2> : k_count<0, NT2, 2>;
         tlaunch(k, (D.n_blocks + 1) / 2, NT2, st, kt.start, kt.stop, d_xyz, D, R, T, Wk, G, parity);
     } else {
-        auto k = R.sem == 1 || R.sem == 3 ? k_count<1> : R.sem == 2 ? k_count<2> : k_count<0>;
+        auto k = R.sem == 3 ? k_count<3> : R.sem == 1 ? k_count<1> : R.sem == 2 ? k_count<2> : k_count<0>;
 #ifndef TSDF_CNT_SPLIT
         tlaunch(k, D.n_blocks, CNT_THREADS, st, kt.start, kt.stop, d_xyz, D, R, T, Wk, G, parity);
 #else

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 5: Voxblox workloads (1/z^2 simple = voxblox's default weight, const weight, merged) with
 # parity, rocprof kernel stats of simple and merged, and the A/B of the sem-3 capacity knobs
-# (old3: round-4 staging 5600 / window 6 per thread).  Logs under gpurun_out/r05/<tag>/.
+# .  Logs under gpurun_out/r05/<tag>/.
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/r05/${1:-modes}
@@ -15,9 +15,9 @@ run voxblox_simple --semantics voxblox
 run voxblox_const --semantics voxblox --const-weight
 run voxblox_merged --semantics voxblox --method merged
 run headline
-TSDF_HIP_LIB=noetic-slam_amd/lib/var/libtsdf_hip_old3.so run voxblox_simple_old3 --semantics voxblox
 for m in simple merged; do
   a="--semantics voxblox"; [ $m = merged ] && a="$a --method merged"
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_$m -o run -- python3 bench.py --no-cpu --steps 16 --warmup 2 $a > $O/prof_$m.log 2>&1 || { tail -5 $O/prof_$m.log; exit 1; }
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$m -o run -- python3 bench.py --no-cpu --steps 16 --warmup 2 $a > $O/prof_$m.log 2>&1 || { tail -5 $O/prof_$m.log; exit 1; }
+  f=$(find $O/prof_$m -name "*kernel_stats.csv" | head -1)
+  cp "$f" $O/kernel_stats_$m.csv && rm -rf $O/prof_$m
 done
-find $O -name "*kernel_stats.csv" | head
