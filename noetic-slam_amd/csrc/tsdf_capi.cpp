@@ -787,21 +787,16 @@ static int grow_smp(tsdf_ctx* c) {
     const uint64_t ns = std::min<uint64_t>(2ull * c->Wk.max_smp, smp_limit(c));
     if (ns <= c->Wk.max_smp) return fail(c, TSDF_ENOMEM, "sample list at its limit");
     uint2* f[2] = {nullptr, nullptr};
-    float* fw[2] = {nullptr, nullptr};  // sem 3: the samples' weights
-    hipError_t e = hipMalloc(&f[0], ns * sizeof(uint2));
-    if (e == hipSuccess) e = hipMalloc(&f[1], ns * sizeof(uint2));
-    for (int q = 0; q < 2 && e == hipSuccess && c->R.sem == 3; q++) e = hipMalloc(&fw[q], ns * sizeof(float));
+    hipError_t e = hipMalloc(&f[0], ns * smp_bytes(c->R.sem));
+    if (e == hipSuccess) e = hipMalloc(&f[1], ns * smp_bytes(c->R.sem));
     if (e != hipSuccess) {
         (void)hipGetLastError();
         for (auto q : f) if (q) (void)hipFree(q);
-        for (auto q : fw) if (q) (void)hipFree(q);
         return fail(c, TSDF_ENOMEM, "sample list allocation failed");
     }
     for (int q = 0; q < 2; q++) {
         (void)hipFree(c->W2[q].smp);
-        if (c->W2[q].smw) (void)hipFree(c->W2[q].smw);
         c->W2[q].smp = f[q];
-        c->W2[q].smw = fw[q];
         c->W2[q].max_smp = (uint32_t)ns;
     }
     c->Wk.max_smp = (uint32_t)ns;
@@ -1122,7 +1117,7 @@ void tsdf_destroy(tsdf_ctx* c) {
                    c->W2[0].ord_hist, c->W2[1].ord_hist,    c->W2[1].pair,    c->W2[1].blk,
                    c->W2[1].blk_n, c->W2[1].fb,        c->W2[1].smp,     c->W2[1].active,
                    c->W2[0].cagg,    c->W2[1].cagg,      c->W2[0].act,     c->W2[1].act,
-                   c->W2[0].spn,     c->W2[1].spn,       c->W2[0].smw,     c->W2[1].smw,
+                   c->W2[0].spn,     c->W2[1].spn,
                    c->W2[0].plan,    c->W2[1].plan,      c->W2[0].rsv,     c->W2[1].rsv,
                    c->W2[0].rsv_n,   c->W2[1].rsv_n};
     for (void* d : dev)
@@ -1281,8 +1276,7 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
         HIPCHK(c, hipMalloc(&W.rsv_n, (size_t)c->max_blocks * sizeof(uint32_t)));
 #endif
         HIPCHK(c, hipMalloc(&W.fb, (size_t)W.max_fb * sizeof(uint4)));
-        HIPCHK(c, hipMalloc(&W.smp, (size_t)W.max_smp * sizeof(uint2)));
-        if (c->R.sem == 3) HIPCHK(c, hipMalloc(&W.smw, (size_t)W.max_smp * sizeof(float)));
+        HIPCHK(c, hipMalloc(&W.smp, (size_t)W.max_smp * smp_bytes(c->R.sem)));
         HIPCHK(c, hipMalloc(&W.spn, (size_t)W.max_spn * sizeof(uint32_t)));
         // (slice, size class) histogram, then first positions (k_compact; zero between batches)
         HIPCHK(c, hipMalloc(&W.ord_hist, 2 * 64 * 32 * sizeof(uint32_t)));

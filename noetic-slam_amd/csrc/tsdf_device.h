@@ -123,8 +123,8 @@ struct RayConst {
     // GetVoxelCenter's half voxel, precomputed so the walk reads it as a scalar kernel argument
     // (formed per voxel it cost a double multiply and two readfirstlanes at every DDA step)
     double hvs_d, inv_s_d, gate_d2;
-    // Voxblox 1/z^2 sample weights (tsdf_params.depth_weight; sem 3 internally, with per-sample
-    // weights in Work::smw)
+    // Voxblox 1/z^2 sample weights (tsdf_params.depth_weight; sem 3 internally, each sample record
+    // carrying its weight: smp_store / smp_load)
     int depth_w;
     float w0_cap;  // cap of a sample's 1/z^2 weight: min(max_weight, 2^16) (TSDF_W0_CAP)
     // Voxblox MergedTsdfIntegrator (tsdf_params.voxblox_method; sem 3): per ray slot of the
@@ -204,8 +204,8 @@ struct Work {
     uint32_t* blk_n; // n_blocks * 2: runs in each list
     uint32_t* plan;  // n_blocks * 2 * PLAN_STRIDE: k_place's staging plan per half (k_count)
     uint4* fb;       // fallback pairs: (tidx, scan, rank, 0)
-    uint2* smp;  // x = truncated sdf (f32 bits), y = scan << 9 | local voxel
-    float* smw;  // Voxblox 1/z^2 (sem 3): each sample's weight, same index as smp
+    uint2* smp;  // x = truncated sdf (f32 bits), y = scan << 9 | local voxel; Voxblox 1/z^2 (sem 3):
+                 // 12-B records (x, y, weight f32 bits), smp_store / smp_load
     uint4* active;  // (h, slot, toff, cnt) per active brick (k_compact)
     uint4* active_ord;  // the same records, largest size class first (k_order; k_integrate's list)
     uint32_t* ord_hist; // per (slice, size class): counts [64][32], then first positions [64][32]
@@ -221,6 +221,27 @@ struct Work {
     uint32_t max_smp;     // capacity of smp
     uint32_t max_spn;     // capacity of spn
 };
+
+// Sample records: 8 B (sdf bits, scan << 9 | voxel); Voxblox 1/z^2 (sem 3) 12 B with the sample's
+// weight, one store and one load per sample instead of a parallel weight array (round 5)
+constexpr size_t smp_bytes(int sem) { return sem == 3 ? 12 : 8; }
+template <int SEM>
+__device__ __forceinline__ void smp_store(const Work& W, uint32_t i, float s, uint32_t tl, float w) {
+    if constexpr (SEM == 3)
+        reinterpret_cast<uint3*>(W.smp)[i] = make_uint3(__float_as_uint(s), tl, __float_as_uint(w));
+    else
+        W.smp[i] = make_uint2(__float_as_uint(s), tl);
+}
+template <int SEM>
+__device__ __forceinline__ uint2 smp_load(const Work& W, uint32_t i, float& w) {
+    if constexpr (SEM == 3) {
+        const uint3 v = reinterpret_cast<const uint3*>(W.smp)[i];
+        w = __uint_as_float(v.z);
+        return make_uint2(v.x, v.y);
+    } else {
+        return W.smp[i];
+    }
+}
 
 // per-batch counters, double-buffered by batch parity (zeroed by k_finish at the end of a batch)
 struct Counters {

@@ -96,7 +96,7 @@ __global__ __launch_bounds__(INT_THREADS, TSDF_INT_WAVES) void k_integrate(Batch
     constexpr int PER = SEM == 3 ? TSDF_INT_PER3 : INT_PER;  // register-cached samples per thread
     constexpr uint32_t CAP = PER * INT_THREADS;                // samples (>= live cells) per window
     constexpr int NSLOT = FUSED ? INT_SPT * SPAN : PER;  // register-cached samples per thread
-    constexpr bool VB = SEM == 1 || SEM == 3;  // Voxblox fuse (3: per-sample weights in Work::smw)
+    constexpr bool VB = SEM == 1 || SEM == 3;  // Voxblox fuse (3: per-sample weights in the records)
     constexpr int NW = SEM == 3 ? NSLOT : 1;    // register-cached sample weights per thread
     typedef typename std::conditional<VB, unsigned long long, uint32_t>::type CellB;
     __shared__ unsigned long long cA[CAP];  // live cell: sum of trunc(s w * 2^32)
@@ -171,8 +171,9 @@ __global__ __launch_bounds__(INT_THREADS, TSDF_INT_WAVES) void k_integrate(Batch
             for (int j = 0; j < PER; j++) {
                 const uint32_t i = tid + j * INT_THREADS;
                 // base + i >= max_smp: capacity overflow (reported by k_compact)
-                B.c[j] = (i < n && base + i < Wk.max_smp) ? Wk.smp[base + i] : make_uint2(0u, ~0u);
-                if constexpr (SEM == 3) B.cw[j] = (i < n && base + i < Wk.max_smp) ? Wk.smw[base + i] : 0.0f;
+                float wv = 0.0f;
+                B.c[j] = (i < n && base + i < Wk.max_smp) ? smp_load<SEM>(Wk, base + i, wv) : make_uint2(0u, ~0u);
+                if constexpr (SEM == 3) B.cw[j] = wv;
             }
         }
         // two walks: absolute position of the brick's scan-tid samples -> relative to its segment
@@ -240,8 +241,9 @@ __global__ __launch_bounds__(INT_THREADS, TSDF_INT_WAVES) void k_integrate(Batch
 #pragma unroll
                 for (int j = 0; j < PER; j++) {
                     const uint32_t i = q + tid + j * INT_THREADS;
-                    c[j] = (i < n && base + i < Wk.max_smp) ? Wk.smp[base + i] : make_uint2(0u, ~0u);
-                    if constexpr (SEM == 3) cw[j] = (i < n && base + i < Wk.max_smp) ? Wk.smw[base + i] : 0.0f;
+                    float wv = 0.0f;
+                    c[j] = (i < n && base + i < Wk.max_smp) ? smp_load<SEM>(Wk, base + i, wv) : make_uint2(0u, ~0u);
+                    if constexpr (SEM == 3) cw[j] = wv;
                 }
             }
         };
@@ -615,8 +617,9 @@ __global__ __launch_bounds__(SML_WAVES * 64) void k_integrate_small(BatchRef D, 
         for (int j = 0; j < SML_K; j++) {
             const uint32_t i = lane + 64 * j;
             const bool ok = i < n && base + i < Wk.max_smp;  // past max_smp: overflow (k_compact)
-            P.c[j] = ok ? Wk.smp[base + i] : make_uint2(0u, 0u);
-            if constexpr (SEM == 3) P.cw[j] = ok ? Wk.smw[base + i] : 0.0f;
+            float wv = 0.0f;
+            P.c[j] = ok ? smp_load<SEM>(Wk, base + i, wv) : make_uint2(0u, 0u);
+            if constexpr (SEM == 3) P.cw[j] = wv;
         }
     };
     auto add = [&](uint2 c, float wv_stored) {
@@ -669,7 +672,9 @@ __global__ __launch_bounds__(SML_WAVES * 64) void k_integrate_small(BatchRef D, 
             }
             for (uint32_t i = max(q0, 64u * SML_K) + lane; i < q1; i += 64) {  // past the cache
                 if (base + i >= Wk.max_smp) continue;
-                add(Wk.smp[base + i], SEM == 3 ? Wk.smw[base + i] : 0.0f);
+                float wv = 0.0f;
+                const uint2 cs = smp_load<SEM>(Wk, base + i, wv);
+                add(cs, wv);
             }
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the cells complete
             __builtin_amdgcn_wave_barrier();

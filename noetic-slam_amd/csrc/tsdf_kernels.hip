@@ -1149,6 +1149,11 @@ __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) v
 #ifdef TSDF_PLC_PHASE
     if (threadIdx.x == 0) pt[3] = clock64();
 #endif
+    // Voxblox 1/z^2: a sample's weight (the ray's 1/z^2, then the dropoff); 0 for the others
+    auto sample_w = [&](const typename Walk<SEM>::State& st, float s) -> float {
+        if constexpr (SEM == 3) return vb_weight(R, st.w0, s);
+        else return 0.0f;
+    };
     // a pair code -> its samples' global position (when `with_pos`: s_base is filled), staging
     // position (lpos < STG), count
     auto resolve = [&](uint32_t code, bool with_pos, uint32_t& pos, uint32_t& lpos, uint32_t& cnt) {
@@ -1242,8 +1247,7 @@ __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) v
                 } else if (st && !staged) {
                     if constexpr (DIRECT) {
                         if (pos != NO_PAIR && pos + w < Wk.max_smp) {
-                            Wk.smp[pos + w] = make_uint2(__float_as_uint(s), (t << 9) | l);
-                            if constexpr (SEM == 3) Wk.smw[pos + w] = vb_weight(R, rs.w0, s);
+                            smp_store<SEM>(Wk, pos + w, s, (t << 9) | l, sample_w(rs, s));
                         }
                     } else {
                         ovf = true;
@@ -1282,8 +1286,7 @@ __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) v
                             st_s[lpos + w] = s;
                             st_l[lpos + w] = (StL)(SEM == 3 ? l | (threadIdx.x << 9) : l);
                         } else if (pos != NO_PAIR && pos + w < Wk.max_smp) {
-                            Wk.smp[pos + w] = make_uint2(__float_as_uint(s), (t << 9) | l);
-                            if constexpr (SEM == 3) Wk.smw[pos + w] = vb_weight(R, r.w0, s);
+                            smp_store<SEM>(Wk, pos + w, s, (t << 9) | l, sample_w(r, s));
                         }
                     }
                     w++;
@@ -1327,10 +1330,8 @@ __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) v
             const uint32_t dst = b + (j - s_loff[slot]);
             if (dst < Wk.max_smp) {
                 const uint32_t sl = st_l[j];
-                Wk.smp[dst] = make_uint2(__float_as_uint(st_s[j]), (t << 9) | (sl & 511u));
-#ifndef TSDF_ABLATE_PL_NOSMW  // diagnostic build: no per-sample weight stores (wrong results)
-                if constexpr (SEM == 3) Wk.smw[dst] = vb_weight(R, s_w0[sl >> 9], st_s[j]);
-#endif
+                smp_store<SEM>(Wk, dst, st_s[j], (t << 9) | (sl & 511u),
+                               SEM == 3 ? vb_weight(R, s_w0[sl >> 9], st_s[j]) : 0.0f);
             }
         }
     }

@@ -11,7 +11,8 @@
 //   k_mg_merge  one lane per sorted entry; the first entry of each (scan, key) run computes the
 //               bundle's running weighted mean of p - o (integrateVoxel's merge, in the run's
 //               order; a clearing bundle keeps its first kept point) and writes ONE ray -- o + mean,
-//               weight (negative: clearing) -- into the slot of the bundle's first point.
+//               weight (negative: clearing) -- into the slot of the bundle's first point; the
+//               run's entries are loaded MG_U at a time ahead of the sequential merge.
 // The walk kernels then run unchanged over the batch's slots (RayConst::ray_w), so block counts,
 // offsets and the ray layout stay those of the input; empty slots leave at the walk's init.
 #include <hip/hip_runtime.h>
@@ -72,6 +73,14 @@ __global__ __launch_bounds__(MG_THREADS) void k_mg_keys(const float* __restrict_
     }
 }
 
+// One lane per sorted entry; the lane at a (scan, key) run start merges the run.  The merge is a
+// sequential running mean (bit for bit integrateVoxel's), but its operands need not arrive one
+// dependent round trip at a time: the lane loads MG_U entries ahead (keys and indices contiguous,
+// then the points' (d, w) gathers, all in flight together) and merges them from registers, so a
+// long bundle (a near-range blob: thousands of points in one voxel) costs ~MG_U times fewer
+// memory round trips.  A run ends at the next key or at the first point of a later scan (the sort
+// is stable and a batch's points are in scan order, so the run's indices stay below the scan's end).
+constexpr int MG_U = 8;
 __global__ __launch_bounds__(MG_THREADS) void k_mg_merge(BatchRef D, MgBufs M, uint32_t n) {
     const uint32_t j = blockIdx.x * MG_THREADS + threadIdx.x;
     if (j >= n) return;
@@ -79,19 +88,37 @@ __global__ __launch_bounds__(MG_THREADS) void k_mg_merge(BatchRef D, MgBufs M, u
     if (key == ~0ull) return;
     const uint32_t i0 = M.idx2[j];
     const uint32_t t = M.sid[i0];
-    if (j > 0 && M.key2[j - 1] == key && M.sid[M.idx2[j - 1]] == t) return;  // not a run start
+    const uint32_t lo = D.s[t].off, hi = D.s[t + 1].off;  // scan t's points
+    if (j > 0 && M.key2[j - 1] == key && M.idx2[j - 1] >= lo) return;  // not a run start
     const bool clearing = (key >> 63) != 0;
     float mx = 0.0f, my = 0.0f, mz = 0.0f, mw = 0.0f;
-    for (uint32_t q = j; q < n && M.key2[q] == key; q++) {
-        const uint32_t i = M.idx2[q];
-        if (M.sid[i] != t) break;
-        const float4 d = M.dw[i];
-        if (d.w < 1e-6f || (clearing && mw > 0.0f)) continue;  // kEpsilon; clearing: first only
-        const float nw = mw + d.w;
-        mx = (mx * mw + d.x * d.w) / nw;
-        my = (my * mw + d.y * d.w) / nw;
-        mz = (mz * mw + d.z * d.w) / nw;
-        mw = mw + d.w;
+    for (uint32_t q = j;; q += MG_U) {
+        uint64_t kk[MG_U];
+        uint32_t ii[MG_U];
+#pragma unroll
+        for (int u = 0; u < MG_U; u++) {
+            const bool in = q + u < n;
+            kk[u] = in ? M.key2[q + u] : ~key;
+            ii[u] = in ? M.idx2[q + u] : hi;
+        }
+        float4 dd[MG_U];
+#pragma unroll
+        for (int u = 0; u < MG_U; u++)
+            dd[u] = (kk[u] == key && ii[u] < hi) ? M.dw[ii[u]] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        bool end = false;
+#pragma unroll
+        for (int u = 0; u < MG_U; u++) {
+            end = end || kk[u] != key || ii[u] >= hi;
+            const float4 d = dd[u];
+            // kEpsilon; a clearing bundle keeps its first kept point only
+            if (end || d.w < 1e-6f || (clearing && mw > 0.0f)) continue;
+            const float nw = mw + d.w;
+            mx = (mx * mw + d.x * d.w) / nw;
+            my = (my * mw + d.y * d.w) / nw;
+            mz = (mz * mw + d.z * d.w) / nw;
+            mw = mw + d.w;
+        }
+        if (end) break;
     }
     if (!(mw > 0.0f)) return;
     M.xyz_out[3 * (size_t)i0] = D.s[t].ox + mx;

@@ -437,7 +437,7 @@ struct Walk<1> {  // TSDF_SEM_VOXBLOX
 };
 
 // Voxblox with the 1/z^2 weight (internal sem 3): the same walk; k_place stores every sample's
-// weight (Work::smw) because k_integrate cannot recompute it from the sample
+// weight in its 12-B record (smp_store) because k_integrate cannot recompute it from the sample
 template <>
 struct Walk<3> : Walk<1> {};
 
