@@ -1127,7 +1127,7 @@ void tsdf_destroy(tsdf_ctx* c) {
         if (c->stage_done[i]) (void)hipEventDestroy(c->stage_done[i]);
         MgBufs& M = c->mg[i];
         for (void* q : {(void*)M.key, (void*)M.key2, (void*)M.idx, (void*)M.idx2, (void*)M.dw,
-                        (void*)M.sid, (void*)M.xyz_out, (void*)M.w_out, M.tmp})
+                        (void*)M.sid, (void*)M.xyz_out, (void*)M.w_out, M.tmp, (void*)M.tab})
             if (q) (void)hipFree(q);
     }
     if (c->bc_ev) (void)hipEventDestroy(c->bc_ev);
@@ -1288,8 +1288,11 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
             const uint64_t n = c->batch_points;
             M.cap = n;
             M.tmp_bytes = mg_sort_scratch(n);
-            HIPCHK(c, hipMalloc(&M.key, n * 8));
-            HIPCHK(c, hipMalloc(&M.key2, n * 8));
+            M.tab_bits = mg_tab_bits(n);
+            HIPCHK(c, hipMalloc(&M.tab, (size_t)8 << M.tab_bits));
+            HIPCHK(c, hipMemset(M.tab, 0, (size_t)8 << M.tab_bits));  // every slot empty (key 0)
+            HIPCHK(c, hipMalloc(&M.key, n * 4));
+            HIPCHK(c, hipMalloc(&M.key2, n * 4));
             HIPCHK(c, hipMalloc(&M.idx, n * 4));
             HIPCHK(c, hipMalloc(&M.idx2, n * 4));
             HIPCHK(c, hipMalloc(&M.dw, n * sizeof(float4)));

@@ -403,16 +403,21 @@ hipError_t launch_halo_build(const Table& H, const Pool& HP, const uint32_t* d_t
 // every scan bundled by voxel; xyz_out / w_out hold one ray per bundle at its first point's slot
 // (other slots: NaN point, weight 0), so the batch keeps its ray layout and block counts
 struct MgBufs {
-    uint64_t *key = nullptr, *key2 = nullptr;
+    uint32_t *key = nullptr, *key2 = nullptr;  // the point's bundle id (its voxel's slot in tab)
     uint32_t *idx = nullptr, *idx2 = nullptr;
     float4* dw = nullptr;     // p - o and the point's getVoxelWeight
-    uint16_t* sid = nullptr;  // the point's scan in the batch
+    uint16_t* sid = nullptr;  // the point's scan in the batch | clearing << 15
     float* xyz_out = nullptr;
     float* w_out = nullptr;
     void* tmp = nullptr;      // radix-sort scratch
     size_t tmp_bytes = 0;
     uint64_t cap = 0;         // points
+    // voxel key -> bundle id: open addressing over 2^tab_bits >= 2 cap slots (EMPTY between
+    // batches: k_mg_merge empties the slots it used)
+    uint64_t* tab = nullptr;
+    uint32_t tab_bits = 0;
 };
+uint32_t mg_tab_bits(uint64_t n_points);
 size_t mg_sort_scratch(uint64_t n_points);
 hipError_t launch_mg_prepass(const float* d_xyz, const BatchRef& B, uint32_t n_blocks,
                              uint64_t n_points, const RayConst& R, MgBufs& M, hipStream_t st);
