@@ -14,8 +14,8 @@ for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_
            "SQ_INSTS_FLAT SQ_LDS_BANK_CONFLICT SQ_INSTS_SMEM" \
            "SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $grp --kernel-include-regex "tsdf::" --output-format csv -d "$OUT/p$i" -o pmc -- $CMD \
-    > "$OUT/p$i.log" 2>&1 || { echo "pass $i ($grp) failed"; tail -5 "$OUT/p$i.log"; }
+  timeout -s KILL 200 rocprofv3 --pmc $grp --kernel-include-regex "tsdf::" --output-format csv -d "$OUT/p$i" -o pmc -- $CMD \
+    > "$OUT/p$i.log" 2>&1 || { rc=$?; echo "pass $i ($grp) failed rc=$rc"; tail -5 "$OUT/p$i.log"; [ $rc -ge 124 ] && exit 1; }
 done
 python3 profiles/summarize_pmc.py "$OUT" > "$OUT/summary.txt" || true
 rm -rf "$OUT"/p[0-9]*/
