@@ -87,3 +87,18 @@ def test_traffic_file_is_used_only_for_its_own_build(tmp_path, monkeypatch):
     val, src = bench.read_traffic(str(bad), "count")
     assert val is None and src["error"] == "unreadable"
 
+
+
+def test_voxblox_method_and_weight_options(monkeypatch):
+    """`--semantics voxblox --method merged` and `--const-weight` (round 5) reach
+    the bench's arguments; the defaults are Simple with 1/z^2 weights, and a bad method is refused."""
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--semantics", "voxblox", "--method", "merged",
+                                      "--const-weight"])
+    a = bench.parse()
+    assert (a.semantics, a.method, a.const_weight) == ("voxblox", "merged", True)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--semantics", "voxblox"])
+    a = bench.parse()
+    assert (a.method, a.const_weight) == ("simple", False)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--method", "fast"])
+    with pytest.raises(SystemExit):
+        bench.parse()
