@@ -58,3 +58,43 @@ def test_bench_settings_bitwise(bench_scans, pipeline, semantics):
     assert np.array_equal(gw.view(np.uint32), ow.view(np.uint32))
     bad = np.count_nonzero(gs.view(np.uint32) != os_.view(np.uint32))
     assert bad == 0, "%d sdf mismatches" % bad
+
+
+@pytest.mark.parametrize("method", ["simple", "merged"])
+def test_bench_voxblox_settings_bitwise(method):
+    """`bench.py --semantics voxblox [--method merged]` (round 5): 64 full scans with their
+    7-element poses (the 1/z^2 weight's sensor axis) as one device batch, pipelined -- the 12-B
+    sample records carrying the weights and the Merged pre-pass (hashed bundle ids) at the bench's
+    scale, bit for bit against the oracle."""
+    import math
+    import torch
+    from tsdf_map import HipTSDFVolume
+    from tsdf_map.scan_gen import TorchOusterSim, pose_on_circle
+    sim = TorchOusterSim(torch.device("cuda", 0))
+    parts, offs, poses = [], [0], []
+    for j in range(64):
+        k = 2000 + j
+        p, o = sim.scan(k)
+        yaw = pose_on_circle(k)[1]
+        parts.append(p)
+        offs.append(offs[-1] + p.shape[0])
+        poses.append(np.concatenate([o, [0.0, 0.0, math.sin(yaw / 2), math.cos(yaw / 2)]]))
+    x = torch.cat(parts).contiguous()
+    offs, poses = np.array(offs, np.uint64), np.stack(poses)
+    torch.cuda.synchronize()
+    g = HipTSDFVolume(VS, TAU, max_points=1 << 17, max_bricks=1 << 20, max_batch=64, pipeline=2,
+                      semantics="voxblox", method=method, use_const_weight=False)
+    g.integrate_batch_device(x.data_ptr(), offs, poses)
+    ov = oracle.OracleTSDFVolume(VS, TAU, semantics="voxblox", method=method,
+                                 use_const_weight=False, threads=8)
+    xs = x.cpu().numpy()
+    for j in range(64):
+        ov.integrate(xs[offs[j]:offs[j + 1]], poses[j])
+    gi, gs, gw = g.export_voxels()
+    oi, os_, ow = ov.export_voxels()
+    assert gi.shape[0] > 2_000_000
+    assert gi.shape == oi.shape and np.array_equal(gi, oi)
+    assert np.array_equal(gw.view(np.uint32), ow.view(np.uint32))
+    bad = np.count_nonzero(gs.view(np.uint32) != os_.view(np.uint32))
+    assert bad == 0, "%d sdf mismatches" % bad
+    assert g.stats()["n_rays_total"] == ov.stats()["n_rays_total"]
