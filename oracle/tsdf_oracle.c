@@ -1114,24 +1114,82 @@ static int cmp_brick(const void* a, const void* b) {
     return 0;
 }
 
-/* unique bricks holding at least one voxel with W > 0, sorted by (z, y, x) */
+/* unique bricks holding at least one voxel with W > 0, sorted by (z, y, x): deduplicated through
+   an open-addressing set of brick indices first (one entry per brick, not per voxel), then sorted */
 static brick_ent* list_bricks(const tsdf_ctx* c, uint64_t* nb) {
     mt_collect(c);
-    brick_ent* e = (brick_ent*)malloc((c->n ? c->n : 1) * sizeof(brick_ent));
-    if (!e) return NULL;
-    uint64_t k = 0;
+    uint64_t cap = 1024, u = 0;
+    while (cap < 2 * (c->n / 64 + 1)) cap *= 2;
+    brick_ent* e = (brick_ent*)malloc(cap / 2 * sizeof(brick_ent));
+    uint32_t* set = (uint32_t*)malloc(cap * sizeof(uint32_t)); /* entry index + 1; 0 = free */
+    if (!e || !set) { free(e); free(set); return NULL; }
+    memset(set, 0, cap * sizeof(uint32_t));
     for (uint64_t i = 0; i < c->cap; i++) {
         const vox_t* v = &c->tab[i];
         if (!v->used || !(v->W > 0.0f)) continue;
-        e[k].b[0] = fdiv8(v->x); e[k].b[1] = fdiv8(v->y); e[k].b[2] = fdiv8(v->z);
-        k++;
+        const int32_t b[3] = {fdiv8(v->x), fdiv8(v->y), fdiv8(v->z)};
+        uint64_t h = mix3(b[0], b[1], b[2]) & (cap - 1);
+        for (;; h = (h + 1) & (cap - 1)) {
+            if (!set[h]) break;
+            const int32_t* q = e[set[h] - 1].b;
+            if (q[0] == b[0] && q[1] == b[1] && q[2] == b[2]) break;
+        }
+        if (set[h]) continue;
+        if (2 * (u + 1) > cap) { /* rehash into a set twice the size */
+            const uint64_t nc = 2 * cap;
+            brick_ent* ne = (brick_ent*)realloc(e, nc / 2 * sizeof(brick_ent));
+            uint32_t* ns = (uint32_t*)calloc(nc, sizeof(uint32_t));
+            if (!ne || !ns) { free(ne ? ne : e); free(ns); free(set); return NULL; }
+            e = ne;
+            for (uint64_t j = 0; j < u; j++) {
+                uint64_t g = mix3(e[j].b[0], e[j].b[1], e[j].b[2]) & (nc - 1);
+                while (ns[g]) g = (g + 1) & (nc - 1);
+                ns[g] = (uint32_t)(j + 1);
+            }
+            free(set);
+            set = ns;
+            cap = nc;
+            h = mix3(b[0], b[1], b[2]) & (cap - 1);
+            while (set[h]) h = (h + 1) & (cap - 1);
+        }
+        e[u].b[0] = b[0]; e[u].b[1] = b[1]; e[u].b[2] = b[2];
+        set[h] = (uint32_t)(++u);
     }
-    qsort(e, k, sizeof(brick_ent), cmp_brick);
-    uint64_t u = 0;
-    for (uint64_t i = 0; i < k; i++)
-        if (u == 0 || cmp_brick(&e[u - 1], &e[i]) != 0) e[u++] = e[i];
+    free(set);
+    qsort(e, u, sizeof(brick_ent), cmp_brick);
     *nb = u;
     return e;
+}
+
+/* index of the sorted brick list by brick coordinates: an open-addressing set of (index + 1) */
+typedef struct { uint32_t* slot; uint64_t cap; const brick_ent* e; } brick_index;
+
+static int brick_index_build(brick_index* x, const brick_ent* e, uint64_t nb) {
+    x->cap = 1024;
+    while (x->cap < 2 * nb) x->cap *= 2;
+    x->e = e;
+    x->slot = (uint32_t*)calloc(x->cap, sizeof(uint32_t));
+    if (!x->slot) return TSDF_ENOMEM;
+    for (uint64_t i = 0; i < nb; i++) {
+        uint64_t g = mix3(e[i].b[0], e[i].b[1], e[i].b[2]) & (x->cap - 1);
+        while (x->slot[g]) g = (g + 1) & (x->cap - 1);
+        x->slot[g] = (uint32_t)(i + 1);
+    }
+    return TSDF_OK;
+}
+
+/* the brick's index in the list, -1 when it is not listed */
+static int64_t brick_index_find(const brick_index* x, int32_t bx, int32_t by, int32_t bz) {
+    for (uint64_t g = mix3(bx, by, bz) & (x->cap - 1); x->slot[g]; g = (g + 1) & (x->cap - 1)) {
+        const int32_t* q = x->e[x->slot[g] - 1].b;
+        if (q[0] == bx && q[1] == by && q[2] == bz) return (int64_t)x->slot[g] - 1;
+    }
+    return -1;
+}
+
+/* in-brick index z*64 + y*8 + x of voxel (x, y, z) */
+static int vox_local(int32_t x, int32_t y, int32_t z) {
+    return ((z - 8 * fdiv8(z)) << 6) | ((y - 8 * fdiv8(y)) << 3) | (x - 8 * fdiv8(x));
 }
 
 int tsdf_num_bricks(tsdf_ctx* c, uint64_t* n) {
@@ -1155,11 +1213,23 @@ int tsdf_export_bricks(tsdf_ctx* c, int32_t* coords, float* sdf, float* weight, 
     for (uint64_t i = 0; i < nb; i++) {
         if (coords) { coords[3 * i] = e[i].b[0]; coords[3 * i + 1] = e[i].b[1]; coords[3 * i + 2] = e[i].b[2]; }
         for (int l = 0; l < 512; l++) {
-            const int lx = l & 7, ly = (l >> 3) & 7, lz = l >> 6;
-            const vox_t* v = vox_find(c, e[i].b[0] * 8 + lx, e[i].b[1] * 8 + ly, e[i].b[2] * 8 + lz);
-            if (sdf) sdf[512 * i + l] = v ? v->S : c->bg;
-            if (weight) weight[512 * i + l] = v ? v->W : 0.0f;
+            if (sdf) sdf[512 * i + l] = c->bg; /* absent voxels: the background */
+            if (weight) weight[512 * i + l] = 0.0f;
         }
+    }
+    if (nb && (sdf || weight)) { /* every stored voxel of a listed brick, in one pass over the table */
+        brick_index x;
+        if (brick_index_build(&x, e, nb)) { free(e); return TSDF_ENOMEM; }
+        for (uint64_t i = 0; i < c->cap; i++) {
+            const vox_t* v = &c->tab[i];
+            if (!v->used) continue;
+            const int64_t bi = brick_index_find(&x, fdiv8(v->x), fdiv8(v->y), fdiv8(v->z));
+            if (bi < 0) continue;
+            const uint64_t o = 512 * (uint64_t)bi + vox_local(v->x, v->y, v->z);
+            if (sdf) sdf[o] = v->S;
+            if (weight) weight[o] = v->W;
+        }
+        free(x.slot);
     }
     free(e);
     return TSDF_OK;
@@ -1623,15 +1693,9 @@ int tsdf_halo_keys_device(tsdf_ctx* c, uint64_t* keys, uint64_t cap, uint64_t* n
     uint64_t* have = (uint64_t*)malloc((nb ? nb : 1) * sizeof(uint64_t));
     uint64_t* need = (uint64_t*)malloc((nb ? 7 * nb : 1) * sizeof(uint64_t));
     if (!have || !need) { free(e); free(have); free(need); return TSDF_ENOMEM; }
-    /* observed bricks only: a reset copy of a brick owned elsewhere (W = 0 after a border reduce)
-       is requested like an absent one */
-    uint64_t nh = 0;
-    for (uint64_t i = 0; i < nb; i++)
-        if (brick_observed(c, e[i].b)) {
-            e[nh] = e[i];
-            have[nh++] = pack_key(e[i].b);
-        }
-    nb = nh;
+    /* observed bricks only (list_bricks lists the bricks with a W > 0 voxel): a reset copy of a
+       brick owned elsewhere (W = 0 after a border reduce) is requested like an absent one */
+    for (uint64_t i = 0; i < nb; i++) have[i] = pack_key(e[i].b);
     qsort(have, nb, sizeof(uint64_t), cmp_u64);
     uint64_t m = 0;
     for (uint64_t i = 0; i < nb; i++)
@@ -1661,12 +1725,20 @@ int tsdf_halo_pack_device(tsdf_ctx* c, const uint64_t* req, uint64_t n_req, uint
     *n_rows = 0;
     if (!n_req) return TSDF_OK;
     if (!req || !send) return set_err(c, TSDF_EINVAL, "null buffer");
+    /* the bricks observed here (a W > 0 voxel), as sorted keys */
+    uint64_t nb = 0;
+    brick_ent* e = list_bricks(c, &nb);
+    uint64_t* have = (uint64_t*)malloc((nb ? nb : 1) * sizeof(uint64_t));
+    if (!e || !have) { free(e); free(have); return TSDF_ENOMEM; }
+    for (uint64_t i = 0; i < nb; i++) have[i] = pack_key(e[i].b);
+    free(e);
+    qsort(have, nb, sizeof(uint64_t), cmp_u64);
     uint64_t row = 0;
     for (uint64_t i = 0; i < n_req; i++) {
         if (req[i] == ~0ull) continue;
+        if (!bsearch(&req[i], have, nb, sizeof(uint64_t), cmp_u64)) continue;
         int32_t b[3];
         key_brick(req[i], b);
-        if (!brick_observed(c, b)) continue;
         if (row < cap_rows) {
             uint32_t* t = send + row * TILE_WORDS;
             for (int l = 0; l < 512; l++) {
@@ -1678,6 +1750,7 @@ int tsdf_halo_pack_device(tsdf_ctx* c, const uint64_t* req, uint64_t n_req, uint
         }
         row++;
     }
+    free(have);
     *n_rows = row;
     return row > cap_rows ? set_err(c, TSDF_EOVERFLOW, "halo send buffer too small") : TSDF_OK;
 }
@@ -1809,32 +1882,6 @@ static int cmp_halo(const void* a, const void* b) {
     return x < y ? -1 : (x > y);
 }
 
-/* voxel (x, y, z): from its brick's halo tile when there is one, else the context's own voxel;
-   voxels of the brick being meshed (own = its key) always from the context itself */
-static int corner(const tsdf_ctx* c, const halo_ent* h, uint64_t nh, uint64_t own, int32_t x,
-                  int32_t y, int32_t z, float* S, float* W) {
-    if (nh) {
-        const int32_t b[3] = {fdiv8(x), fdiv8(y), fdiv8(z)};
-        if (pack_key(b) == own) nh = 0;
-    }
-    if (nh) {
-        const int32_t b[3] = {fdiv8(x), fdiv8(y), fdiv8(z)};
-        const halo_ent q = {pack_key(b), NULL};
-        const halo_ent* f = (const halo_ent*)bsearch(&q, h, nh, sizeof(halo_ent), cmp_halo);
-        if (f) {
-            const int l = ((z - 8 * b[2]) << 6) | ((y - 8 * b[1]) << 3) | (x - 8 * b[0]);
-            *S = ((const float*)f->tile)[l];
-            *W = ((const float*)f->tile)[512 + l];
-            return 1;
-        }
-    }
-    const vox_t* v = vox_find(c, x, y, z);
-    if (!v) return 0;
-    *S = v->S;
-    *W = v->W;
-    return 1;
-}
-
 static int mesh_impl(tsdf_ctx* c, float min_weight, int32_t table, const uint32_t* halo,
                      uint64_t n_halo, float* tri, uint64_t cap, uint64_t* n_tri) {
     if (!c || !n_tri) return TSDF_EINVAL;
@@ -1855,19 +1902,68 @@ static int mesh_impl(tsdf_ctx* c, float min_weight, int32_t table, const uint32_
     if (!e) { free(h); return TSDF_ENOMEM; }
     const float vs = c->vs;
     uint64_t nt = 0;
+    /* the observed voxels in dense per-brick tiles (one pass over the voxel table; brick i of the
+       sorted list at tile i), so a cube's corners are array reads instead of hash probes */
+    brick_index bx;
+    float* ts = (float*)calloc((nb ? nb : 1) * 512, sizeof(float));
+    float* tw = (float*)calloc((nb ? nb : 1) * 512, sizeof(float));
+    if (brick_index_build(&bx, e, nb) || !ts || !tw) {
+        free(bx.slot); free(ts); free(tw); free(e); free(h);
+        return TSDF_ENOMEM;
+    }
+    for (uint64_t i = 0; i < c->cap; i++) {
+        const vox_t* v = &c->tab[i];
+        if (!v->used || !(v->W > 0.0f)) continue;
+        const int64_t bi = brick_index_find(&bx, fdiv8(v->x), fdiv8(v->y), fdiv8(v->z));
+        const int l = vox_local(v->x, v->y, v->z);
+        ts[(uint64_t)bi * 512 + l] = v->S;
+        tw[(uint64_t)bi * 512 + l] = v->W;
+    }
+    /* the brick's 9^3 corner neighbourhood: its own voxels from its tile, a neighbour brick's from
+       its halo tile when there is one, else from its tile here (corner()'s precedence); cu[] =
+       usable (observed, W >= min_weight) */
+    float cs[729];
+    uint8_t cu[729];
     for (uint64_t b = 0; b < nb; b++) {
+        const int32_t x0 = e[b].b[0] * 8, y0 = e[b].b[1] * 8, z0 = e[b].b[2] * 8;
+        for (int d = 0; d < 8; d++) {
+            const int32_t nbk[3] = {e[b].b[0] + (d & 1), e[b].b[1] + ((d >> 1) & 1), e[b].b[2] + (d >> 2)};
+            const float *S = NULL, *W = NULL;
+            if (d == 0) {
+                S = ts + b * 512; W = tw + b * 512;
+            } else {
+                if (n_halo) {
+                    const halo_ent q = {pack_key(nbk), NULL};
+                    const halo_ent* f = (const halo_ent*)bsearch(&q, h, n_halo, sizeof(halo_ent), cmp_halo);
+                    if (f) { S = (const float*)f->tile; W = (const float*)f->tile + 512; }
+                }
+                if (!S) {
+                    const int64_t bi = brick_index_find(&bx, nbk[0], nbk[1], nbk[2]);
+                    if (bi >= 0) { S = ts + (uint64_t)bi * 512; W = tw + (uint64_t)bi * 512; }
+                }
+            }
+            /* the part of the 9^3 block this brick covers: local 0..7 (own) or 0 (neighbour side) */
+            const int nx = (d & 1) ? 1 : 8, ny = ((d >> 1) & 1) ? 1 : 8, nz = (d >> 2) ? 1 : 8;
+            for (int lz = 0; lz < nz; lz++)
+                for (int ly = 0; ly < ny; ly++)
+                    for (int lx = 0; lx < nx; lx++) {
+                        const int m = ((d >> 2) ? 8 : lz) * 81 + (((d >> 1) & 1) ? 8 : ly) * 9 + ((d & 1) ? 8 : lx);
+                        const int l = (lz << 6) | (ly << 3) | lx;
+                        const float wv = W ? W[l] : 0.0f;
+                        cu[m] = wv > 0.0f && wv >= min_weight;
+                        cs[m] = S ? S[l] : 0.0f;
+                    }
+        }
         for (int l = 0; l < 512; l++) {
-            const int32_t x = e[b].b[0] * 8 + (l & 7), y = e[b].b[1] * 8 + ((l >> 3) & 7),
-                          z = e[b].b[2] * 8 + (l >> 6);
+            const int32_t x = x0 + (l & 7), y = y0 + ((l >> 3) & 7), z = z0 + (l >> 6);
+            const int m0 = (l >> 6) * 81 + ((l >> 3) & 7) * 9 + (l & 7);
             float S[8];
             int ok = 1, k = 0;
             for (int q = 0; q < 8 && ok; q++) {
-                float sv = 0.0f, wv = 0.0f;
-                if (!corner(c, h, n_halo, pack_key(e[b].b), x + (q & 1), y + ((q >> 1) & 1),
-                            z + ((q >> 2) & 1), &sv, &wv) ||
-                    !(wv > 0.0f) || !(wv >= min_weight)) { ok = 0; break; }
-                S[q] = sv;
-                if (sv < 0.0f) k |= 1 << q;
+                const int m = m0 + ((q >> 2) & 1) * 81 + ((q >> 1) & 1) * 9 + (q & 1);
+                if (!cu[m]) { ok = 0; break; }
+                S[q] = cs[m];
+                if (S[q] < 0.0f) k |= 1 << q;
             }
             if (!ok) continue;
             const int ntc = mc_tab[k][0];
@@ -1891,6 +1987,7 @@ static int mesh_impl(tsdf_ctx* c, float min_weight, int32_t table, const uint32_
             }
         }
     }
+    free(bx.slot); free(ts); free(tw);
     free(e);
     free(h);
     *n_tri = nt;
