@@ -139,7 +139,7 @@ def test_gpu_f64_filter_stress(carving):
     scans = _filter_stress_scans()
     g = fill(HipTSDFVolume(0.05, 0.15, semantics="vdbfusion_f64", **kw), scans)
     g.sync()
-    o = fill(oracle.OracleTSDFVolume(0.05, 0.15, semantics="vdbfusion_f64", **kw), scans)
+    o = fill(oracle.OracleTSDFVolume(0.05, 0.15, semantics="vdbfusion_f64", threads=8, **kw), scans)
     r = compare(g.export_voxels(), o.export_voxels())
     print("f64 filter stress (carving=%s):" % carving, r)
     assert r["only_a"] == r["only_b"] == r["weight_mismatch"] == 0
