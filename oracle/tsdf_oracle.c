@@ -806,6 +806,18 @@ static int mt_integrate(tsdf_ctx* c, const char* base, uint64_t n, uint32_t poin
 static void mt_collect(const tsdf_ctx* cc) {
     tsdf_ctx* c = (tsdf_ctx*)cc;
     if (c->n_thr <= 1 || !c->mt_dirty) return;
+    /* sized once for the union (the partitions hold disjoint voxels), not grown insert by insert */
+    uint64_t total = 0, ncap = c->cap ? c->cap : (1u << 16);
+    for (int p = 0; p < c->n_thr; p++) total += c->sub[p]->n;
+    while (2 * (total + 1) > ncap) ncap *= 2;
+    if (ncap > c->cap && c->n_touched == 0) {
+        vox_t* nt = (vox_t*)calloc(ncap, sizeof(vox_t));
+        if (nt) {
+            free(c->tab);
+            c->tab = nt;
+            c->cap = ncap;
+        }
+    }
     if (c->cap) memset(c->tab, 0, c->cap * sizeof(vox_t));
     c->n = 0;
     for (int p = 0; p < c->n_thr; p++) {
@@ -1311,6 +1323,41 @@ static int cmp_vrec(const void* a, const void* b) {
     return 0;
 }
 
+/* (z, y, x) order of cmp_vrec by a stable LSD radix sort over the biased coordinates (|index| <
+   2^23: 24 bits each), x's bytes first; a byte every record shares is skipped (qsort when the
+   scratch buffer cannot be had) */
+static void sort_vrec(vrec* r, uint64_t n) {
+    vrec* tmp = n > 1 ? (vrec*)malloc(n * sizeof(vrec)) : NULL;
+    if (!tmp) {
+        if (n > 1) qsort(r, n, sizeof(vrec), cmp_vrec);
+        return;
+    }
+    vrec *src = r, *dst = tmp;
+    for (int pass = 0; pass < 9; pass++) {
+        const int axis = pass / 3, shift = 8 * (pass % 3);
+        uint64_t cnt[256] = {0};
+#define VREC_DIGIT(v) \
+    (((uint32_t)((axis == 0 ? (v).x : axis == 1 ? (v).y : (v).z) + VOX_LIMIT) >> shift) & 255u)
+        for (uint64_t i = 0; i < n; i++) cnt[VREC_DIGIT(src[i])]++;
+        int same = 0;
+        for (int d = 0; d < 256; d++) same |= cnt[d] == n;
+        if (same) continue;
+        uint64_t o = 0;
+        for (int d = 0; d < 256; d++) {
+            const uint64_t k = cnt[d];
+            cnt[d] = o;
+            o += k;
+        }
+        for (uint64_t i = 0; i < n; i++) dst[cnt[VREC_DIGIT(src[i])]++] = src[i];
+#undef VREC_DIGIT
+        vrec* t = src;
+        src = dst;
+        dst = t;
+    }
+    if (src != r) memcpy(r, src, n * sizeof(vrec));
+    free(tmp);
+}
+
 /* every voxel with W > 0, sorted by (z, y, x): ijk[3*i..], sdf[i], w[i] */
 int tsdf_oracle_export_voxels(const tsdf_ctx* c, int32_t* ijk, float* sdf, float* w, uint64_t cap,
                               uint64_t* n_out) {
@@ -1326,7 +1373,7 @@ int tsdf_oracle_export_voxels(const tsdf_ctx* c, int32_t* ijk, float* sdf, float
         r[k].x = v->x; r[k].y = v->y; r[k].z = v->z; r[k].S = v->S; r[k].W = v->W;
         k++;
     }
-    qsort(r, n, sizeof(vrec), cmp_vrec);
+    sort_vrec(r, n);
     for (uint64_t i = 0; i < n; i++) {
         ijk[3 * i] = r[i].x; ijk[3 * i + 1] = r[i].y; ijk[3 * i + 2] = r[i].z;
         sdf[i] = r[i].S;
