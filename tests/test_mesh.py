@@ -6,8 +6,9 @@ with the generated one below.  The generated table is pinned by what a correct m
 table must satisfy: the product library's table equals the oracle's
 independent construction; single-corner cases give one triangle on that corner's three edges;
 and the mesh of a closed analytic surface is watertight, consistently oriented, of Euler
-characteristic 2 and encloses the analytic volume.  The GPU mesh is then compared with the
-oracle's bit for bit (same triangles, same order).
+characteristic 2 and encloses the analytic volume.  The oracle's mesh itself (corner gather, halo
+tiles, min_weight) equals a plain numpy restatement bit for bit.  The GPU mesh is then compared with
+the oracle's bit for bit (same triangles, same order).
 """
 import ctypes as C
 import math
@@ -331,3 +332,78 @@ def test_gpu_scan_mesh_lorensen_bitwise(sim):
     vg, _ = g.extract_triangle_mesh(table="lorensen")
     assert vo.shape[0] > 1000
     assert vg.shape == vo.shape and np.array_equal(vg, vo)
+
+
+def numpy_marching_cubes(coords, sdf, weight, local, tab, vs, min_weight):
+    """An independent restatement of the oracle's mesh (oracle/tsdf_oracle.c mesh_impl) over a
+    dense grid: the cubes whose min voxel lies in a `local` brick, bricks in (z, y, x) order, cubes
+    by in-brick index, triangles in table order; vertex = corner a's centre + t vs along the edge,
+    t = S_a / (S_a - S_b), all in fp32."""
+    edges = [(b, b | (1 << d)) for d in range(3) for b in range(8) if not b & (1 << d)]
+    lo = coords.min(0) * 8
+    dim = (coords.max(0) - coords.min(0) + 2) * 8  # +1 brick of unobserved margin
+    S = np.zeros(dim[::-1], np.float32)
+    U = np.zeros(dim[::-1], bool)
+    for c, s, w in zip(coords, sdf.reshape(-1, 8, 8, 8), weight.reshape(-1, 8, 8, 8)):
+        o = c * 8 - lo
+        S[o[2]:o[2] + 8, o[1]:o[1] + 8, o[0]:o[0] + 8] = s
+        U[o[2]:o[2] + 8, o[1]:o[1] + 8, o[0]:o[0] + 8] = (w > 0) & (w >= min_weight)
+    vs32 = np.float32(vs)
+    out = []
+    order = np.lexsort((coords[local, 0], coords[local, 1], coords[local, 2]))
+    for c in coords[local][order]:
+        o = c * 8 - lo
+        for l in range(512):
+            x, y, z = o[0] + (l & 7), o[1] + ((l >> 3) & 7), o[2] + (l >> 6)
+            cs = [(x + (q & 1), y + ((q >> 1) & 1), z + (q >> 2)) for q in range(8)]
+            if not all(U[k[2], k[1], k[0]] for k in cs):
+                continue
+            sv = [S[k[2], k[1], k[0]] for k in cs]
+            case = sum(1 << q for q in range(8) if sv[q] < 0)
+            gx, gy, gz = (c[0] * 8 + (l & 7), c[1] * 8 + ((l >> 3) & 7), c[2] * 8 + (l >> 6))
+            for t in range(tab[case, 0]):
+                for j in range(3):
+                    a, b = edges[tab[case, 1 + 3 * t + j]]
+                    ax = {1: 0, 2: 1, 4: 2}[a ^ b]
+                    tt = np.float32(sv[a] / np.float32(sv[a] - sv[b]))
+                    p = [(np.float32(g + ((a >> i) & 1)) + np.float32(0.5)) * vs32
+                         for i, g in enumerate((gx, gy, gz))]
+                    p[ax] = np.float32(p[ax] + np.float32(tt * vs32))
+                    out.append(p)
+    return np.asarray(out, np.float32).reshape(-1, 3)
+
+
+@pytest.mark.parametrize("tname", ["generated", "lorensen"])
+@pytest.mark.parametrize("min_weight", [0.0, 0.75])
+@pytest.mark.parametrize("with_halo", [False, True])
+def test_oracle_mesh_equals_numpy_restatement(tname, min_weight, with_halo):
+    """Pins the oracle's marching cubes (its dense-tile corner gather, its halo precedence and the
+    min_weight rule) against the plain restatement above, bit for bit, on a sphere with holes,
+    low-weight voxels and, with_halo, the +x half of the bricks handed over as halo tiles."""
+    from tsdf_map import _abi
+    rng = np.random.default_rng(7)
+    coords, sdf, w = sphere_bricks(0.37)
+    sdf = (sdf + rng.normal(0, 0.004, sdf.shape)).astype(np.float32)
+    w = np.where(rng.random(w.shape) < 0.03, 0.0, np.where(rng.random(w.shape) < 0.05, 0.5, 1.0))
+    w = w.astype(np.float32)
+    local = coords[:, 0] < 1 if with_halo else np.ones(len(coords), bool)
+    o = oracle.OracleTSDFVolume(VS, TAU)
+    o.import_bricks(coords[local], sdf[local], w[local])
+    halo = None
+    tiles = np.zeros((int((~local).sum()), _abi.TILE_WORDS), np.uint32)
+    if with_halo:
+        for k, i in enumerate(np.nonzero(~local)[0]):
+            tiles[k, :512] = sdf[i].reshape(-1).view(np.uint32)
+            tiles[k, 512:1024] = w[i].reshape(-1).view(np.uint32)
+            key = sum(int(coords[i, a] + (1 << 20)) << (21 * a) for a in range(3))
+            tiles[k, 1024], tiles[k, 1025] = key & 0xFFFFFFFF, key >> 32
+        halo = (tiles.ctypes.data, tiles.shape[0])
+    verts, _ = o.extract_triangle_mesh(min_weight=min_weight, table=tname, halo=halo)
+    buf = (C.c_uint8 * (256 * 32))()
+    assert oracle.load().tsdf_mc_table_of(_abi.MC_TABLES[tname], buf) == 0
+    tab = np.frombuffer(buf, np.uint8).reshape(256, 32)
+    ref = numpy_marching_cubes(coords, sdf, w, local, tab, VS, min_weight)
+    assert ref.shape[0] > 300
+    assert verts.shape == ref.shape and np.array_equal(verts.view(np.uint32), ref.view(np.uint32))
+    if with_halo:  # the halo is what meshes the cubes on the local / halo border
+        assert o.extract_triangle_mesh(min_weight=min_weight, table=tname)[0].shape[0] < ref.shape[0]
