@@ -4,11 +4,14 @@
 A step integrates one batch of synthetic scans that are already resident in HBM (the C1/M1
 workload of SURVEY.md §8d: OS-1-128 1024x10 beams, analytic scene, circular trajectory at 10 Hz,
 5 cm voxels, 15 cm truncation, no carving), scan after scan, through libtsdf_hip.so's
-tsdf_integrate_batch_device.  Multi-GPU (one process per GPU, torch.distributed over RCCL): every
-rank holds every FULL scan of the step and integrates its azimuth sector of each (the sector
-filter runs inside the walk kernels, in the timed region: tsdf_params.n_sectors / sector) into its
-own partial field (weak scaling: a step of N GPUs holds N * batch scans, each rank's share is
-`batch` scans' worth of rays); no collective runs on the data path — the device-resident
+tsdf_integrate_batch_device.  Multi-GPU (one process per GPU, torch.distributed over RCCL): rank k
+integrates sector k of every scan of the step into its own partial field (tsdf_params.n_sectors /
+sector; weak scaling: a step of N GPUs holds N * batch scans, each rank's share is `batch` scans'
+worth of rays).  The default sector rule (ABI v10) is the index rule: sector k is the
+contiguous k-th 1/N of each scan's points -- the scans are in DLIO's time order, so a column
+(azimuth) range of the spin -- and the rank's kernels read only that share; `--sector-rule world`
+runs the world-frame pseudo-angle rule, where every rank reads every point and its walk kernels
+drop the other sectors' rays.  No collective runs on the data path — the device-resident
 border-brick reduce over RCCL (tsdf_map.distributed.border_reduce) is a read-out operation, timed
 separately (readout_merge_ms).
 
@@ -84,6 +87,10 @@ def parse():
                          "(rehearsal of the scaling runs on a one-GPU box)")
     ap.add_argument("--rehearsal-sector", type=int, default=0, metavar="K",
                     help="with --rank-rehearsal N: play rank K (sector K of N) instead of rank 0")
+    ap.add_argument("--sector-rule", default="index", choices=("index", "world"),
+                    help="tsdf_params.sector_rule with N > 1 shards: index (default; contiguous "
+                         "1/N of each scan's points, i.e. sensor-frame column sectors) or world "
+                         "(world-frame pseudo-angle sectors, every rank reads every point)")
     ap.add_argument("--walk", default="two", choices=("two", "single"),
                     help="front end (tsdf_params.walk): two = k_count + k_place (default); single = "
                          "every ray walked once (k_walk + k_spans) when the band allows it")
@@ -294,7 +301,7 @@ def main():
                              n_sectors=n_shards,  # this rank's azimuth sector of every scan
                              sector=(args.rehearsal_sector % n_shards if world == 1 and n_shards > 1
                                      else rank),
-                             walk=args.walk)
+                             walk=args.walk, sector_rule=args.sector_rule)
 
     vol = make_volume()
 
@@ -499,11 +506,16 @@ def main():
                        "semantics": args.semantics,
                        "voxblox": ({"method": args.method, "weight": "const" if args.const_weight
                                     else "1/z^2"} if args.semantics == "voxblox" else None),
-                       "parallelism": ("azimuth-sector x%d" % world if world > 1 else
-                                       "rank-%d rehearsal of azimuth-sector x%d" % (
-                                           args.rehearsal_sector % n_shards, n_shards)
+                       "parallelism": ("%s-sector x%d" % (args.sector_rule, world) if world > 1 else
+                                       "rank-%d rehearsal of %s-sector x%d" % (
+                                           args.rehearsal_sector % n_shards, args.sector_rule,
+                                           n_shards)
                                        if n_shards > 1 else "single"),
-                       "sector_split": "in-kernel (timed)" if n_shards > 1 else None,
+                       "sector_rule": args.sector_rule if n_shards > 1 else None,
+                       "sector_split": (None if n_shards <= 1 else
+                                        "index share: the rank reads only its contiguous 1/N of "
+                                        "each resident scan (timed)" if args.sector_rule == "index"
+                                        else "in-kernel world-frame filter (timed)"),
                        "front_end": ("single walk (k_walk + k_spans)" if "walk" in kernel_ms_per_launch
                                      else "two walks (k_count + k_place)")},
             "roofline": roofline,

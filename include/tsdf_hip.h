@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define TSDF_ABI_VERSION 9
+#define TSDF_ABI_VERSION 10
 #define TSDF_MAX_BATCH 512 /* scans per GPU batch (see tsdf_params.max_batch) */
 #define TSDF_BRICK_SIDE 8 /* voxels per brick edge: a brick is 8^3 = 512 voxels */
 
@@ -142,7 +142,24 @@ typedef struct tsdf_params {
      * cloud over its own PCIe link.  TSDF_SECTOR_INPUT_SPLIT: classified and split on the host,
      * each context receives only its sector's points (round 3's path).  Read from ctxs[0]. */
     int32_t sector_input;
+    /* ABI v10: which rays are sector k's (n_sectors > 1).
+     * TSDF_SECTOR_RULE_INDEX (default): each cloud's points are split into n_sectors
+     * contiguous index ranges, sector k holding points [floor(k n / N), floor((k + 1) n / N)) of
+     * an n-point cloud.  DLIO's deskewed cloud is sorted by point time (reference
+     * src/dlio/src/dlio/odom.cc:635-636) and an Ouster column is one firing time
+     * (src/ouster/src/os_ros.cpp:195-229), so these are contiguous column (azimuth) ranges of the
+     * spin in the sensor frame.  A context then reads, receives and walks only its share of every
+     * cloud: the host entry points copy only the share, the device batch entry points read only
+     * it, and no kernel classifies points.
+     * TSDF_SECTOR_RULE_WORLD: the world-frame pseudo-angle sectors of tsdf_sector_of (ABI v4-v9's
+     * only rule): a brick's owner stays fixed while the sensor turns, at the price of every
+     * context reading every point (the kernels drop the other sectors' rays).
+     * Either rule partitions each cloud's rays, so the reduced field is the unsharded one. */
+    int32_t sector_rule;
 } tsdf_params;
+
+#define TSDF_SECTOR_RULE_WORLD 0
+#define TSDF_SECTOR_RULE_INDEX 1
 
 #define TSDF_VB_SIMPLE 0
 #define TSDF_VB_MERGED 1
@@ -270,9 +287,11 @@ int tsdf_integrate_batch_device_pose(tsdf_ctx* ctx, const float* d_xyz,
 int tsdf_sync(tsdf_ctx* ctx);
 
 /* Dense read-out of voxels lo..hi-1 (voxel index coordinates, voxel i spans [i*vs, (i+1)*vs)),
- * x fastest: out[((z-lo2)*(hi1-lo1) + (y-lo1))*(hi0-lo0) + (x-lo0)].  Unobserved voxels read
- * (sdf_trunc, 0) — VDBFusion's background values.  sdf / weight are host buffers. */
-int tsdf_query_dense(tsdf_ctx* ctx, const int32_t lo[3], const int32_t hi[3], float* sdf,
+ * x fastest: out[((z-lo2)*(hi1-lo1) + (y-lo1))*(hi0-lo0) + (x-lo0)].  Unobserved voxels, and
+ * voxels outside the map's index domain (|i| >= 2^23 per axis), read (sdf_trunc, 0) — VDBFusion's
+ * background values.  sdf / weight are host buffers.  ABI v10: int64 bounds; each
+ * extent hi - lo must be below 2^31 and the box below 2^40 voxels (TSDF_EINVAL otherwise). */
+int tsdf_query_dense(tsdf_ctx* ctx, const int64_t lo[3], const int64_t hi[3], float* sdf,
                      float* weight);
 
 int tsdf_num_bricks(tsdf_ctx* ctx, uint64_t* n);

@@ -282,6 +282,9 @@ struct tsdf_ctx {
     // Voxblox MergedTsdfIntegrator (tsdf_params.voxblox_method): the bundling pre-pass' buffers,
     // one set per batch parity (tsdf_merged.hip)
     bool merged = false;
+    // TSDF_SECTOR_RULE_INDEX sharding (ABI v10): the context takes points [share_lo, share_hi) of
+    // every cloud (idx_share); the kernels' azimuth filter is off (R.sec_on = 0)
+    bool idx_rule = false;
     MgBufs mg[2];
     // tsdf_create_sharded: the contexts whose device memory this one reaches directly (peer access
     // or the same device); tsdf_integrate_sectors' fan-out: its copy-done event (this device)
@@ -1070,6 +1073,7 @@ void tsdf_default_params(tsdf_params* p) {
     p->semantics = TSDF_SEM_VDBFUSION_F64;  // ABI v8: the mode matching VDBFusion exactly
     p->voxblox_method = TSDF_VB_SIMPLE;
     p->sector_input = TSDF_SECTOR_INPUT_FANOUT;
+    p->sector_rule = TSDF_SECTOR_RULE_INDEX;  // ABI v10: SURVEY §8e's contiguous column sectors
     p->allow_clear = 1;  // voxblox TsdfIntegratorBase::Config defaults
     p->use_weight_dropoff = 1;
     p->max_weight = 10000.0f;
@@ -1183,7 +1187,9 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
     c->R.w0_cap = p->max_weight > 0.0f && p->max_weight < TSDF_W0_CAP ? p->max_weight : TSDF_W0_CAP;
     c->R.bg = p->semantics == TSDF_SEM_VOXBLOX ? 0.0f : c->R.tau;
     c->R.tau_m_vs = c->R.tau - c->R.vs;
-    sector_bounds(p->sector_yaw0, p->sector, p->n_sectors, c->R);
+    c->idx_rule = p->n_sectors > 1 && p->sector_rule == TSDF_SECTOR_RULE_INDEX;
+    if (c->idx_rule) c->R.sec_on = 0;
+    else sector_bounds(p->sector_yaw0, p->sector, p->n_sectors, c->R);
     const double vs_d = (double)c->R.vs;  // VDBVolume keeps voxel_size as float
     c->R.hvs_d = vs_d * 0.5;               // exact
     c->R.inv_s_d = 1.0 / vs_d;
@@ -1375,6 +1381,7 @@ int tsdf_create(const tsdf_params* p, tsdf_ctx** out) {
         (p->semantics == TSDF_SEM_VOXBLOX && !(p->max_weight > 0.0f)) ||
         (p->voxblox_method != TSDF_VB_SIMPLE && p->voxblox_method != TSDF_VB_MERGED) ||
         p->sector_input < TSDF_SECTOR_INPUT_FANOUT || p->sector_input > TSDF_SECTOR_INPUT_SPLIT ||
+        (p->sector_rule != TSDF_SECTOR_RULE_WORLD && p->sector_rule != TSDF_SECTOR_RULE_INDEX) ||
         (p->n_sectors > 1 && p->sector >= p->n_sectors) || !std::isfinite(p->sector_yaw0) ||
         (p->max_bricks_hard && p->max_bricks_hard < p->max_bricks))
         return TSDF_EINVAL;
@@ -1466,6 +1473,7 @@ static int pend_push(tsdf_ctx* c, uint64_t n, const ScanPose& P) {
     BatchDesc& D = c->pend;
     const uint32_t s = D.n_scans;
     set_pose(D, s, P);
+    D.s[s].xoff = 0;  // staged scans are contiguous
     D.s[s + 1].off = D.s[s].off + (uint32_t)n;
     D.n_scans = s + 1;
     c->n_points_in += n;
@@ -1480,12 +1488,32 @@ static int pend_room(tsdf_ctx* c, uint64_t n) {
     return TSDF_OK;
 }
 
+// TSDF_SECTOR_RULE_INDEX (ABI v10): sector k of N holds points
+// [floor(k n / N), floor((k + 1) n / N)) of an n-point cloud -- contiguous column ranges of the
+// spin for DLIO's time-sorted cloud (odom.cc:635-636).  The oracle's idx_share is the same.
+static void idx_share(const tsdf_ctx* c, uint64_t n, uint64_t& lo, uint64_t& hi) {
+    if (!c->idx_rule) {
+        lo = 0;
+        hi = n;
+        return;
+    }
+    const unsigned __int128 N = c->p.n_sectors, k = c->p.sector;
+    lo = (uint64_t)((unsigned __int128)n * k / N);
+    hi = (uint64_t)((unsigned __int128)n * (k + 1) / N);
+}
+
 static int integrate_impl(tsdf_ctx* c, const void* pts, uint64_t n, uint32_t point_step,
                           uint32_t xyz_offset, int32_t xyz_is_f64, const ScanPose& P) {
     if (border_busy(c)) return TSDF_EINVAL;
     const uint32_t need = xyz_is_f64 ? 24u : 12u;
     if (point_step < need || xyz_offset > point_step - need)
         return fail(c, TSDF_EINVAL, "point_step/xyz_offset inconsistent");
+    {  // the context's share of the cloud (all of it unless index-sharded)
+        uint64_t lo, hi;
+        idx_share(c, n, lo, hi);
+        if (pts) pts = static_cast<const char*>(pts) + lo * point_step;
+        n = hi - lo;
+    }
     if (n > c->max_points)
         return fail(c, TSDF_EINVAL, "scan of %llu points exceeds max_points %llu",
                     (unsigned long long)n, (unsigned long long)c->max_points);
@@ -1707,9 +1735,32 @@ static int sectors_impl(tsdf_ctx* const* ctxs, uint32_t n_ctx, const void* pts, 
     for (uint32_t k = 0; k < n_ctx; k++) {
         const tsdf_ctx* c = ctxs[k];
         const bool sharded = n_ctx == 1 ? c->p.n_sectors <= 1 : c->p.n_sectors == n_ctx;
-        if (!sharded || (n_ctx > 1 && (c->p.sector != k || c->p.sector_yaw0 != c0->p.sector_yaw0)))
-            return fail(c0, TSDF_EINVAL, "context %u is not sector %u of %u (same sector_yaw0)", k,
-                        k, n_ctx);
+        if (!sharded || (n_ctx > 1 && (c->p.sector != k || c->p.sector_yaw0 != c0->p.sector_yaw0 ||
+                                       c->p.sector_rule != c0->p.sector_rule)))
+            return fail(c0, TSDF_EINVAL,
+                        "context %u is not sector %u of %u (same sector_yaw0 and sector_rule)", k, k,
+                        n_ctx);
+    }
+    // TSDF_SECTOR_RULE_INDEX (ABI v10): context k's share is a contiguous index range of the
+    // cloud, so it packs and copies only that range over its own PCIe link -- one pass over the
+    // cloud in total, no classification, no fan-out (a Merged context bundles its share's points)
+    if (n_ctx > 1 && c0->idx_rule) {
+        HostTiming& hti = c0->split_ht;
+        hti.start();
+        hti.lap(0);
+        for (uint32_t k = 0; k < n_ctx; k++) {
+            const int rc = integrate_impl(ctxs[k], pts, n, point_step, xyz_offset, xyz_is_f64, P);
+            if (rc) {
+                if (k) c0->err = ctxs[k]->err;
+                return rc;
+            }
+        }
+        hti.lap(3);
+        hti.n++;
+        return TSDF_OK;
+    }
+    for (uint32_t k = 0; k < n_ctx; k++) {
+        const tsdf_ctx* c = ctxs[k];
         if (n > c->max_points)  // a context may receive every point
             return fail(c0, TSDF_EINVAL, "scan of %llu points exceeds max_points of context %u",
                         (unsigned long long)n, k);
@@ -1896,17 +1947,24 @@ static int batch_device_impl(tsdf_ctx* c, const float* d_xyz, const uint64_t* of
     HIPCHK(c, hipSetDevice(c->device));
     int rc = flush(c);
     if (rc) return rc;
+    // Each scan's share (all of it unless index-sharded: then only [lo, hi) of it is read, and the
+    // shares of a batch's scans are not contiguous -- ScanRec.xoff = the gap before each share)
     uint32_t s = 0;
     while (s < n_scans) {
         BatchDesc D;
         D.n_scans = 0;
         D.s[0].off = 0;
-        const uint64_t b0 = offs[s];
-        while (s < n_scans && D.n_scans < c->max_batch &&
-               offs[s + 1] - b0 <= c->batch_points) {
+        uint64_t lo, hi;
+        idx_share(c, offs[s + 1] - offs[s], lo, hi);
+        const uint64_t b0 = offs[s] + lo;
+        while (s < n_scans && D.n_scans < c->max_batch) {
+            idx_share(c, offs[s + 1] - offs[s], lo, hi);
+            const uint64_t x0 = offs[s] + lo - b0, nb = D.s[D.n_scans].off + (hi - lo);
+            if (nb > c->batch_points || x0 + (hi - lo) > 0xFFFFFFFFull) break;
             const double* q = origins + (uint64_t)pose_stride * s;
             set_pose(D, D.n_scans, pose_stride == 7 ? pose_of(q) : pose_of_origin(q));
-            D.s[D.n_scans + 1].off = (uint32_t)(offs[s + 1] - b0);
+            D.s[D.n_scans].xoff = (uint32_t)(x0 - D.s[D.n_scans].off);
+            D.s[D.n_scans + 1].off = (uint32_t)nb;
             D.n_scans++;
             s++;
         }
@@ -1941,6 +1999,12 @@ int tsdf_integrate_device(tsdf_ctx* c, const float* d_xyz, uint64_t n, const dou
     if (!c) return TSDF_EINVAL;
     if (border_busy(c)) return TSDF_EINVAL;
     if ((!d_xyz && n) || !origin) return fail(c, TSDF_EINVAL, "null argument");
+    {  // the context's share of the scan (all of it unless index-sharded)
+        uint64_t lo, hi;
+        idx_share(c, n, lo, hi);
+        if (d_xyz) d_xyz += 3 * lo;
+        n = hi - lo;
+    }
     if (n > c->max_points)
         return fail(c, TSDF_EINVAL, "scan of %llu points exceeds max_points %llu",
                     (unsigned long long)n, (unsigned long long)c->max_points);
@@ -1997,16 +2061,22 @@ static int drain(tsdf_ctx* c) {
     return emit_metrics(c);
 }
 
-int tsdf_query_dense(tsdf_ctx* c, const int32_t lo[3], const int32_t hi[3], float* sdf,
+int tsdf_query_dense(tsdf_ctx* c, const int64_t lo[3], const int64_t hi[3], float* sdf,
                      float* weight) {
     if (!c) return TSDF_EINVAL;
     if (!lo || !hi) return fail(c, TSDF_EINVAL, "null argument");
     int dims[3];
     for (int a = 0; a < 3; a++) {
         if (hi[a] < lo[a]) return fail(c, TSDF_EINVAL, "hi < lo");
-        dims[a] = hi[a] - lo[a];
+        // (the extent as unsigned: hi - lo of int64 bounds may exceed the int64 range)
+        const uint64_t ext = (uint64_t)hi[a] - (uint64_t)lo[a];
+        if (ext >= (1ull << 31)) return fail(c, TSDF_EINVAL, "query extent >= 2^31 voxels");
+        dims[a] = (int)ext;
     }
-    const uint64_t total = (uint64_t)dims[0] * dims[1] * dims[2];
+    uint64_t total = 0;  // (dims[0] dims[1] < 2^62; the third factor may overflow)
+    if (__builtin_mul_overflow((uint64_t)dims[0] * (uint64_t)dims[1], (uint64_t)dims[2], &total) ||
+        total >= (1ull << 40))
+        return fail(c, TSDF_EINVAL, "query box >= 2^40 voxels");
     int rc = drain(c);
     if (rc) return rc;
     if (!total) return TSDF_OK;

@@ -159,13 +159,15 @@ __host__ __device__ inline bool in_sector(const RayConst& R, float dx, float dy)
 // records to a device ring slot, and the kernels get a BatchRef to them (a batch of up to 512
 // scans does not fit the kernel-argument segment).
 // zx, zy, zz: the sensor's z axis in the world frame (Voxblox's 1/z^2 weight, RayConst::depth_w)
+// xoff (ABI v10): the scan's points are d_xyz[3 (i + xoff)] for its batch rays i -- nonzero only
+// for device batches of a TSDF_SECTOR_RULE_INDEX context, whose scans' shares are not contiguous
 struct ScanRec {
     uint32_t off, blk;
     float ox, oy, oz;
     float zx;
     double odx, ody, odz;
     float zy, zz;
-    uint32_t pad[2];
+    uint32_t xoff, pad;
 };
 static_assert(sizeof(ScanRec) == 64, "ScanRec layout");
 struct BatchDesc {
@@ -357,7 +359,7 @@ hipError_t launch_integrate_small(const BatchRef& D, const RayConst& R, const Ta
 hipError_t launch_integrate(const BatchRef& D, const RayConst& R, const Table& T, const Work& Wk,
                             const Pool& Pl, Globals* G, int parity, bool fused, bool big,
                             hipStream_t st, const KTime& kt = {});
-hipError_t launch_query_dense(const Table& T, const Pool& Pl, const int lo[3], const int dims[3],
+hipError_t launch_query_dense(const Table& T, const Pool& Pl, const int64_t lo[3], const int dims[3],
                               float bg, float* d_sdf, float* d_w, hipStream_t st);
 hipError_t launch_import(const Table& T, const Pool& Pl, const int32_t* d_coords, uint32_t n,
                          const float* d_sdf, const float* d_w, uint32_t* d_tidx, Globals* G,

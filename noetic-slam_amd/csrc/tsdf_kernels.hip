@@ -218,14 +218,15 @@ __global__ __launch_bounds__(NT, SEM == 2 && (NT == CNT_THREADS || G == 2) ? TSD
         const uint32_t t = g ? tb[G - 1] : tb[0], r0 = g ? r0b[G - 1] : r0b[0];
         const uint32_t r1 = g ? r1b[G - 1] : r1b[0];
         const float ox = D.s[t].ox, oy = D.s[t].oy, oz = D.s[t].oz;
+        const float* __restrict__ xs = scan_xyz(xyz, D, t, R);
         const uint32_t lo = G == 1 ? r0 + threadIdx.x : r0 + (uint32_t)(pass * NT) % RPB + threadIdx.x;
         const uint32_t hi = G == 1 ? r1 : min(r1, r0 + (uint32_t)(pass * NT) % RPB + NT);
         for (uint32_t i = lo; i < hi; i += NT) {
             uint32_t* pc = Wk.pair + (size_t)i * maxp;
             uint32_t k = 0;
             typename Walk<SEM>::State r;
-            const bool ok = Walk<SEM>::init(R, D, t, i, xyz[3 * (size_t)i], xyz[3 * (size_t)i + 1],
-                                            xyz[3 * (size_t)i + 2], r);
+            const bool ok = Walk<SEM>::init(R, D, t, i, xs[3 * (size_t)i], xs[3 * (size_t)i + 1],
+                                            xs[3 * (size_t)i + 2], r);
             valid += ok ? 1u : 0u;
             const uint32_t sub = 2u * (uint32_t)g + (i - r0 >= (uint32_t)(RPB / 2) ? 1u : 0u);
             // One pair per distinct brick; a line visits a brick in one contiguous run of DDA
@@ -639,9 +640,10 @@ __global__ __launch_bounds__(FLG_THREADS) void k_sector_flags(const float* __res
     uint32_t t, r0, r1;
     block_range(D, b, t, r0, r1);
     const float ox = D.s[t].ox, oy = D.s[t].oy;
+    const float* __restrict__ xs = scan_xyz(xyz, D, t, R);
     bool any = false;
     for (uint32_t i = r0 + (threadIdx.x & 63); i < r1; i += 64)
-        any |= in_sector(R, xyz[3 * (size_t)i] - ox, xyz[3 * (size_t)i + 1] - oy);
+        any |= in_sector(R, xs[3 * (size_t)i] - ox, xs[3 * (size_t)i + 1] - oy);
     const bool v = __any(any);
     // the block joins the walk kernels' list (order is immaterial: blocks are independent)
     if ((threadIdx.x & 63) == 0 && v) Wk.act[atomicAdd(&G->ctr[parity].n_act, 1u)] = b;
@@ -1084,9 +1086,10 @@ __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) v
     uint4 code4 = make_uint4(NO_PAIR, NO_PAIR, NO_PAIR, NO_PAIR);
     const uint32_t* pc = Wk.pair + (size_t)i * maxp;
     if (i < r1) {
-        px = xyz[3 * (size_t)i];
-        py = xyz[3 * (size_t)i + 1];
-        pz = xyz[3 * (size_t)i + 2];
+        const float* __restrict__ xs = scan_xyz(xyz, D, t, R);
+        px = xs[3 * (size_t)i];
+        py = xs[3 * (size_t)i + 1];
+        pz = xs[3 * (size_t)i + 2];
         if (maxp == 4) code4 = *reinterpret_cast<const uint4*>(pc);
     }
     const uint32_t nruns = Wk.blk_n[wb];
@@ -1347,18 +1350,20 @@ __global__ __launch_bounds__(PLC_THREADS, SEM == 2 ? TSDF_F64_PLACE_WAVES : 1) v
 // ------------------------------------------------------------------------------------------------
 // read-out / import
 
-__global__ void k_query_dense(Table T, Pool Pl, int lo0, int lo1, int lo2, int nx, int ny, int nz,
-                              float bg_sdf, float* __restrict__ out_sdf,
+// ABI v10: int64 bounds; a voxel outside the index domain reads the background
+__global__ void k_query_dense(Table T, Pool Pl, int64_t lo0, int64_t lo1, int64_t lo2, int nx,
+                              int ny, int nz, float bg_sdf, float* __restrict__ out_sdf,
                               float* __restrict__ out_w) {
     const uint64_t total = (uint64_t)nx * ny * nz;
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < total;
          i += (uint64_t)gridDim.x * blockDim.x) {
-        const int x = lo0 + (int)(i % nx);
-        const int y = lo1 + (int)((i / nx) % ny);
-        const int z = lo2 + (int)(i / ((uint64_t)nx * ny));
+        const int64_t xl = lo0 + (int64_t)(i % nx);
+        const int64_t yl = lo1 + (int64_t)((i / nx) % ny);
+        const int64_t zl = lo2 + (int64_t)(i / ((uint64_t)nx * ny));
         float s = bg_sdf, w = 0.0f;
-        if (x > -VOX_LIMIT && x < VOX_LIMIT && y > -VOX_LIMIT && y < VOX_LIMIT &&
-            z > -VOX_LIMIT && z < VOX_LIMIT) {
+        if (xl > -VOX_LIMIT && xl < VOX_LIMIT && yl > -VOX_LIMIT && yl < VOX_LIMIT &&
+            zl > -VOX_LIMIT && zl < VOX_LIMIT) {
+            const int x = (int)xl, y = (int)yl, z = (int)zl;
             const int64_t h = table_find(T, brick_key_of(x, y, z));
             if (h >= 0) {
                 const uint32_t slot = T.slots[h];
@@ -1650,7 +1655,7 @@ hipError_t launch_rehash(const Table& T, uint32_t n, Globals* G, hipStream_t st)
     return hipGetLastError();
 }
 
-hipError_t launch_query_dense(const Table& T, const Pool& Pl, const int lo[3], const int dims[3],
+hipError_t launch_query_dense(const Table& T, const Pool& Pl, const int64_t lo[3], const int dims[3],
                               float bg, float* d_sdf, float* d_w, hipStream_t st) {
     const uint64_t total = (uint64_t)dims[0] * dims[1] * dims[2];
     k_query_dense<<<grid_for(total, 256, 8192), 256, 0, st>>>(T, Pl, lo[0], lo[1], lo[2], dims[0],

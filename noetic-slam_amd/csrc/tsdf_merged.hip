@@ -42,8 +42,9 @@ __global__ __launch_bounds__(MG_THREADS) void k_mg_keys(const float* __restrict_
     const float zx = D.s[t].zx, zy = D.s[t].zy, zz = D.s[t].zz;
     const bool axis = zx != 0.0f || zy != 0.0f || zz != 0.0f;
     const float nan = __builtin_nanf("");
+    const float* __restrict__ xs = xyz + 3 * (size_t)D.s[t].xoff;  // the input (ABI v10 xoff)
     for (uint32_t i = r0 + threadIdx.x; i < r1; i += MG_THREADS) {
-        const float px = xyz[3 * (size_t)i], py = xyz[3 * (size_t)i + 1], pz = xyz[3 * (size_t)i + 2];
+        const float px = xs[3 * (size_t)i], py = xs[3 * (size_t)i + 1], pz = xs[3 * (size_t)i + 2];
         const float dx = px - ox, dy = py - oy, dz = pz - oz;
         const float depth = __builtin_sqrtf(dx * dx + (dy * dy + dz * dz));
         bool ok = depth > 0.0f && !(depth < R.min_range);

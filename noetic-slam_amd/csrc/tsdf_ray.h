@@ -202,6 +202,14 @@ __device__ __forceinline__ void block_range(const BatchRef& D, uint32_t b, uint3
     r1 = min(D.s[t + 1].off, r0 + RPB);
 }
 
+// The points of scan t for its batch rays i (ABI v10): xyz[3 (i + xoff)], xoff nonzero only for
+// the device batches of an index-sharded context.  The merged pre-pass writes its bundle rays in
+// batch-ray order (RayConst::ray_w set), so the walk kernels read that output without the gap.
+__device__ __forceinline__ const float* scan_xyz(const float* xyz, const BatchRef& D, uint32_t t,
+                                                 const RayConst& R) {
+    return R.ray_w ? xyz : xyz + 3 * (size_t)D.s[t].xoff;
+}
+
 constexpr float VB_MIN_WEIGHT = 1.0f / 65536.0f;  // lighter samples are dropped whole
 
 struct VbState {
@@ -623,6 +631,7 @@ __device__ __forceinline__ bool vdb_gate_filtered(const RayConst& R, float ox, f
     bool g = pos || (neg && in);
     const bool open = !(d2 <= r.bchk) || !(pos || neg) || (neg && !(in || out));
     if (__builtin_expect(__any(open), 0)) {
+#ifdef TSDF_F64_GATE_R05  // A/B only: round 5's branch (8 VGPR spills at the 6-wave bound)
         if (open) {
             // the origin, vs / 2 and the point re-read or re-converted here (opaque to hoisting),
             // so that the rare branch keeps no double live across the walk loop
@@ -633,6 +642,41 @@ __device__ __forceinline__ bool vdb_gate_filtered(const RayConst& R, float ox, f
             vdb_geom_at((double)vs * 0.5, q->odx, q->ody, q->odz, px, py, pz, r.vx, r.vy, r.vz, pd, dd);
             g = pd > 0.0 || (pd < 0.0 && dd < R.gate_d2);
         }
+#else
+        if (open) {
+            // the origin, vs / 2 and the point re-read or re-converted here (opaque to hoisting),
+            // so that the rare branch keeps no double live across the walk loop
+            // (the scan record and vs are wave-uniform, as vdb_init's origin: scalar registers, and
+            // the record is read with scalar loads)
+            const uint64_t qv = (uint64_t)r.sr;
+            uint64_t qa = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(qv >> 32)) << 32) |
+                          __builtin_amdgcn_readfirstlane((uint32_t)qv);
+            float px = r.px, py = r.py, pz = r.pz;
+            float vs = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, R.vs)));
+            asm volatile("" : "+s"(qa), "+v"(px), "+v"(py), "+v"(pz), "+s"(vs));
+            typedef const __attribute__((address_space(4))) ScanRec* ConstRec;
+            const ConstRec q = (ConstRec)qa;
+            // one origin component at a time, and the squared distance formed eagerly beside the
+            // projection (no short-circuit): the branch then holds ~12 VGPRs of doubles and the
+            // walk's registers stay where they are (no scratch spills at the 6-wave bound)
+            const double hv = (double)vs * 0.5;
+            double c = (double)(int)(2u * (uint32_t)r.vz + 1u) * hv;
+            double b = (double)pz - c;
+            double pd = (c - q->odz) * b;
+            double dd = b * b;
+            asm volatile("" : "+v"(pd), "+v"(dd));
+            c = (double)(int)(2u * (uint32_t)r.vy + 1u) * hv;
+            b = (double)py - c;
+            pd = (c - q->ody) * b + pd;
+            dd = b * b + dd;
+            asm volatile("" : "+v"(pd), "+v"(dd));
+            c = (double)(int)(2u * (uint32_t)r.vx + 1u) * hv;
+            b = (double)px - c;
+            pd = (c - q->odx) * b + pd;
+            dd = b * b + dd;
+            g = (pd > 0.0) | ((pd < 0.0) & (dd < R.gate_d2));
+        }
+#endif
     }
     return g;
 }

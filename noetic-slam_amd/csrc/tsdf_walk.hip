@@ -93,9 +93,10 @@ __global__ __launch_bounds__(WLK_THREADS) void k_walk(const float* __restrict__ 
     const uint32_t i = r0 + threadIdx.x;
     float px = 0.0f, py = 0.0f, pz = 0.0f;
     if (i < r1) {
-        px = xyz[3 * (size_t)i];
-        py = xyz[3 * (size_t)i + 1];
-        pz = xyz[3 * (size_t)i + 2];
+        const float* __restrict__ xs = scan_xyz(xyz, D, t, R);
+        px = xs[3 * (size_t)i];
+        py = xs[3 * (size_t)i + 1];
+        pz = xs[3 * (size_t)i + 2];
     }
     for (int j = threadIdx.x; j < HCAP; j += WLK_THREADS) {
         s_key[j] = EMPTY_KEY;

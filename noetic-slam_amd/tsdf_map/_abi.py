@@ -16,7 +16,7 @@ STATUS_NAMES = {
     TSDF_EHIP: "TSDF_EHIP", TSDF_ENODEV: "TSDF_ENODEV", TSDF_EOVERFLOW: "TSDF_EOVERFLOW",
 }
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 TILE_WORDS = 1028  # TSDF_TILE_WORDS: u32 words of one border-brick tile
 MAX_WORLD = 64
 SEM_VDBFUSION = 0
@@ -32,6 +32,7 @@ WALK_SINGLE = 1  # k_walk + k_spans when the band allows it
 MC_TABLES = {"generated": 0, "lorensen": 1, "lorensen_rule": 2}  # TSDF_MC_*
 VB_METHODS = {"simple": 0, "merged": 1}  # tsdf_params.voxblox_method (TSDF_VB_*)
 SECTOR_INPUTS = {"fanout": 0, "h2d": 1, "split": 2}  # tsdf_params.sector_input
+SECTOR_RULES = {"world": 0, "index": 1}  # tsdf_params.sector_rule (TSDF_SECTOR_RULE_*, ABI v10)
 
 
 class TsdfParams(C.Structure):
@@ -66,6 +67,8 @@ class TsdfParams(C.Structure):
         # ABI v8
         ("voxblox_method", C.c_int32),
         ("sector_input", C.c_int32),
+        # ABI v10
+        ("sector_rule", C.c_int32),
     ]
 
 
@@ -103,6 +106,7 @@ class TsdfStats(C.Structure):
 P = C.c_void_p
 D3 = C.POINTER(C.c_double)
 I3 = C.POINTER(C.c_int32)
+L3 = C.POINTER(C.c_int64)
 FP = C.POINTER(C.c_float)
 U64P = C.POINTER(C.c_uint64)
 class OsFormat(C.Structure):
@@ -129,7 +133,7 @@ SIGNATURES = {
     "tsdf_integrate_batch_device": (C.c_int, [P, P, U64P, C.c_uint32, D3]),
     "tsdf_integrate_batch_device_pose": (C.c_int, [P, P, U64P, C.c_uint32, D3]),
     "tsdf_sync": (C.c_int, [P]),
-    "tsdf_query_dense": (C.c_int, [P, I3, I3, FP, FP]),
+    "tsdf_query_dense": (C.c_int, [P, L3, L3, FP, FP]),  # ABI v10: int64 bounds
     "tsdf_num_bricks": (C.c_int, [P, U64P]),
     "tsdf_export_bricks": (C.c_int, [P, I3, FP, FP, C.c_uint64, U64P]),
     "tsdf_import_bricks": (C.c_int, [P, I3, FP, FP, C.c_uint64]),
@@ -200,6 +204,7 @@ def default_params(lib=None, **kw):
         p.n_sectors, p.sector, p.sector_yaw0, p.max_bricks_hard = 0, 0, 0.0, 0
         p.walk = WALK_TWO
         p.depth_weight, p.voxblox_method, p.sector_input = 1, 0, 0
+        p.sector_rule = SECTOR_RULES["index"]
     for k, v in kw.items():
         if not hasattr(p, k):
             raise TypeError("unknown tsdf_params field %r" % k)

@@ -8,7 +8,7 @@ PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_DIR = os.path.join(PKG_ROOT, "lib")
 HIP_LIB = os.path.join(LIB_DIR, "libtsdf_hip.so")
 
-ABI_VERSION = 9  # TSDF_ABI_VERSION of include/tsdf_hip.h
+ABI_VERSION = 10  # TSDF_ABI_VERSION of include/tsdf_hip.h
 
 _hip = None
 

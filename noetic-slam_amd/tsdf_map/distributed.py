@@ -44,6 +44,14 @@ class BorderReduceAborted(RuntimeError):
     """Another rank failed during the reduce; this rank rolled back (its field is unchanged)."""
 
 
+class BorderReduceFatal(RuntimeError):
+    """The reduce cannot end consistently: a collective raised on this rank (the process group
+    must be taken as broken -- the other ranks may still wait in it until its timeout; this rank
+    rolled back, its field is unchanged), or the commit failed here after every rank voted to
+    commit (the peers committed: this rank's sent bricks still hold mass their owners now hold
+    too, so the fields are inconsistent across ranks)."""
+
+
 def _all_ok(ok, group, cdev):
     """Every rank's local status, agreed by an all-reduce (MIN)."""
     import torch
@@ -59,7 +67,8 @@ def border_reduce(vol, group=None, comm_device=None, _fault=None):
     Returns {"bricks_sent", "bricks_received", "tile_bytes", "ms": {"keys", "pack", "exchange",
     "merge"}} for this rank (wall time of each step; "exchange" is the tile all-to-all).  On any
     rank's failure every rank rolls back and raises (BorderReduceAborted on the healthy ranks).
-    `_fault` (tests): a step name ("keys", "pack", "merge") at which this rank raises."""
+    `_fault` (tests): a step name ("keys", "pack", "exchange", "recv", "merge", "commit") at
+    which this rank fails ("commit": its first commit attempts fail)."""
     import torch
     import torch.distributed as dist
 
@@ -123,14 +132,21 @@ def border_reduce(vol, group=None, comm_device=None, _fault=None):
     keys, n = got
     cnt = torch.tensor([n], dtype=torch.int64, device=cdev)
     counts = [torch.zeros_like(cnt) for _ in range(world)]
-    dist.all_gather(counts, cnt, group=group)
+    dist.all_gather(counts, cnt, group=group)  # (no transaction is open yet: nothing to undo)
     counts = [int(c.item()) for c in counts]
     stride = max(1, max(counts))
-    mine = torch.full((stride,), -1, dtype=torch.int64, device=cdev)
-    mine[:n] = keys[:n].to(cdev)
+
+    def keys_stage():
+        mine = torch.full((stride,), -1, dtype=torch.int64, device=cdev)
+        mine[:n] = keys[:n].to(cdev)
+        return mine
+
+    mine = guarded(keys_stage)
+    vote_or_abort(False)
     allk = [torch.empty_like(mine) for _ in range(world)]
     dist.all_gather(allk, mine, group=group)
-    allk = torch.stack(allk).to(vdev).contiguous()
+    allk = guarded(lambda: torch.stack(allk).to(vdev).contiguous())
+    vote_or_abort(False)
     lap("keys")
 
     # 2. pack the bricks owned elsewhere (rows grouped by destination rank); they keep their mass
@@ -147,33 +163,72 @@ def border_reduce(vol, group=None, comm_device=None, _fault=None):
     send, send_counts = got
     lap("pack")
 
-    # 3. one all-to-all of the tiles
-    try:
-        sc = torch.tensor(send_counts, dtype=torch.int64, device=cdev)
-        rc = torch.empty_like(sc)
-        dist.all_to_all_single(rc, sc, group=group)
-        recv_counts = [int(x) for x in rc.tolist()]
-        n_send, n_recv = sum(send_counts), sum(recv_counts)
-        recv = torch.empty((max(n_recv, 1), TILE_WORDS), dtype=torch.int32, device=cdev)
-        dist.all_to_all_single(recv[:n_recv], send[:n_send].to(cdev),
-                               output_split_sizes=recv_counts, input_split_sizes=send_counts,
-                               group=group)
-        recv = recv.to(vdev)
-        ready()
-    except Exception:  # the collective itself failed (on every rank): roll back
-        vol.border_commit(False)
-        raise
+    def collective(fn):
+        """A collective every rank reaches; if it raises here, the group's state is unknown (the
+        peers may be inside it): roll back and report the group broken."""
+        try:
+            return fn()
+        except Exception as e:
+            vol.border_commit(False)
+            raise BorderReduceFatal("border reduce: a collective failed on rank %d (%s: %s); "
+                                    "the process group must be re-created" %
+                                    (rank, type(e).__name__, e)) from e
+
+    # 3. one all-to-all of the tiles.  The local work around it (the count and tile buffers on the
+    # collective's device, the received tiles back on the library's) runs guarded, with a vote
+    # before each collective, so a local failure never leaves a peer alone in a collective.
+    n_send = sum(send_counts)
+
+    def exchange_prep():
+        fault("exchange")
+        return (torch.tensor(send_counts, dtype=torch.int64, device=cdev),
+                send[:n_send].to(cdev).contiguous())
+
+    got = guarded(exchange_prep)
+    vote_or_abort(True)
+    sc, send_c = got
+    rc = torch.empty_like(sc)
+    collective(lambda: dist.all_to_all_single(rc, sc, group=group))
+    recv_counts = [int(x) for x in rc.tolist()]
+    n_recv = sum(recv_counts)
+
+    def recv_alloc():
+        fault("recv")
+        return torch.empty((max(n_recv, 1), TILE_WORDS), dtype=torch.int32, device=cdev)
+
+    recv = guarded(recv_alloc)
+    vote_or_abort(True)
+    collective(lambda: dist.all_to_all_single(recv[:n_recv], send_c,
+                                              output_split_sizes=recv_counts,
+                                              input_split_sizes=send_counts, group=group))
     lap("exchange")
 
     # 4. merge on the owner, sources in ascending rank order (snapshot first)
     def merge_step():
         fault("merge")
-        vol.border_merge(recv.data_ptr(), recv_counts)
+        r = recv.to(vdev).contiguous()
+        ready()
+        vol.border_merge(r.data_ptr(), recv_counts)
 
     guarded(merge_step)
     # 5. commit only when every rank merged; else every rank restores
     vote_or_abort(True)
-    vol.border_commit(True)
+    # every rank voted to commit: a failure here cannot be rolled back (the peers commit), so the
+    # commit is retried a bounded number of times before the fields are declared inconsistent
+    last = None
+    for attempt in range(3):
+        try:
+            if _fault == "commit" and attempt < 2:
+                raise RuntimeError("injected fault at commit (attempt %d) on rank %d" % (attempt, rank))
+            vol.border_commit(True)
+            last = None
+            break
+        except Exception as e:
+            last = e
+    if last is not None:
+        raise BorderReduceFatal("border reduce: rank %d could not commit after every rank voted "
+                                "to (%s); its sent bricks' mass is now double-counted across "
+                                "ranks" % (rank, last)) from last
     lap("merge")
     return {"bricks_sent": n_send, "bricks_received": n_recv,
             "tile_bytes": 4 * TILE_WORDS * (n_send + n_recv), "ms": ms}

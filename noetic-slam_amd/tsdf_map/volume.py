@@ -107,7 +107,7 @@ class TSDFVolume:
                     max_batch=32, pipeline=False, semantics="vdbfusion_f64", allow_clear=True,
                     use_weight_dropoff=True, max_weight=10000.0, n_sectors=0, sector=0,
                     sector_yaw0=0.0, max_bricks_hard=0, walk="two", use_const_weight=False,
-                    method="simple", sector_input="fanout"):
+                    method="simple", sector_input="fanout", sector_rule="index"):
         """tsdf_params from the VDBFusion / Voxblox-style keyword arguments."""
         if semantics not in _abi.SEMANTICS:
             raise ValueError("semantics must be one of %s" % sorted(_abi.SEMANTICS))
@@ -143,6 +143,12 @@ class TSDFVolume:
         if sector_input not in _abi.SECTOR_INPUTS:
             raise ValueError("sector_input must be one of %s" % sorted(_abi.SECTOR_INPUTS))
         p.sector_input = _abi.SECTOR_INPUTS[sector_input]
+        # which rays are sector k's (ABI v10): "index" (contiguous index ranges of each cloud,
+        # DLIO's time order: sensor-frame column sectors; the default) or "world" (world-frame
+        # pseudo-angle sectors)
+        if sector_rule not in _abi.SECTOR_RULES:
+            raise ValueError("sector_rule must be one of %s" % sorted(_abi.SECTOR_RULES))
+        p.sector_rule = _abi.SECTOR_RULES[sector_rule]
         return p
 
     # -- lifecycle ------------------------------------------------------------------------------
@@ -213,15 +219,15 @@ class TSDFVolume:
     # -- read-out -------------------------------------------------------------------------------
     def query_dense(self, lo, hi):
         """(sdf, weight) of voxels lo..hi-1 as [z, y, x] float32 arrays."""
-        lo = np.asarray(lo, np.int32).reshape(3)
-        hi = np.asarray(hi, np.int32).reshape(3)
+        lo = np.asarray(lo, np.int64).reshape(3)
+        hi = np.asarray(hi, np.int64).reshape(3)
         dims = (hi - lo)
         if np.any(dims < 0):
             raise ValueError("hi < lo")
         s = np.empty((dims[2], dims[1], dims[0]), np.float32)
         w = np.empty_like(s)
-        self._check(self._lib.tsdf_query_dense(self._ctx, lo.ctypes.data_as(_abi.I3),
-                                               hi.ctypes.data_as(_abi.I3),
+        self._check(self._lib.tsdf_query_dense(self._ctx, lo.ctypes.data_as(_abi.L3),
+                                               hi.ctypes.data_as(_abi.L3),
                                                s.ctypes.data_as(_abi.FP),
                                                w.ctypes.data_as(_abi.FP)), "query_dense")
         return s, w

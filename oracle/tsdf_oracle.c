@@ -252,6 +252,7 @@ void tsdf_default_params(tsdf_params* p) {
     p->depth_weight = 1; /* voxblox use_const_weight = false (upstream's default) */
     p->voxblox_method = TSDF_VB_SIMPLE;
     p->sector_input = TSDF_SECTOR_INPUT_FANOUT;
+    p->sector_rule = TSDF_SECTOR_RULE_INDEX; /* ABI v10 */
 }
 
 int tsdf_abi_version(void) { return TSDF_ABI_VERSION; }
@@ -266,6 +267,8 @@ int tsdf_create(const tsdf_params* params, tsdf_ctx** out) {
         (params->voxblox_method != TSDF_VB_SIMPLE && params->voxblox_method != TSDF_VB_MERGED) ||
         (params->sector_input < TSDF_SECTOR_INPUT_FANOUT ||
          params->sector_input > TSDF_SECTOR_INPUT_SPLIT) ||
+        (params->sector_rule != TSDF_SECTOR_RULE_WORLD &&
+         params->sector_rule != TSDF_SECTOR_RULE_INDEX) ||
         (params->n_sectors > 1 && params->sector >= params->n_sectors) ||
         !isfinite(params->sector_yaw0))
         return TSDF_EINVAL;
@@ -279,7 +282,7 @@ int tsdf_create(const tsdf_params* params, tsdf_ctx** out) {
     c->zax[0] = 0.0f; c->zax[1] = 0.0f; c->zax[2] = 0.0f; /* no orientation: weight 1 */
     c->bg = c->sem == TSDF_SEM_VOXBLOX ? 0.0f : c->tau;
     c->mode = ORACLE_MODE_SCAN_FUSED;
-    {
+    if (params->sector_rule == TSDF_SECTOR_RULE_WORLD) { /* the index rule slices at entry */
         const sector_t r = sector_bounds(params->sector_yaw0, params->sector, params->n_sectors);
         c->sec_on = r.on; c->sec_wrap = r.wrap; c->sec_lo = r.lo; c->sec_hi = r.hi;
     }
@@ -1005,6 +1008,16 @@ static int integrate_scan(tsdf_ctx* c, const void* pts, uint64_t n, uint32_t poi
     const uint32_t need = xyz_is_f64 ? 24u : 12u;
     if (point_step < need || xyz_offset > point_step - need)
         return set_err(c, TSDF_EINVAL, "point_step/xyz_offset inconsistent");
+    if (c->p.n_sectors > 1 && c->p.sector_rule == TSDF_SECTOR_RULE_INDEX && !c->mg_on) {
+        /* ABI v10, SURVEY §8e: sector k of N takes points [floor(k n / N), floor((k + 1) n / N)) --
+           for DLIO's time-sorted cloud (reference odom.cc:635-636) contiguous column ranges (the
+           merged bundles of the share are not sliced again) */
+        const unsigned __int128 N = c->p.n_sectors, k = c->p.sector;
+        const uint64_t lo = (uint64_t)((unsigned __int128)n * k / N);
+        const uint64_t hi = (uint64_t)((unsigned __int128)n * (k + 1) / N);
+        if (pts) pts = (const char*)pts + lo * point_step;
+        n = hi - lo;
+    }
     const float ox = (float)origin[0], oy = (float)origin[1], oz = (float)origin[2];
     if (c->sem == TSDF_SEM_VOXBLOX && c->p.voxblox_method == TSDF_VB_MERGED && !c->mg_on) {
         /* MergedTsdfIntegrator: walk the scan's bundled rays instead of its points */
@@ -1094,17 +1107,28 @@ int tsdf_set_metrics_log(tsdf_ctx* c, const char* path) {
     return path ? set_err(c, TSDF_EINVAL, "the oracle writes no metrics log") : TSDF_OK;
 }
 
-int tsdf_query_dense(tsdf_ctx* c, const int32_t lo[3], const int32_t hi[3], float* sdf,
+/* ABI v10: int64 bounds, the GPU library's limits (extent < 2^31, box < 2^40);
+   voxels outside the index domain (|i| >= 2^23) read the background */
+int tsdf_query_dense(tsdf_ctx* c, const int64_t lo[3], const int64_t hi[3], float* sdf,
                      float* weight) {
     if (!c || !lo || !hi) return TSDF_EINVAL;
     mt_collect(c);
-    for (int a = 0; a < 3; a++)
+    uint64_t ext[3];
+    for (int a = 0; a < 3; a++) {
         if (hi[a] < lo[a]) return set_err(c, TSDF_EINVAL, "hi < lo");
+        ext[a] = (uint64_t)hi[a] - (uint64_t)lo[a];
+        if (ext[a] >= (1ull << 31)) return set_err(c, TSDF_EINVAL, "query extent >= 2^31 voxels");
+    }
+    uint64_t total = 0;
+    if (__builtin_mul_overflow(ext[0] * ext[1], ext[2], &total) || total >= (1ull << 40))
+        return set_err(c, TSDF_EINVAL, "query box >= 2^40 voxels");
     uint64_t i = 0;
-    for (int32_t z = lo[2]; z < hi[2]; z++)
-        for (int32_t y = lo[1]; y < hi[1]; y++)
-            for (int32_t x = lo[0]; x < hi[0]; x++, i++) {
-                const vox_t* v = vox_find(c, x, y, z);
+    const int64_t lim = VOX_LIMIT;
+    for (int64_t z = lo[2]; z < hi[2]; z++)
+        for (int64_t y = lo[1]; y < hi[1]; y++)
+            for (int64_t x = lo[0]; x < hi[0]; x++, i++) {
+                const int in = x > -lim && x < lim && y > -lim && y < lim && z > -lim && z < lim;
+                const vox_t* v = in ? vox_find(c, (int32_t)x, (int32_t)y, (int32_t)z) : NULL;
                 if (sdf) sdf[i] = v ? v->S : c->bg;
                 if (weight) weight[i] = v ? v->W : 0.0f;
             }
@@ -1642,14 +1666,17 @@ static int sectors_check(tsdf_ctx* const* ctxs, uint32_t n_ctx) {
         const int sharded = n_ctx == 1 ? c->p.n_sectors <= 1 : c->p.n_sectors == n_ctx;
         if (!sharded || (n_ctx > 1 && (c->p.sector != k || c->p.sector_yaw0 != ctxs[0]->p.sector_yaw0)))
             return set_err(ctxs[0], TSDF_EINVAL, "a context is not its sector of n (same sector_yaw0)");
+        if (n_ctx > 1 && c->p.sector_rule != ctxs[0]->p.sector_rule)
+            return set_err(ctxs[0], TSDF_EINVAL, "the contexts' sector_rule differs");
         if (c->brd_open)
             return set_err(ctxs[0], TSDF_EINVAL, "a border reduce is open on a context");
     }
     return TSDF_OK;
 }
 
-/* every context integrates the whole cloud and keeps its sector's rays: the fields the GPU
- * library's fan-out / split give, bit for bit */
+/* every context integrates the whole cloud and keeps its sector's rays (the world rule) or its
+ * share's points (the index rule, sliced in integrate_scan): the fields the GPU library's fan-out /
+ * split / per-context shares give, bit for bit */
 int tsdf_integrate_sectors(tsdf_ctx* const* ctxs, uint32_t n_ctx, const void* pts, uint64_t n,
                            uint32_t point_step, uint32_t xyz_offset, int32_t xyz_is_f64,
                            const double pose[7]) {

@@ -154,7 +154,7 @@ static void readout(const scan_t* sc) {
     field_t fa = field(a), fb = field(b);
     CHECK(same(fa, fb), "import != export");
     drop(fa); drop(fb);
-    const int32_t lo[3] = {-40, -40, -10}, hi[3] = {40, 40, 10};
+    const int64_t lo[3] = {-40, -40, -10}, hi[3] = {40, 40, 10};
     float* qs = (float*)malloc(80 * 80 * 20 * 4);
     float* qw = (float*)malloc(80 * 80 * 20 * 4);
     OK(tsdf_query_dense(a, lo, hi, qs, qw));

@@ -37,7 +37,7 @@ def test_hip_library_exports_every_declared_symbol():
     missing = [f for f in header_functions() if f not in syms]
     assert not missing, missing
     lib = load_hip_library()
-    assert lib.tsdf_abi_version() == 9
+    assert lib.tsdf_abi_version() == 10
 
 
 def test_hip_library_is_gfx950_code():
@@ -67,8 +67,10 @@ def test_default_params_roundtrip():
     assert p.voxblox_method == _abi.VB_METHODS["simple"] == 0  # ABI v8
     assert p.sector_input == _abi.SECTOR_INPUTS["fanout"] == 0
     assert p.semantics == _abi.SEM_VDBFUSION_F64  # ABI v8 default
-    # the ctypes mirror ends where the C struct ends (ABI v8 appended `sector_input`)
-    assert _abi.TsdfParams._fields_[-1][0] == "sector_input"
+    # ABI v10: SURVEY §8e's contiguous index (column) sectors are the default rule
+    assert p.sector_rule == _abi.SECTOR_RULES["index"] == 1
+    # the ctypes mirror ends where the C struct ends (ABI v10 appended `sector_rule`)
+    assert _abi.TsdfParams._fields_[-1][0] == "sector_rule"
 
 
 def test_struct_layouts_match_the_header(tmp_path):
@@ -127,7 +129,8 @@ def test_invalid_params_rejected_before_device():
     from tsdf_map import _abi, load_hip_library
     lib = load_hip_library()
     for kw in ({"voxel_size": 0.0}, {"sdf_trunc": -1.0}, {"brick_side": 16},
-               {"space_carving": 1}):  # carving needs a finite max_range
+               {"space_carving": 1},  # carving needs a finite max_range
+               {"sector_rule": 2}):  # ABI v10: TSDF_SECTOR_RULE_WORLD or _INDEX only
         p = _abi.default_params(lib, **kw)
         ctx = ctypes.c_void_p()
         assert lib.tsdf_create(ctypes.byref(p), ctypes.byref(ctx)) == _abi.TSDF_EINVAL
@@ -153,3 +156,31 @@ def test_product_package_never_imports_the_oracle():
                 for pat in (r"#\s*include\s*[\"<][^\">]*oracle", r"libtsdf_oracle", r"-ltsdf_oracle",
                             r"^\s*(import|from)\s+oracle", r"oracle/build"):
                     assert not re.search(pat, txt, flags=re.M), (f, pat)
+
+
+def test_query_dense_takes_int64_bounds():
+    """ABI v10: tsdf_query_dense's lo / hi are int64_t[3] in the
+    header, in the ctypes table, and in both libraries' behaviour (the oracle, on the CPU): a box
+    beyond the int32 range reads the background, and oversized extents are refused."""
+    import re
+    from tsdf_map import _abi
+    hdr = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    proto = re.search(r"int tsdf_query_dense\(([^)]*)\)", hdr).group(1)
+    assert "const int64_t lo[3]" in proto and "const int64_t hi[3]" in proto, proto
+    args = _abi.SIGNATURES["tsdf_query_dense"][1]
+    assert args[1] is ctypes.POINTER(ctypes.c_int64) and args[2] is ctypes.POINTER(ctypes.c_int64)
+    import oracle
+    v = oracle.OracleTSDFVolume(0.05, 0.15)
+    v.integrate(np.array([[2.0, 0.0, 0.0]], np.float32), np.zeros(3))
+    big = 1 << 40  # far outside int32 and the index domain (|i| < 2^23)
+    s, w = v.query_dense([big, -big, 0], [big + 3, -big + 2, 2])
+    assert s.shape == (2, 2, 3) and np.all(s == np.float32(0.15)) and np.all(w == 0)
+    # the observed voxels still read back with 64-bit bounds
+    s, w = v.query_dense([37, -2, -2], [43, 2, 2])
+    assert w.max() > 0
+    for lo, hi in (([0, 0, 0], [1 << 31, 1, 1]), ([0, 0, 0], [1 << 14, 1 << 14, 1 << 13]),
+                   ([-(1 << 62), 0, 0], [(1 << 62), 1, 1]), ([0, 0, 0], [-1, 1, 1])):
+        lo6, hi6 = np.array(lo, np.int64), np.array(hi, np.int64)
+        rc = v._lib.tsdf_query_dense(v._ctx, lo6.ctypes.data_as(_abi.L3),
+                                     hi6.ctypes.data_as(_abi.L3), None, None)
+        assert rc == _abi.TSDF_EINVAL, (lo, hi)
