@@ -648,9 +648,12 @@ __device__ __forceinline__ bool vdb_gate_filtered(const RayConst& R, float ox, f
             // so that the rare branch keeps no double live across the walk loop
             // (the scan record and vs are wave-uniform, as vdb_init's origin: scalar registers, and
             // the record is read with scalar loads)
+            // (readfirstlane returns int: both halves go through uint32_t, or the low half of the
+            // address would be sign-extended into the high one)
             const uint64_t qv = (uint64_t)r.sr;
-            uint64_t qa = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(qv >> 32)) << 32) |
-                          __builtin_amdgcn_readfirstlane((uint32_t)qv);
+            const uint32_t qlo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)qv);
+            const uint32_t qhi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(qv >> 32));
+            uint64_t qa = ((uint64_t)qhi << 32) | qlo;
             float px = r.px, py = r.py, pz = r.pz;
             float vs = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, R.vs)));
             asm volatile("" : "+s"(qa), "+v"(px), "+v"(py), "+v"(pz), "+s"(vs));
