@@ -1707,6 +1707,19 @@ int tsdf_border_reduce_local(tsdf_ctx* const* ctxs, uint32_t n, uint64_t* bricks
         if (!ctxs[k]) return TSDF_EINVAL;
     if (bricks_moved) *bricks_moved = 0;
     if (n == 1) return TSDF_OK;
+    {   /* test hook (the node's fallback, tests/test_node_stub.py): TSDF_ORACLE_REDUCE_FAIL = k
+           makes the first k reduces of the process fail as an aborted transaction would, every
+           context unchanged */
+        static int fails_left = -1;
+        if (fails_left < 0) {
+            const char* e = getenv("TSDF_ORACLE_REDUCE_FAIL");
+            fails_left = e ? atoi(e) : 0;
+        }
+        if (fails_left > 0) {
+            fails_left--;
+            return set_err(ctxs[0], TSDF_EHIP, "injected border-reduce failure (aborted, fields unchanged)");
+        }
+    }
     int rc = TSDF_OK;
     uint64_t counts[TSDF_MAX_WORLD] = {0}, stride = 1;
     for (uint32_t k = 0; k < n && rc == TSDF_OK; k++) {

@@ -2,7 +2,8 @@
 // "name=value;..." overrides from $TSDF_STUB_PARAMS), subscriptions by topic, and a spin() that
 // replays $TSDF_STUB_STREAM (tsdf_replay's "TSDFSTR2" topic stream) into them in arrival order:
 // 'P' records to the pose subscription, 'C' records (dlio::Point-shaped PointCloud2) to the cloud
-// subscription.
+// subscription, 'S' records call the node's advertised "save_map" service (~save_map), an 'X'
+// record ends the process on the spot (a crash: no destructors run).
 #pragma once
 #include <cstdarg>
 #include <cstdint>
@@ -40,6 +41,11 @@ inline std::map<std::string, std::function<void(std::shared_ptr<const void>)>>& 
     static std::map<std::string, std::function<void(std::shared_ptr<const void>)>> m;
     return m;
 }
+// service name (the private name as advertised) -> handler returning the response's success
+inline std::map<std::string, std::function<bool()>>& services() {
+    static std::map<std::string, std::function<bool()>> m;
+    return m;
+}
 inline std::string param_override(const std::string& name) {
     const char* e = std::getenv("TSDF_STUB_PARAMS");
     if (!e) return "";
@@ -58,6 +64,7 @@ inline void parse(const std::string& s, std::string& v) { v = s; }
 }  // namespace stub
 
 class Subscriber {};
+class ServiceServer {};
 
 class NodeHandle {
    public:
@@ -80,6 +87,18 @@ class NodeHandle {
             (obj->*fn)(std::static_pointer_cast<const M>(m));
         };
         return Subscriber();
+    }
+    template <class Req, class Res, class C>
+    ServiceServer advertiseService(const std::string& name, bool (C::*fn)(Req&, Res&), C* obj) {
+        stub::services()[name] = [obj, fn, name]() {
+            Req q;
+            Res r;
+            const bool ok = (obj->*fn)(q, r);
+            std::fprintf(stderr, "[STUB] service %s: %s %s\n", name.c_str(),
+                         ok && r.success ? "success" : "failure", r.message.c_str());
+            return ok && r.success;
+        };
+        return ServiceServer();
     }
 };
 
@@ -140,6 +159,11 @@ inline void spin() {
             m->data.resize((size_t)n * step);
             if (n && std::fread(m->data.data(), step, n, f) != n) break;
             if (stub::subs().count(cloud_topic)) stub::subs()[cloud_topic](m);
+        } else if (type == 'S') {  // a call of ~save_map at this point of the stream
+            if (stub::services().count("save_map")) stub::services()["save_map"]();
+        } else if (type == 'X') {  // the process dies here: no destructor, no shutdown save
+            std::fflush(stderr);
+            std::_Exit(3);
         } else {
             break;
         }

@@ -21,7 +21,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, rule="index"):
     import sys
     for p in (os.path.join(REPO, "noetic-slam_amd"), os.path.join(REPO, "oracle")):
         sys.path.insert(0, p)
@@ -34,8 +34,10 @@ def _worker(rank, world, port, out_dir):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     sim = OusterSim()
-    # the sector filter inside the integrate (tsdf_params.n_sectors / sector), as on the GPUs
-    vol = oracle.OracleTSDFVolume(0.05, 0.15, n_sectors=world, sector=rank, sector_yaw0=0.3)
+    # the sector rule inside the integrate (tsdf_params.n_sectors / sector / sector_rule), as on
+    # the GPUs: the contiguous index share of every scan, or the world-frame azimuth filter
+    vol = oracle.OracleTSDFVolume(0.05, 0.15, n_sectors=world, sector=rank, sector_yaw0=0.3,
+                                  sector_rule=rule)
     for k in (0, 3):
         pts, org = sim.scan(k)
         vol.integrate(np.ascontiguousarray(pts[::8]), org)
@@ -49,9 +51,11 @@ def _worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sector_sharded_merge_gloo(world, tmp_path):
-    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+@pytest.mark.parametrize("world,rule", [(2, "index"), (3, "index"), (2, "world"), (3, "world")])
+def test_sector_sharded_merge_gloo(world, rule, tmp_path):
+    """Both sector rules (ABI v10): the index rule's contiguous shares and the world-frame azimuth
+    sectors each partition the rays, so the reduced union is the single-volume field."""
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path), rule), nprocs=world,
                        join=True, start_method="spawn")
     import oracle
     from tsdf_map import bricks_to_voxels
@@ -114,12 +118,15 @@ def _fault_worker(rank, world, port, out_dir, fault_rank, step):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,step", [(2, "merge"), (3, "merge"), (3, "pack"), (2, "keys")])
+@pytest.mark.parametrize("world,step", [(2, "merge"), (3, "merge"), (3, "pack"), (2, "keys"),
+                                        (2, "exchange"), (3, "exchange"), (3, "recv")])
 def test_border_reduce_failure_leaves_fields_unchanged(world, step, tmp_path):
     """a rank failing between pack and merge (or earlier) makes every rank roll back:
     the faulty rank raises its error, the others BorderReduceAborted, and every rank's field is bit
     for bit the one before the reduce (no mass lost at the sources, none double-counted at the
-    owners); the contexts take scans and reduce again afterwards."""
+    owners); the contexts take scans and reduce again afterwards.  ADVICE r5: "exchange" (the
+    tile staging just before the all-to-alls) and "recv" (the receive buffer, between them) are
+    local failures too: voted on before each collective, so no peer is left inside one."""
     fault_rank = world - 1
     mp.start_processes(_fault_worker, args=(world, _free_port(), str(tmp_path), fault_rank, step),
                        nprocs=world, join=True, start_method="spawn")
@@ -181,3 +188,57 @@ def test_sharded_mesh_gloo(world, tmp_path):
         want = tri_set(union.extract_triangle_mesh(table=table)[0])
         assert got.shape[0] > 1000
         assert np.array_equal(got, want), table
+
+
+def _commit_worker(rank, world, port, out_dir, fault_rank):
+    import sys
+    for p in (os.path.join(REPO, "noetic-slam_amd"), os.path.join(REPO, "oracle")):
+        sys.path.insert(0, p)
+    import torch.distributed as dist
+    import oracle
+    from tsdf_map.distributed import border_reduce
+    from tsdf_map.scan_gen import OusterSim
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sim = OusterSim()
+    vol = oracle.OracleTSDFVolume(0.05, 0.15, n_sectors=world, sector=rank)
+    for k in (0, 3):
+        pts, org = sim.scan(k)
+        vol.integrate(np.ascontiguousarray(pts[::8]), org)
+    info = border_reduce(vol, _fault="commit" if rank == fault_rank else None)
+    c, s_, w = vol.export_bricks()
+    keep = (w.reshape(len(c), -1) > 0).any(1)
+    np.savez(os.path.join(out_dir, "rank%d.npz" % rank), coords=c[keep], sdf=s_[keep],
+             weight=w[keep], sent=info["bricks_sent"])
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_border_reduce_commit_is_retried(tmp_path):
+    """once every rank voted to commit, a rank whose commit fails retries it (bounded)
+    instead of raising with its peers committed; here its first two attempts fail and the third
+    commits, so the reduce ends partitioned (each brick on one rank) and equal to the single
+    volume.  A commit that keeps failing raises BorderReduceFatal (the fields would then be
+    inconsistent across ranks)."""
+    world = 2
+    mp.start_processes(_commit_worker, args=(world, _free_port(), str(tmp_path), 1), nprocs=world,
+                       join=True, start_method="spawn")
+    import oracle
+    from tsdf_map import bricks_to_voxels
+    from tsdf_map.scan_gen import OusterSim
+    parts = [np.load(str(tmp_path / ("rank%d.npz" % r))) for r in range(world)]
+    assert int(parts[1]["sent"]) > 0
+    coords = np.concatenate([p["coords"] for p in parts])
+    assert len({tuple(x) for x in coords.tolist()}) == coords.shape[0]
+    mi, ms, mw = bricks_to_voxels(coords, np.concatenate([p["sdf"] for p in parts]),
+                                  np.concatenate([p["weight"] for p in parts]))
+    sim = OusterSim()
+    ref = oracle.OracleTSDFVolume(0.05, 0.15)
+    for k in (0, 3):
+        pts, org = sim.scan(k)
+        ref.integrate(np.ascontiguousarray(pts[::8]), org)
+    ri, rs, rw = ref.export_voxels()
+    assert np.array_equal(mi, ri) and np.array_equal(mw, rw)
+    assert np.max(np.abs(ms - rs)) <= 1e-5
