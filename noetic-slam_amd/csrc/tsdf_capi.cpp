@@ -460,7 +460,8 @@ static int launch(tsdf_ctx* c, const float* d_xyz, BatchDesc& D) {
     RayConst R = c->R;
     const float* d_rays = d_xyz;
     if (c->merged && D.n_blocks) {
-        HIPCHK(c, launch_mg_prepass(d_xyz, B, D.n_blocks, D.s[D.n_scans].off, c->R, c->mg[par], st));
+        HIPCHK(c, launch_mg_prepass(d_xyz, B, D.n_blocks, D.s[D.n_scans].off, c->R, c->mg[par],
+                                    &c->G->ctr[par].ovf, st));
         d_rays = c->mg[par].xyz_out;
         R.ray_w = c->mg[par].w_out;
     }
@@ -844,7 +845,9 @@ static int check_and_replay(tsdf_ctx* c) {
             return TSDF_OK;
         }
         int rc = TSDF_ENOMEM;
-        if (!(g.overflow & OVF_PAIRS)) {  // pair slots per ray are a geometric bound, not a capacity
+        // pair slots per ray are a geometric bound, and the merged tables' 1.25x sizing a proof,
+        // not capacities
+        if (!(g.overflow & (OVF_PAIRS | OVF_MG))) {
             rc = TSDF_OK;
             if (g.overflow & (OVF_TABLE | OVF_POOL | OVF_ACTIVE))
                 rc = grow_capacity(c, std::max<uint64_t>(g.pool_count, c->T.max_bricks + 1));
@@ -1130,8 +1133,8 @@ void tsdf_destroy(tsdf_ctx* c) {
         if (c->h_stage[i]) (void)hipHostFree(c->h_stage[i]);
         if (c->stage_done[i]) (void)hipEventDestroy(c->stage_done[i]);
         MgBufs& M = c->mg[i];
-        for (void* q : {(void*)M.key, (void*)M.key2, (void*)M.idx, (void*)M.idx2, (void*)M.dw,
-                        (void*)M.sid, (void*)M.xyz_out, (void*)M.w_out, M.tmp, (void*)M.tab})
+        for (void* q : {(void*)M.slot, (void*)M.gid, (void*)M.xyz_out, (void*)M.w_out,
+                        (void*)M.tab, (void*)M.grp})
             if (q) (void)hipFree(q);
     }
     if (c->bc_ev) (void)hipEventDestroy(c->bc_ev);
@@ -1293,19 +1296,15 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
             MgBufs& M = c->mg[q];
             const uint64_t n = c->batch_points;
             M.cap = n;
-            M.tmp_bytes = mg_sort_scratch(n);
-            M.tab_bits = mg_tab_bits(n);
-            HIPCHK(c, hipMalloc(&M.tab, (size_t)8 << M.tab_bits));
-            HIPCHK(c, hipMemset(M.tab, 0, (size_t)8 << M.tab_bits));  // every slot empty (key 0)
-            HIPCHK(c, hipMalloc(&M.key, n * 4));
-            HIPCHK(c, hipMalloc(&M.key2, n * 4));
-            HIPCHK(c, hipMalloc(&M.idx, n * 4));
-            HIPCHK(c, hipMalloc(&M.idx2, n * 4));
-            HIPCHK(c, hipMalloc(&M.dw, n * sizeof(float4)));
-            HIPCHK(c, hipMalloc(&M.sid, n * 2));
+            M.tab_bits = M.grp_bits = mg_tab_bits(n);  // >= 1.25 n records each
+            HIPCHK(c, hipMalloc(&M.tab, (size_t)32 << M.tab_bits));
+            HIPCHK(c, hipMemset(M.tab, 0, (size_t)32 << M.tab_bits));  // every record empty
+            HIPCHK(c, hipMalloc(&M.grp, (size_t)16 << M.grp_bits));
+            HIPCHK(c, hipMemset(M.grp, 0, (size_t)16 << M.grp_bits));
+            HIPCHK(c, hipMalloc(&M.slot, n * 4));
+            HIPCHK(c, hipMalloc(&M.gid, n * 4));
             HIPCHK(c, hipMalloc(&M.xyz_out, n * 12));
             HIPCHK(c, hipMalloc(&M.w_out, n * 4));
-            HIPCHK(c, hipMalloc(&M.tmp, std::max<size_t>(M.tmp_bytes, 16)));
         }
     }
     HIPCHK(c, hipMalloc(&c->G, sizeof(Globals)));
@@ -2687,8 +2686,16 @@ int tsdf_border_merge_device(tsdf_ctx* c, const uint32_t* d_recv, const uint64_t
     if (rc) return rc;
     uint32_t* bk = nullptr;
     HIPCHK(c, hipMalloc(&bk, total * TSDF_TILE_WORDS * 4));
+    // the backup joins the abort's restore list only once its snapshot is launched (a
+    // failed launch left uninitialised rows for the restore to write over held bricks)
+    {
+        const hipError_t e = launch_border_snapshot(c->T, c->Pl, d_recv, total, bk, c->stream);
+        if (e != hipSuccess) {
+            (void)hipFree(bk);
+            return fail(c, TSDF_EHIP, "border snapshot: %s", hipGetErrorString(e));
+        }
+    }
     c->brd_backup.push_back({bk, total});
-    HIPCHK(c, launch_border_snapshot(c->T, c->Pl, d_recv, total, bk, c->stream));
     uint64_t row = 0;
     for (uint32_t r = 0; r < world; r++) {  // sources in ascending rank order
         if (recv_counts[r])

@@ -97,7 +97,9 @@ static_assert(HCAP <= (1 << (PAIR_CNT_SHIFT - PAIR_LID_SHIFT)), "lid overflows")
 constexpr uint32_t OVF_TABLE = 1u, OVF_POOL = 2u, OVF_PAIRS = 4u, OVF_ACTIVE = 8u, OVF_FB = 16u,
                    OVF_SMP = 32u,  // the batch's samples exceed the sample list (single walk:
                                    // the workgroup regions)
-                   OVF_SPN = 64u;  // single walk: the batch's spans exceed the span list
+                   OVF_SPN = 64u,  // single walk: the batch's spans exceed the span list
+                   OVF_MG = 128u;  // merged pre-pass: a key / group table probe found no slot
+                                   // (cannot happen at its 1.25x sizing; not a growable capacity)
 // a border tile whose brick this context lacks (tsdf_border_merge_device; sticky like OVF_*)
 constexpr uint32_t ERR_MERGE_KEY = 1u << 8;
 
@@ -404,25 +406,24 @@ hipError_t launch_halo_build(const Table& H, const Pool& HP, const uint32_t* d_t
 // Voxblox MergedTsdfIntegrator's bundling pre-pass (tsdf_merged.hip): per batch, the points of
 // every scan bundled by voxel; xyz_out / w_out hold one ray per bundle at its first point's slot
 // (other slots: NaN point, weight 0), so the batch keeps its ray layout and block counts
+// Merged pre-pass buffers (tsdf_merged.hip), one set per batch parity
 struct MgBufs {
-    uint32_t *key = nullptr, *key2 = nullptr;  // the point's bundle id (its voxel's slot in tab)
-    uint32_t *idx = nullptr, *idx2 = nullptr;
-    float4* dw = nullptr;     // p - o and the point's getVoxelWeight
-    uint16_t* sid = nullptr;  // the point's scan in the batch | clearing << 15
-    float* xyz_out = nullptr;
-    float* w_out = nullptr;
-    void* tmp = nullptr;      // radix-sort scratch
-    size_t tmp_bytes = 0;
-    uint64_t cap = 0;         // points
-    // voxel key -> bundle id: open addressing over 2^tab_bits >= 2 cap slots (EMPTY between
-    // batches: k_mg_merge empties the slots it used)
+    uint32_t* slot = nullptr;  // per point: its key's record in tab (~0: dropped point)
+    uint32_t* gid = nullptr;   // per point: its (slot, scan) group in grp (~0: a one-point bundle)
+    float* xyz_out = nullptr;  // per point slot: the bundle ray's end point (NaN: no ray)
+    float* w_out = nullptr;    // its weight (negative: clearing)
+    uint64_t cap = 0;          // points
+    // bundle key -> record {key, seen mask, dup mask, pad} (4 u64): open addressing over
+    // 2^tab_bits >= 1.25 cap records, all zero between batches (k_mg_lead frees what it used)
     uint64_t* tab = nullptr;
-    uint32_t tab_bits = 0;
+    // (slot, scan) -> record {key, (~first point) | members << 32} (2 u64), the same size and life
+    uint64_t* grp = nullptr;
+    uint32_t tab_bits = 0, grp_bits = 0;
 };
 uint32_t mg_tab_bits(uint64_t n_points);
-size_t mg_sort_scratch(uint64_t n_points);
 hipError_t launch_mg_prepass(const float* d_xyz, const BatchRef& B, uint32_t n_blocks,
-                             uint64_t n_points, const RayConst& R, MgBufs& M, hipStream_t st);
+                             uint64_t n_points, const RayConst& R, MgBufs& M, uint32_t* ovf,
+                             hipStream_t st);
 // Ouster packets (tsdf_ouster.hip)
 struct OsField {
     uint32_t nbytes;  // little-endian source bytes (0: the profile has no such field)

@@ -1,25 +1,28 @@
 // tsdf_merged.hip — Voxblox MergedTsdfIntegrator's bundling pre-pass (tsdf_params.voxblox_method =
 // TSDF_VB_MERGED).  The bit-exact CPU twin is oracle/tsdf_oracle.c mg_bundle.
 //
-// Per batch, before the walk kernels:
-//   k_mg_keys   one lane per point (k_count's block layout: RPB points of one scan per block):
-//               isPointValid, getVoxelWeight and the bundle key (clearing bit | the point's voxel,
-//               21 biased bits per axis), inserted into a per-batch table whose slot becomes the
-//               point's bundle id (2^tab_bits for a dropped point); every output ray slot starts
-//               empty (NaN point, weight 0)
-//   radix sort  (bundle id, point index) pairs over the whole batch, tab_bits + 1 key bits
-//               (hipcub, stable: a bundle's points stay in cloud order, and equal voxels of
-//               different scans in scan order)
-//   k_mg_merge  one lane per sorted entry; the first entry of each (scan, key) run computes the
-//               bundle's running weighted mean of p - o (integrateVoxel's merge, in the run's
-//               order; a clearing bundle keeps its first kept point) and writes ONE ray -- o + mean,
-//               weight (negative: clearing) -- into the slot of the bundle's first point; the
-//               run's entries are loaded MG_U at a time ahead of the sequential merge.
+// A bundle is the points of ONE scan that fall into one (clearing, voxel) key; it casts one ray from
+// the running weighted mean of its points in cloud order.  About 97 % of a scan's points are alone in
+// their bundle, so the pre-pass (round 6) never sorts: it finds the multi-point bundles through a
+// batch-wide key table whose records carry per-scan bitmasks, merges only those, in place.
+//   k_mg_keys    one lane per point (k_count's block layout: RPB points of one scan per block):
+//                isPointValid and the bundle key (clearing bit | the point's voxel, 21 biased bits per
+//                axis) inserted into the table (its slot h is the point's `slot`), then
+//                seen[h] |= bit(scan) -- a second point of the scan in h also sets dup[h] |= bit(scan)
+//   k_mg_single  one lane per point: a point whose (slot, scan) is not dup is a one-point bundle and
+//                writes its ray at once (the merge's arithmetic for one point, bit for bit); a dup
+//                point joins its (slot, scan) group in a second table (count, and the group's first
+//                point by an atomic max of ~index)
+//   k_mg_lead    one lane per point: every point frees its key-table record for the next batch; a
+//                group's first point walks the scan's slots forward from itself, merges the group's
+//                members in cloud order (it stops after `count` of them) and writes the bundle's ray
+//                into its own slot, then frees the group record
+// Scans t and t + 64 of one batch share a mask bit: two one-point bundles of such scans in one voxel
+// both take the group path, which is exact too (each group merges its own scan's points).
 // The walk kernels then run unchanged over the batch's slots (RayConst::ray_w), so block counts,
-// offsets and the ray layout stay those of the input; empty slots leave at the walk's init.
+// offsets and the ray layout stay those of the input; empty slots (NaN point, weight 0) leave at the
+// walk's init.
 #include <hip/hip_runtime.h>
-
-#include <hipcub/hipcub.hpp>
 
 #include "tsdf_device.h"
 #include "tsdf_ray.h"
@@ -33,155 +36,236 @@ constexpr float MG_W_CAP = 1048576.0f;  // a bundle's weight cap (the fixed-poin
 constexpr int MG_VOX_LIM = 1 << 20;     // voxel indices beyond drop the point (21-bit key axes)
 // an empty key-table slot: no key is 0 (a kept voxel's biased axes lie in [1, 2^21 - 1])
 constexpr uint64_t MG_EMPTY = 0ull;
+constexpr uint32_t MG_NONE = ~0u;  // a dropped point's slot / a one-point bundle's group
+
+// One point's bundle facts, shared by the three kernels (the oracle's mg_bundle, op for op):
+// validity, the clearing flag, the bundle key, p - o and getVoxelWeight.
+struct MgPoint {
+    bool ok, clearing;
+    uint64_t key;
+    float dx, dy, dz, pw;
+};
+
+__device__ __forceinline__ MgPoint mg_point(const RayConst& R, float px, float py, float pz,
+                                            float ox, float oy, float oz, float zx, float zy,
+                                            float zz, bool axis) {
+    MgPoint m;
+    m.dx = px - ox;
+    m.dy = py - oy;
+    m.dz = pz - oz;
+    const float depth = __builtin_sqrtf(m.dx * m.dx + (m.dy * m.dy + m.dz * m.dz));
+    bool ok = depth > 0.0f && !(depth < R.min_range);
+    m.clearing = depth > R.max_range;
+    ok = ok && (!m.clearing || R.allow_clear);
+    // getGridIndexFromPoint(point_G, 1 / voxel_size): floor(x / vs + kCoordinateEpsilon)
+    const float fx = __builtin_floorf(px * R.inv_vs + 1e-6f);
+    const float fy = __builtin_floorf(py * R.inv_vs + 1e-6f);
+    const float fz = __builtin_floorf(pz * R.inv_vs + 1e-6f);
+    const float lim = (float)MG_VOX_LIM;
+    m.ok = ok && fx > -lim && fx < lim && fy > -lim && fy < lim && fz > -lim && fz < lim;
+    m.key = m.ok ? ((uint64_t)(m.clearing ? 1u : 0u) << 63) |
+                       ((uint64_t)(uint32_t)((int)fz + MG_VOX_LIM) << 42) |
+                       ((uint64_t)(uint32_t)((int)fy + MG_VOX_LIM) << 21) |
+                       (uint64_t)(uint32_t)((int)fx + MG_VOX_LIM)
+                 : MG_EMPTY;
+    m.pw = 1.0f;  // getVoxelWeight (vb_init's w0)
+    if (R.depth_w && axis) {
+        const float z = fabsf(zx * m.dx + (zy * m.dy + zz * m.dz));
+        m.pw = z > 1e-6f ? fminf(1.0f / (z * z), R.w0_cap) : 0.0f;
+    }
+    return m;
+}
+
+// integrateVoxel's merge step (kEpsilon; a clearing bundle keeps its first kept point only)
+__device__ __forceinline__ void mg_step(const MgPoint& p, bool clearing, float& mx, float& my,
+                                        float& mz, float& mw) {
+    if (p.pw < 1e-6f || (clearing && mw > 0.0f)) return;
+    const float nw = mw + p.pw;
+    mx = (mx * mw + p.dx * p.pw) / nw;
+    my = (my * mw + p.dy * p.pw) / nw;
+    mz = (mz * mw + p.dz * p.pw) / nw;
+    mw = mw + p.pw;
+}
+
+// The bundle's ray in the slot of its first point (no ray: NaN point, weight 0)
+__device__ __forceinline__ void mg_out(const MgBufs& M, uint32_t i, const ScanRec& s, bool clearing,
+                                       float mx, float my, float mz, float mw) {
+    float x = __builtin_nanf(""), y = x, z = x, w = 0.0f;
+    if (mw > 0.0f) {
+        x = s.ox + mx;
+        y = s.oy + my;
+        z = s.oz + mz;
+        const float bw = mw < MG_W_CAP ? mw : MG_W_CAP;
+        w = clearing ? -bw : bw;
+    }
+    M.xyz_out[3 * (size_t)i] = x;
+    M.xyz_out[3 * (size_t)i + 1] = y;
+    M.xyz_out[3 * (size_t)i + 2] = z;
+    M.w_out[i] = w;
+}
 
 __global__ __launch_bounds__(MG_THREADS) void k_mg_keys(const float* __restrict__ xyz, BatchRef D,
-                                                        RayConst R, MgBufs M) {
+                                                        RayConst R, MgBufs M, uint32_t* ovf) {
     uint32_t t, r0, r1;
     block_range(D, blockIdx.x, t, r0, r1);
-    const float ox = D.s[t].ox, oy = D.s[t].oy, oz = D.s[t].oz;
-    const float zx = D.s[t].zx, zy = D.s[t].zy, zz = D.s[t].zz;
-    const bool axis = zx != 0.0f || zy != 0.0f || zz != 0.0f;
-    const float nan = __builtin_nanf("");
-    const float* __restrict__ xs = xyz + 3 * (size_t)D.s[t].xoff;  // the input (ABI v10 xoff)
+    const ScanRec s = D.s[t];
+    const bool axis = s.zx != 0.0f || s.zy != 0.0f || s.zz != 0.0f;
+    const float* __restrict__ xs = xyz + 3 * (size_t)s.xoff;  // the input (ABI v10 xoff)
+    const uint64_t bit = 1ull << (t & 63u);
+    const uint64_t mask = (1ull << M.tab_bits) - 1ull;
     for (uint32_t i = r0 + threadIdx.x; i < r1; i += MG_THREADS) {
-        const float px = xs[3 * (size_t)i], py = xs[3 * (size_t)i + 1], pz = xs[3 * (size_t)i + 2];
-        const float dx = px - ox, dy = py - oy, dz = pz - oz;
-        const float depth = __builtin_sqrtf(dx * dx + (dy * dy + dz * dz));
-        bool ok = depth > 0.0f && !(depth < R.min_range);
-        const bool clearing = depth > R.max_range;
-        ok = ok && (!clearing || R.allow_clear);
-        // getGridIndexFromPoint(point_G, 1 / voxel_size): floor(x / vs + kCoordinateEpsilon)
-        const float fx = __builtin_floorf(px * R.inv_vs + 1e-6f);
-        const float fy = __builtin_floorf(py * R.inv_vs + 1e-6f);
-        const float fz = __builtin_floorf(pz * R.inv_vs + 1e-6f);
-        const float lim = (float)MG_VOX_LIM;
-        ok = ok && fx > -lim && fx < lim && fy > -lim && fy < lim && fz > -lim && fz < lim;
-        float pw = 1.0f;  // getVoxelWeight (vb_init's w0)
-        if (R.depth_w && axis) {
-            const float z = fabsf(zx * dx + (zy * dy + zz * dz));
-            pw = z > 1e-6f ? fminf(1.0f / (z * z), R.w0_cap) : 0.0f;
-        }
-        // the bundle id: the slot of (clearing, voxel) in the batch's key table; a dropped point
-        // sorts past every bundle
-        uint32_t id = 1u << M.tab_bits;
-        if (ok) {
-            const uint64_t key = ((uint64_t)(clearing ? 1u : 0u) << 63) |
-                                 ((uint64_t)(uint32_t)((int)fz + MG_VOX_LIM) << 42) |
-                                 ((uint64_t)(uint32_t)((int)fy + MG_VOX_LIM) << 21) |
-                                 (uint64_t)(uint32_t)((int)fx + MG_VOX_LIM);
-            const uint64_t mask = (1ull << M.tab_bits) - 1ull;
-            // the table holds >= 2x the batch's points, so a free slot always exists
-            for (uint64_t h = mix64(key) & mask;; h = (h + 1) & mask) {
-                const uint64_t k = M.tab[h];
-                if (k == key) { id = (uint32_t)h; break; }
+        const MgPoint p = mg_point(R, xs[3 * (size_t)i], xs[3 * (size_t)i + 1],
+                                   xs[3 * (size_t)i + 2], s.ox, s.oy, s.oz, s.zx, s.zy, s.zz, axis);
+        uint32_t h = MG_NONE;
+        if (p.ok) {
+            // the table holds >= 1.25 x the batch's points, so a free slot exists; the probe count
+            // is capped all the same (an exhausted probe drops the point and raises OVF_MG)
+            uint64_t q = mix64(p.key) & mask;
+            for (uint64_t n = 0; n <= mask; n++, q = (q + 1) & mask) {
+                const uint64_t k = M.tab[4 * q];
+                if (k == p.key) {
+                    h = (uint32_t)q;
+                    break;
+                }
                 if (k == MG_EMPTY) {
-                    const unsigned long long old = atomicCAS((unsigned long long*)&M.tab[h],
+                    const unsigned long long old = atomicCAS((unsigned long long*)&M.tab[4 * q],
                                                              (unsigned long long)MG_EMPTY,
-                                                             (unsigned long long)key);
-                    if (old == MG_EMPTY || old == key) { id = (uint32_t)h; break; }
+                                                             (unsigned long long)p.key);
+                    if (old == MG_EMPTY || old == p.key) {
+                        h = (uint32_t)q;
+                        break;
+                    }
                 }
             }
+            if (h == MG_NONE) {
+                atomicOr(ovf, OVF_MG);
+            } else {
+                const unsigned long long old = atomicOr((unsigned long long*)&M.tab[4 * (size_t)h + 1], bit);
+                if (old & bit) atomicOr((unsigned long long*)&M.tab[4 * (size_t)h + 2], bit);
+            }
         }
-        M.key[i] = id;
-        M.idx[i] = i;
-        M.dw[i] = make_float4(dx, dy, dz, pw);
-        M.sid[i] = (uint16_t)(t | (clearing ? 0x8000u : 0u));
-        M.xyz_out[3 * (size_t)i] = nan;
-        M.xyz_out[3 * (size_t)i + 1] = nan;
-        M.xyz_out[3 * (size_t)i + 2] = nan;
-        M.w_out[i] = 0.0f;
+        M.slot[i] = h;
     }
 }
 
-// One lane per sorted entry; the lane at a (scan, key) run start merges the run.  The merge is a
-// sequential running mean (bit for bit integrateVoxel's), but its operands need not arrive one
-// dependent round trip at a time: the lane loads MG_U entries ahead (keys and indices contiguous,
-// then the points' (d, w) gathers, all in flight together) and merges them from registers, so a
-// long bundle (a near-range blob: thousands of points in one voxel) costs ~MG_U times fewer
-// memory round trips.  A run ends at the next key or at the first point of a later scan (the sort
-// is stable and a batch's points are in scan order, so the run's indices stay below the scan's end).
-constexpr int MG_U = 8;
-__global__ __launch_bounds__(MG_THREADS) void k_mg_merge(BatchRef D, MgBufs M, uint32_t n) {
-    const uint32_t j = blockIdx.x * MG_THREADS + threadIdx.x;
-    if (j >= n) return;
-    const uint32_t key = M.key2[j];
-    if (key >= (1u << M.tab_bits)) return;  // dropped points
-    const uint32_t i0 = M.idx2[j];
-    const uint32_t st = M.sid[i0];
-    const uint32_t t = st & 0x7FFFu;
-    const uint32_t lo = D.s[t].off, hi = D.s[t + 1].off;  // scan t's points
-    const bool first = j == 0 || M.key2[j - 1] != key;   // the bundle id's first run
-    if (!first && M.idx2[j - 1] >= lo) return;            // not a run start
-    if (first) M.tab[key] = MG_EMPTY;                      // the slot is free for the next batch
-    const bool clearing = (st & 0x8000u) != 0;
-    float mx = 0.0f, my = 0.0f, mz = 0.0f, mw = 0.0f;
-    for (uint32_t q = j;; q += MG_U) {
-        uint32_t kk[MG_U];
-        uint32_t ii[MG_U];
-#pragma unroll
-        for (int u = 0; u < MG_U; u++) {
-            const bool in = q + u < n;
-            kk[u] = in ? M.key2[q + u] : ~key;
-            ii[u] = in ? M.idx2[q + u] : hi;
+__global__ __launch_bounds__(MG_THREADS) void k_mg_single(const float* __restrict__ xyz, BatchRef D,
+                                                          RayConst R, MgBufs M, uint32_t* ovf) {
+    uint32_t t, r0, r1;
+    block_range(D, blockIdx.x, t, r0, r1);
+    const ScanRec s = D.s[t];
+    const bool axis = s.zx != 0.0f || s.zy != 0.0f || s.zz != 0.0f;
+    const float* __restrict__ xs = xyz + 3 * (size_t)s.xoff;
+    const uint64_t gmask = (1ull << M.grp_bits) - 1ull;
+    for (uint32_t i = r0 + threadIdx.x; i < r1; i += MG_THREADS) {
+        const uint32_t h = M.slot[i];
+        uint32_t g = MG_NONE;
+        bool single = false;
+        if (h != MG_NONE) single = ((M.tab[4 * (size_t)h + 2] >> (t & 63u)) & 1ull) == 0ull;
+        if (single) {  // a one-point bundle: its ray now
+            const MgPoint p = mg_point(R, xs[3 * (size_t)i], xs[3 * (size_t)i + 1],
+                                       xs[3 * (size_t)i + 2], s.ox, s.oy, s.oz, s.zx, s.zy, s.zz,
+                                       axis);
+            float mx = 0.0f, my = 0.0f, mz = 0.0f, mw = 0.0f;
+            mg_step(p, p.clearing, mx, my, mz, mw);
+            mg_out(M, i, s, p.clearing, mx, my, mz, mw);
+        } else {
+            mg_out(M, i, s, false, 0.0f, 0.0f, 0.0f, 0.0f);  // no ray here (a group's leader's later)
+            if (h != MG_NONE) {  // join the (slot, scan) group
+                const uint64_t key = ((uint64_t)h << 16) | (uint64_t)(t + 1u);  // never 0
+                uint64_t q = mix64(key) & gmask;
+                for (uint64_t n = 0; n <= gmask; n++, q = (q + 1) & gmask) {
+                    const uint64_t k = M.grp[2 * q];
+                    if (k == key) {
+                        g = (uint32_t)q;
+                        break;
+                    }
+                    if (k == MG_EMPTY) {
+                        const unsigned long long old = atomicCAS((unsigned long long*)&M.grp[2 * q],
+                                                                 (unsigned long long)MG_EMPTY,
+                                                                 (unsigned long long)key);
+                        if (old == MG_EMPTY || old == key) {
+                            g = (uint32_t)q;
+                            break;
+                        }
+                    }
+                }
+                if (g == MG_NONE) {
+                    atomicOr(ovf, OVF_MG);
+                } else {
+                    uint32_t* v = reinterpret_cast<uint32_t*>(&M.grp[2 * (size_t)g + 1]);
+                    atomicMax(&v[0], ~i);  // the group's first point (~index: 0 means none)
+                    atomicAdd(&v[1], 1u);  // its members
+                }
+            }
         }
-        float4 dd[MG_U];
-#pragma unroll
-        for (int u = 0; u < MG_U; u++)
-            dd[u] = (kk[u] == key && ii[u] < hi) ? M.dw[ii[u]] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        bool end = false;
-#pragma unroll
-        for (int u = 0; u < MG_U; u++) {
-            end = end || kk[u] != key || ii[u] >= hi;
-            const float4 d = dd[u];
-            // kEpsilon; a clearing bundle keeps its first kept point only
-            if (end || d.w < 1e-6f || (clearing && mw > 0.0f)) continue;
-            const float nw = mw + d.w;
-            mx = (mx * mw + d.x * d.w) / nw;
-            my = (my * mw + d.y * d.w) / nw;
-            mz = (mz * mw + d.z * d.w) / nw;
-            mw = mw + d.w;
-        }
-        if (end) break;
+        M.gid[i] = g;
     }
-    if (!(mw > 0.0f)) return;
-    M.xyz_out[3 * (size_t)i0] = D.s[t].ox + mx;
-    M.xyz_out[3 * (size_t)i0 + 1] = D.s[t].oy + my;
-    M.xyz_out[3 * (size_t)i0 + 2] = D.s[t].oz + mz;
-    const float bw = mw < MG_W_CAP ? mw : MG_W_CAP;
-    M.w_out[i0] = clearing ? -bw : bw;
+}
+
+__global__ __launch_bounds__(MG_THREADS) void k_mg_lead(const float* __restrict__ xyz, BatchRef D,
+                                                        RayConst R, MgBufs M) {
+    uint32_t t, r0, r1;
+    block_range(D, blockIdx.x, t, r0, r1);
+    const ScanRec s = D.s[t];
+    const uint32_t hi = D.s[t + 1].off;  // scan t's points end here
+    const bool axis = s.zx != 0.0f || s.zy != 0.0f || s.zz != 0.0f;
+    const float* __restrict__ xs = xyz + 3 * (size_t)s.xoff;
+    for (uint32_t i = r0 + threadIdx.x; i < r1; i += MG_THREADS) {
+        const uint32_t h = M.slot[i];
+        if (h == MG_NONE) continue;
+        // every read of this record happened in k_mg_keys / k_mg_single: free it for the next batch
+        // (idempotent: every point of the slot writes the same zeros)
+        *reinterpret_cast<ulonglong2*>(&M.tab[4 * (size_t)h]) = make_ulonglong2(0ull, 0ull);
+        M.tab[4 * (size_t)h + 2] = 0ull;
+        const uint32_t g = M.gid[i];
+        if (g == MG_NONE) continue;
+        const uint64_t v = M.grp[2 * (size_t)g + 1];
+        if (~(uint32_t)v != i) continue;  // not the group's first point (or already freed: 0)
+        const uint32_t cnt = (uint32_t)(v >> 32);
+        // the group record is read by its members only for this test: the leader frees it now (a
+        // member reading the zeros afterwards sees ~0 != its index, i.e. not the leader, as before)
+        *reinterpret_cast<ulonglong2*>(&M.grp[2 * (size_t)g]) = make_ulonglong2(0ull, 0ull);
+        // the members are the points of scan t in slot h, in cloud order from this one on
+        float mx = 0.0f, my = 0.0f, mz = 0.0f, mw = 0.0f;
+        bool clearing = false;
+        uint32_t found = 0;
+        for (uint32_t j = i; j < hi && found < cnt; j++) {
+            if (M.slot[j] != h) continue;
+            const MgPoint p = mg_point(R, xs[3 * (size_t)j], xs[3 * (size_t)j + 1],
+                                       xs[3 * (size_t)j + 2], s.ox, s.oy, s.oz, s.zx, s.zy, s.zz,
+                                       axis);
+            clearing = p.clearing;  // (the slot's key carries it: the same for every member)
+            mg_step(p, clearing, mx, my, mz, mw);
+            found++;
+        }
+        mg_out(M, i, s, clearing, mx, my, mz, mw);
+    }
 }
 
 }  // namespace
 
 uint32_t mg_tab_bits(uint64_t n_points) {
     uint32_t b = 4;
-    while ((1ull << b) < 2 * n_points) b++;
+    while ((1ull << b) < n_points + n_points / 4) b++;  // >= 1.25 x the batch's points
     return b;
 }
 
-size_t mg_sort_scratch(uint64_t n_points) {
-    size_t bytes = 0;
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const uint32_t*)nullptr,
-                                             (uint32_t*)nullptr, (const uint32_t*)nullptr,
-                                             (uint32_t*)nullptr, (int)n_points, 0,
-                                             (int)mg_tab_bits(n_points) + 1);
-    return bytes;
-}
-
 hipError_t launch_mg_prepass(const float* d_xyz, const BatchRef& B, uint32_t n_blocks,
-                             uint64_t n_points, const RayConst& R, MgBufs& M, hipStream_t st) {
+                             uint64_t n_points, const RayConst& R, MgBufs& M, uint32_t* ovf,
+                             hipStream_t st) {
     if (!n_points) return hipSuccess;
     if (n_points > M.cap) return hipErrorInvalidValue;
-    k_mg_keys<<<n_blocks, MG_THREADS, 0, st>>>(d_xyz, B, R, M);
-    size_t bytes = M.tmp_bytes;
-    // bundle ids are table slots (< 2^tab_bits) or 2^tab_bits for a dropped point: tab_bits + 1
-    // key bits instead of the 64 of the voxel keys (4 sort passes instead of 8)
-    hipError_t e = hipcub::DeviceRadixSort::SortPairs(M.tmp, bytes, M.key, M.key2, M.idx, M.idx2,
-                                                      (int)n_points, 0, (int)M.tab_bits + 1, st);
-    if (e != hipSuccess) return e;
-    k_mg_merge<<<(uint32_t)((n_points + MG_THREADS - 1) / MG_THREADS), MG_THREADS, 0, st>>>(
-        B, M, (uint32_t)n_points);
-    return hipGetLastError();
+    k_mg_keys<<<n_blocks, MG_THREADS, 0, st>>>(d_xyz, B, R, M, ovf);
+    k_mg_single<<<n_blocks, MG_THREADS, 0, st>>>(d_xyz, B, R, M, ovf);
+    k_mg_lead<<<n_blocks, MG_THREADS, 0, st>>>(d_xyz, B, R, M);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        // a pre-pass cut short may leave keys and groups in the tables: empty them, so the next
+        // batch starts from empty tables
+        (void)hipMemsetAsync(M.tab, 0, (size_t)32 << M.tab_bits, st);
+        (void)hipMemsetAsync(M.grp, 0, (size_t)16 << M.grp_bits, st);
+    }
+    return e;
 }
 
 }  // namespace tsdf

@@ -25,7 +25,10 @@ def main():
                          "fed by tsdf_integrate_sectors (--sector-input: fanout = one H2D and "
                          "device copies, h2d = one H2D per context, split = host classification)")
     ap.add_argument("--sector-input", default="fanout", choices=("fanout", "h2d", "split"),
-                    help="tsdf_params.sector_input of the N contexts (ABI v8)")
+                    help="tsdf_params.sector_input of the N contexts (ABI v8; world rule only)")
+    ap.add_argument("--sector-rule", default="index", choices=("index", "world"),
+                    help="tsdf_params.sector_rule (ABI v10): index = each context packs and copies "
+                         "only its contiguous 1/N of the cloud")
     ap.add_argument("--semantics", default="vdbfusion_f64")
     ap.add_argument("--max-batch", type=int, default=32)
     args = ap.parse_args()
@@ -50,7 +53,8 @@ def main():
     vols = [HipTSDFVolume(0.05, 0.15, max_points=1 << 17, max_bricks=1 << 20,
                           max_batch=args.max_batch, semantics=args.semantics,
                           n_sectors=n if n > 1 else 0, sector=k,
-                          sector_input=args.sector_input) for k in range(n)]
+                          sector_input=args.sector_input, sector_rule=args.sector_rule)
+            for k in range(n)]
     vol = vols[0]
     lib = vol._lib
     ctxs = (C.c_void_p * n)(*[v._ctx.value for v in vols])
@@ -82,6 +86,7 @@ def main():
                                  else "tsdf_integrate"),
                       "value": round(args.scans / dt, 2), "scans": args.scans, "sectors": n,
                       "sector_input": args.sector_input if n > 1 else None,
+                      "sector_rule": args.sector_rule if n > 1 else None,
                       "semantics": args.semantics, "max_batch": args.max_batch,
                       "bytes_per_scan_host": int(clouds[0].nbytes),
                       "h2d_bytes_per_scan": int(clouds[0].shape[0] * 12),

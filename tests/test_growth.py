@@ -129,8 +129,9 @@ def test_large_batches_bitwise(sim):
 @pytest.mark.parametrize("walk", ["two", "single"])
 def test_sector_sample_list_grows(sim, walk):
     """A sharded context sizes its sample list (single walk: its k_walk regions) for 1 / n_sectors
-    of the rays; scans whose points all lie in its sector overflow it, and it grows (OVF_SMP)
-    without losing an update."""
+    of the rays; scans whose points all lie in its world-frame sector (the world rule: an
+    index-rule context takes 1 / n_sectors of every cloud by construction) overflow it, and it
+    grows (OVF_SMP) without losing an update."""
     import torch
     from tsdf_map import sector_ids
     # two walks: 819 k sample slots for 8 x 2^15 points; single walk: 1184 regions of 512 rays for
@@ -147,11 +148,11 @@ def test_sector_sample_list_grows(sim, walk):
     org = np.stack([o for _, o in scans])
     d = torch.from_numpy(allp).to("cuda:0")
     torch.cuda.synchronize()
-    g = hip(n_sectors=8, sector=0, walk=walk, **kw)
+    g = hip(n_sectors=8, sector=0, walk=walk, sector_rule="world", **kw)
     g.integrate_batch_device(d.data_ptr(), offs, org)
     g.sync()
     assert g.stats()["n_grows"] >= 1
-    o = ora(n_sectors=8, sector=0)
+    o = ora(n_sectors=8, sector=0, sector_rule="world")
     for p, q in scans:
         o.integrate(p, q)
     assert bitwise(g, o)

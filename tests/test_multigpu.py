@@ -42,13 +42,17 @@ def voxels_equal_bitwise(a, b):
             and np.array_equal(as_.view(np.uint32), bs.view(np.uint32)))
 
 
-@pytest.mark.parametrize("n,yaw0", [(4, 0.0), (3, 0.7)])
-def test_sector_filter_bitwise(sim, n, yaw0):
+@pytest.mark.parametrize("n,yaw0,rule", [(4, 0.0, "world"), (3, 0.7, "world"), (4, 0.0, "index"),
+                                         (3, 0.7, "index")])
+def test_sector_filter_bitwise(sim, n, yaw0, rule):
+    """Each sector context against its oracle twin, bit for bit, and the sectors partition the
+    rays -- the world-frame azimuth filter in the walk kernels, and (ABI v10) the index rule's
+    contiguous share of every cloud."""
     scans = [sim.scan(k) for k in (0, 5)]
     rays = 0
     for k in range(n):
-        g = hip(n_sectors=n, sector=k, sector_yaw0=yaw0)
-        o = ora(n_sectors=n, sector=k, sector_yaw0=yaw0)
+        g = hip(n_sectors=n, sector=k, sector_yaw0=yaw0, sector_rule=rule)
+        o = ora(n_sectors=n, sector=k, sector_yaw0=yaw0, sector_rule=rule)
         for pts, org in scans:
             g.integrate(pts, org)
             o.integrate(pts, org)
@@ -312,20 +316,25 @@ def test_sectors_bare_origin_voxblox_depth_weight(sim):
         assert voxels_equal_bitwise(g[r].export_voxels(), o[r].export_voxels()), r
 
 
-@pytest.mark.parametrize("n,f64,mode", [(3, False, "split"), (4, True, "split"),
-                                         (8, False, "split"), (3, False, "fanout"),
-                                         (4, True, "fanout"), (8, False, "h2d")])
-def test_integrate_sectors_bitwise(sim, n, f64, mode):
+@pytest.mark.parametrize("n,f64,mode,rule", [(3, False, "split", "world"), (4, True, "split", "world"),
+                                              (8, False, "split", "world"),
+                                              (3, False, "fanout", "world"),
+                                              (4, True, "fanout", "world"), (8, False, "h2d", "world"),
+                                              (3, False, "fanout", "index"),
+                                              (4, True, "fanout", "index"),
+                                              (8, False, "fanout", "index")])
+def test_integrate_sectors_bitwise(sim, n, f64, mode, rule):
     """tsdf_integrate_sectors (the live N-GPU input) equals each context integrating
     the full cloud with its in-kernel sector filter (the oracle), bit for bit, for every transfer
     (tsdf_params.sector_input): split (host classification, each context gets its sector's
     points), fanout (one H2D, device-to-device copies to the other contexts) and h2d (one H2D per
-    context from one packed buffer)."""
+    context from one packed buffer).  With the index rule (ABI v10) every context packs and copies
+    only its contiguous share of the cloud, whatever sector_input says."""
     from tsdf_map import integrate_sectors
     yaw0 = 0.4
-    g = [hip(n_sectors=n, sector=r, sector_yaw0=yaw0, max_batch=2, sector_input=mode)
-         for r in range(n)]
-    o = [ora(n_sectors=n, sector=r, sector_yaw0=yaw0) for r in range(n)]
+    g = [hip(n_sectors=n, sector=r, sector_yaw0=yaw0, max_batch=2, sector_input=mode,
+             sector_rule=rule) for r in range(n)]
+    o = [ora(n_sectors=n, sector=r, sector_yaw0=yaw0, sector_rule=rule) for r in range(n)]
     rays = total = 0
     for k in (0, 1, 9):
         pts, org = sim.scan(k)
@@ -346,7 +355,10 @@ def test_integrate_sectors_bitwise(sim, n, f64, mode):
     for r in range(n):
         g[r].sync()
         assert voxels_equal_bitwise(g[r].export_voxels(), o[r].export_voxels()), r
-    if mode == "split":
+    if rule == "index":  # each context received exactly its share
+        assert sum(v.stats()["n_points_in"] for v in g) == total
+        assert max(v.stats()["n_points_in"] for v in g) <= -(-total // n) + 3
+    elif mode == "split":
         assert sum(v.stats()["n_points_in"] for v in g) == rays  # each point went to one context
     else:
         assert all(v.stats()["n_points_in"] == total for v in g)  # every context got the cloud
@@ -358,9 +370,10 @@ def test_fanout_out_of_lockstep(sim):
     leader destroyed while its followers still hold uncopied points all leave every context equal
     to its oracle twin."""
     from tsdf_map import integrate_sectors
-    n, yaw0 = 3, 0.3
-    g = [hip(n_sectors=n, sector=r, sector_yaw0=yaw0, max_batch=3) for r in range(n)]
-    o = [ora(n_sectors=n, sector=r, sector_yaw0=yaw0) for r in range(n)]
+    n, yaw0 = 3, 0.3  # (the fan-out serves the world rule)
+    g = [hip(n_sectors=n, sector=r, sector_yaw0=yaw0, max_batch=3, sector_rule="world")
+         for r in range(n)]
+    o = [ora(n_sectors=n, sector=r, sector_yaw0=yaw0, sector_rule="world") for r in range(n)]
     scans = []
     for k in (0, 1, 2, 5, 7, 9, 11):
         pts, org = sim.scan(k)
@@ -393,12 +406,14 @@ def test_fanout_out_of_lockstep(sim):
         assert voxels_equal_bitwise(g[r].export_voxels(), o[r].export_voxels()), r
 
 
-def test_integrate_sectors_voxblox_merged(sim):
-    """MergedTsdfIntegrator bundles the whole scan before the sector filter, so the sectors take the
-    fan-out (a requested host split is overridden): every context equals its oracle twin."""
+@pytest.mark.parametrize("rule", ["world", "index"])
+def test_integrate_sectors_voxblox_merged(sim, rule):
+    """MergedTsdfIntegrator: with the world rule each context bundles the whole scan before its
+    sector filter, so the sectors take the fan-out (a requested host split is overridden); with the
+    index rule each context bundles its own share.  Every context equals its oracle twin."""
     from tsdf_map import integrate_sectors
     n, yaw0 = 3, 0.2
-    kw = dict(semantics="voxblox", method="merged", use_const_weight=False)
+    kw = dict(semantics="voxblox", method="merged", use_const_weight=False, sector_rule=rule)
     g = [hip(n_sectors=n, sector=r, sector_yaw0=yaw0, max_batch=2, sector_input="split", **kw)
          for r in range(n)]
     o = [ora(n_sectors=n, sector=r, sector_yaw0=yaw0, **kw) for r in range(n)]
@@ -421,3 +436,35 @@ def test_sharded_contexts_report_peer_reach():
     assert all(v.stats()["peer_mask"] == 0b111 for v in g)
     for v in g:
         v.close()
+
+
+@pytest.mark.parametrize("kw", [dict(), dict(semantics="vdbfusion"),
+                                dict(semantics="voxblox", method="merged", use_const_weight=False),
+                                dict(semantics="voxblox", use_const_weight=False),
+                                dict(walk="single")])
+def test_index_rule_device_batches_bitwise(sim, kw):
+    """ABI v10's index rule on resident device batches (the bench's path): each sector context
+    reads only its contiguous share of every scan of the batch -- shares that are not contiguous
+    in the batch buffer (ScanRec.xoff) -- and equals its oracle twin bit for bit; the shares
+    partition the rays.  Covers both walks' point reads and the merged pre-pass's."""
+    import torch
+    n = 3
+    scans = [sim.scan(k) for k in (0, 3, 6, 9)]
+    pts = [np.ascontiguousarray(p[::3]) for p, _ in scans]
+    offs = np.cumsum([0] + [p.shape[0] for p in pts]).astype(np.uint64)
+    poses = np.stack([np.concatenate([o, [0.0, 0.0, np.sin(0.1 * k), np.cos(0.1 * k)]])
+                      for k, (_, o) in enumerate(scans)])
+    d = torch.from_numpy(np.concatenate(pts)).to("cuda:0")
+    torch.cuda.synchronize()
+    rays = 0
+    for r in range(n):
+        g = hip(n_sectors=n, sector=r, max_batch=4, **kw)
+        o = ora(n_sectors=n, sector=r, **kw)
+        g.integrate_batch_device(d.data_ptr(), offs, poses)
+        for p, q in zip(pts, poses):
+            o.integrate(p, q)
+        g.sync()
+        assert voxels_equal_bitwise(g.export_voxels(), o.export_voxels()), r
+        assert g.stats()["n_points_in"] == o.stats()["n_points_in"]
+        rays += g.stats()["n_points_in"]
+    assert rays == int(offs[-1])

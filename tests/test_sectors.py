@@ -48,15 +48,18 @@ def test_sector_geometry():
     assert np.array_equal(sector_ids(axes, o, 4, 0.0), [0, 1, 2, 3, 0])
 
 
-def test_oracle_sector_filter_partitions_the_field(scan0):
-    """n sector-filtered oracle volumes together hold every ray of the scan exactly once."""
+@pytest.mark.parametrize("rule", ["world", "index"])
+def test_oracle_sector_filter_partitions_the_field(scan0, rule):
+    """n sector-filtered oracle volumes together hold every ray of the scan exactly once (both
+    rules: world-frame azimuth sectors, and the index rule's contiguous shares)."""
     pts, org = scan0
     pts = np.ascontiguousarray(pts[::16])
     full = oracle.OracleTSDFVolume(0.05, 0.15)
     full.integrate(pts, org)
     rays = 0
     for k in range(3):
-        v = oracle.OracleTSDFVolume(0.05, 0.15, n_sectors=3, sector=k, sector_yaw0=1.0)
+        v = oracle.OracleTSDFVolume(0.05, 0.15, n_sectors=3, sector=k, sector_yaw0=1.0,
+                                    sector_rule=rule)
         v.integrate(pts, org)
         rays += v.stats()["n_rays_total"]
     assert rays == full.stats()["n_rays_total"]
