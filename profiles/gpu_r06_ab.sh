@@ -16,6 +16,6 @@ for i in $(seq 1 $R); do
   for nl in "$@"; do
     n=${nl%%=*}; lib=${nl#*=}
     TSDF_HIP_LIB=$lib timeout -k 10 200 python3 bench.py --no-cpu --steps 32 $BENCH_ARGS > $O/${n}_$i.json 2> $O/${n}_$i.err || { tail -3 $O/${n}_$i.err; exit 1; }
-    python3 -c "import json; d=json.load(open('$O/${n}_$i.json')); print('${n}_$i', d['value'], d['ms_per_step'], d.get('serial_kernel_ms_per_launch'), d['parity']['bitwise'])"
+    python3 -c "import json; d=json.load(open('$O/${n}_$i.json')); print('${n}_$i', d['value'], d['ms_per_step'], d.get('serial_kernel_ms_per_launch'), (d.get('parity') or {}).get('bitwise'))"
   done
 done
