@@ -1133,8 +1133,8 @@ void tsdf_destroy(tsdf_ctx* c) {
         if (c->h_stage[i]) (void)hipHostFree(c->h_stage[i]);
         if (c->stage_done[i]) (void)hipEventDestroy(c->stage_done[i]);
         MgBufs& M = c->mg[i];
-        for (void* q : {(void*)M.slot, (void*)M.gid, (void*)M.xyz_out, (void*)M.w_out,
-                        (void*)M.tab, (void*)M.grp})
+        for (void* q : {(void*)M.slot, (void*)M.gid, (void*)M.next, (void*)M.xyz_out,
+                        (void*)M.w_out, (void*)M.tab, (void*)M.grp})
             if (q) (void)hipFree(q);
     }
     if (c->bc_ev) (void)hipEventDestroy(c->bc_ev);
@@ -1299,10 +1299,11 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
             M.tab_bits = M.grp_bits = mg_tab_bits(n);  // >= 1.25 n records each
             HIPCHK(c, hipMalloc(&M.tab, (size_t)32 << M.tab_bits));
             HIPCHK(c, hipMemset(M.tab, 0, (size_t)32 << M.tab_bits));  // every record empty
-            HIPCHK(c, hipMalloc(&M.grp, (size_t)16 << M.grp_bits));
-            HIPCHK(c, hipMemset(M.grp, 0, (size_t)16 << M.grp_bits));
+            HIPCHK(c, hipMalloc(&M.grp, (size_t)32 << M.grp_bits));
+            HIPCHK(c, hipMemset(M.grp, 0, (size_t)32 << M.grp_bits));
             HIPCHK(c, hipMalloc(&M.slot, n * 4));
             HIPCHK(c, hipMalloc(&M.gid, n * 4));
+            HIPCHK(c, hipMalloc(&M.next, n * 4));
             HIPCHK(c, hipMalloc(&M.xyz_out, n * 12));
             HIPCHK(c, hipMalloc(&M.w_out, n * 4));
         }

@@ -410,13 +410,15 @@ hipError_t launch_halo_build(const Table& H, const Pool& HP, const uint32_t* d_t
 struct MgBufs {
     uint32_t* slot = nullptr;  // per point: its key's record in tab (~0: dropped point)
     uint32_t* gid = nullptr;   // per point: its (slot, scan) group in grp (~0: a one-point bundle)
+    uint32_t* next = nullptr;  // per group member: the next chain entry (index + 1; 0 ends it)
     float* xyz_out = nullptr;  // per point slot: the bundle ray's end point (NaN: no ray)
     float* w_out = nullptr;    // its weight (negative: clearing)
     uint64_t cap = 0;          // points
     // bundle key -> record {key, seen mask, dup mask, pad} (4 u64): open addressing over
     // 2^tab_bits >= 1.25 cap records, all zero between batches (k_mg_lead frees what it used)
     uint64_t* tab = nullptr;
-    // (slot, scan) -> record {key, (~first point) | members << 32} (2 u64), the same size and life
+    // (slot, scan) -> record {key, (~first member) | members << 32, last member | chain head << 32,
+    // pad} (4 u64), the same size and life
     uint64_t* grp = nullptr;
     uint32_t tab_bits = 0, grp_bits = 0;
 };

@@ -11,12 +11,16 @@
 //                seen[h] |= bit(scan) -- a second point of the scan in h also sets dup[h] |= bit(scan)
 //   k_mg_single  one lane per point: a point whose (slot, scan) is not dup is a one-point bundle and
 //                writes its ray at once (the merge's arithmetic for one point, bit for bit); a dup
-//                point joins its (slot, scan) group in a second table (count, and the group's first
-//                point by an atomic max of ~index)
+//                point joins its (slot, scan) group in a second table: the member count, the first
+//                and last members (atomic max of ~index / index) and a member chain (atomic exchange
+//                of the chain head; `next` per point)
 //   k_mg_lead    one lane per point: every point frees its key-table record for the next batch; a
-//                group's first point walks the scan's slots forward from itself, merges the group's
-//                members in cloud order (it stops after `count` of them) and writes the bundle's ray
-//                into its own slot, then frees the group record
+//                group's first point merges the group's members in cloud order and writes the
+//                bundle's ray into its own slot, then frees the group record.  It finds the members
+//                either by walking the scan's slots forward from itself (cost: the span from first
+//                to last member) or, for a few members spread far apart -- a voxel on the seam of
+//                the spin, whose members sit at both ends of the cloud -- by repeated selection of
+//                the next index from the chain (cost: members^2)
 // Scans t and t + 64 of one batch share a mask bit: two one-point bundles of such scans in one voxel
 // both take the group path, which is exact too (each group merges its own scan's points).
 // The walk kernels then run unchanged over the batch's slots (RayConst::ray_w), so block counts,
@@ -174,13 +178,13 @@ __global__ __launch_bounds__(MG_THREADS) void k_mg_single(const float* __restric
                 const uint64_t key = ((uint64_t)h << 16) | (uint64_t)(t + 1u);  // never 0
                 uint64_t q = mix64(key) & gmask;
                 for (uint64_t n = 0; n <= gmask; n++, q = (q + 1) & gmask) {
-                    const uint64_t k = M.grp[2 * q];
+                    const uint64_t k = M.grp[4 * q];
                     if (k == key) {
                         g = (uint32_t)q;
                         break;
                     }
                     if (k == MG_EMPTY) {
-                        const unsigned long long old = atomicCAS((unsigned long long*)&M.grp[2 * q],
+                        const unsigned long long old = atomicCAS((unsigned long long*)&M.grp[4 * q],
                                                                  (unsigned long long)MG_EMPTY,
                                                                  (unsigned long long)key);
                         if (old == MG_EMPTY || old == key) {
@@ -192,9 +196,11 @@ __global__ __launch_bounds__(MG_THREADS) void k_mg_single(const float* __restric
                 if (g == MG_NONE) {
                     atomicOr(ovf, OVF_MG);
                 } else {
-                    uint32_t* v = reinterpret_cast<uint32_t*>(&M.grp[2 * (size_t)g + 1]);
-                    atomicMax(&v[0], ~i);  // the group's first point (~index: 0 means none)
-                    atomicAdd(&v[1], 1u);  // its members
+                    uint32_t* v = reinterpret_cast<uint32_t*>(&M.grp[4 * (size_t)g + 1]);
+                    atomicMax(&v[0], ~i);                 // the first member (~index; 0: none)
+                    atomicAdd(&v[1], 1u);                 // the members
+                    atomicMax(&v[2], i);                  // the last member
+                    M.next[i] = atomicExch(&v[3], i + 1u);  // the chain (index + 1; 0 ends it)
                 }
             }
         }
@@ -219,24 +225,49 @@ __global__ __launch_bounds__(MG_THREADS) void k_mg_lead(const float* __restrict_
         M.tab[4 * (size_t)h + 2] = 0ull;
         const uint32_t g = M.gid[i];
         if (g == MG_NONE) continue;
-        const uint64_t v = M.grp[2 * (size_t)g + 1];
+        const uint64_t v = M.grp[4 * (size_t)g + 1];
         if (~(uint32_t)v != i) continue;  // not the group's first point (or already freed: 0)
         const uint32_t cnt = (uint32_t)(v >> 32);
+        const uint64_t v2 = M.grp[4 * (size_t)g + 2];
+        const uint32_t last = (uint32_t)v2, head = (uint32_t)(v2 >> 32);
         // the group record is read by its members only for this test: the leader frees it now (a
         // member reading the zeros afterwards sees ~0 != its index, i.e. not the leader, as before)
-        *reinterpret_cast<ulonglong2*>(&M.grp[2 * (size_t)g]) = make_ulonglong2(0ull, 0ull);
+        *reinterpret_cast<ulonglong2*>(&M.grp[4 * (size_t)g]) = make_ulonglong2(0ull, 0ull);
+        M.grp[4 * (size_t)g + 2] = 0ull;
         // the members are the points of scan t in slot h, in cloud order from this one on
         float mx = 0.0f, my = 0.0f, mz = 0.0f, mw = 0.0f;
         bool clearing = false;
-        uint32_t found = 0;
-        for (uint32_t j = i; j < hi && found < cnt; j++) {
-            if (M.slot[j] != h) continue;
+        auto merge_at = [&](uint32_t j) {
             const MgPoint p = mg_point(R, xs[3 * (size_t)j], xs[3 * (size_t)j + 1],
                                        xs[3 * (size_t)j + 2], s.ox, s.oy, s.oz, s.zx, s.zy, s.zz,
                                        axis);
             clearing = p.clearing;  // (the slot's key carries it: the same for every member)
             mg_step(p, clearing, mx, my, mz, mw);
-            found++;
+        };
+        const uint32_t span = last - i + 1u;
+        if (span <= 4096u || (uint64_t)cnt * cnt > span / 8u) {
+            // forward over the scan's slots (sequential 4-B reads)
+            uint32_t found = 0;
+            for (uint32_t j = i; j <= last && j < hi && found < cnt; j++) {
+                if (M.slot[j] != h) continue;
+                merge_at(j);
+                found++;
+            }
+        } else {
+            // few members far apart: the next member is the smallest chain index above the
+            // current one (the chain holds exactly the group's members)
+            uint32_t cur = i;
+            merge_at(cur);
+            for (uint32_t k = 1; k < cnt; k++) {
+                uint32_t best = ~0u;
+                for (uint32_t e = head; e != 0u; e = M.next[e - 1u]) {
+                    const uint32_t j = e - 1u;
+                    best = j > cur && j < best ? j : best;
+                }
+                if (best == ~0u) break;  // (cannot happen: cnt members are chained)
+                cur = best;
+                merge_at(cur);
+            }
         }
         mg_out(M, i, s, clearing, mx, my, mz, mw);
     }
@@ -263,7 +294,7 @@ hipError_t launch_mg_prepass(const float* d_xyz, const BatchRef& B, uint32_t n_b
         // a pre-pass cut short may leave keys and groups in the tables: empty them, so the next
         // batch starts from empty tables
         (void)hipMemsetAsync(M.tab, 0, (size_t)32 << M.tab_bits, st);
-        (void)hipMemsetAsync(M.grp, 0, (size_t)16 << M.grp_bits, st);
+        (void)hipMemsetAsync(M.grp, 0, (size_t)32 << M.grp_bits, st);
     }
     return e;
 }

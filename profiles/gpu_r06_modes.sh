@@ -7,9 +7,9 @@ export TMPDIR=/tmp
 O=gpurun_out/r06/$1
 mkdir -p $O
 run() {  # name, timeout, args...
-  n=$1; t=$2; shift 2
-  timeout -k 10 $t python3 "$@" > $O/$n.json 2> $O/$n.err || { echo "FAILED $n"; tail -5 $O/$n.err; exit 1; }
-  python3 - "$O/$n.json" "$n" <<'PY'
+  local nm=$1 tl=$2; shift 2
+  timeout -k 10 $tl python3 "$@" > $O/$nm.json 2> $O/$nm.err || { echo "FAILED $nm"; tail -5 $O/$nm.err; exit 1; }
+  python3 - "$O/$nm.json" "$nm" <<'PY'
 import json, sys
 for ln in open(sys.argv[1]):
     ln = ln.strip()
@@ -20,12 +20,13 @@ for ln in open(sys.argv[1]):
 PY
 }
 B="bench.py --no-cpu --steps 16"
-run merged 300 $B --semantics voxblox --method merged --parity-steps 1
-run vb_simple 300 $B --semantics voxblox --parity-steps 1
-run vb_const 300 $B --semantics voxblox --const-weight --parity-steps 1
-for n in 2 4 8; do
-  run reh_index_n$n 300 $B --rank-rehearsal $n --sector-rule index
-  run reh_world_n$n 300 $B --rank-rehearsal $n --sector-rule world
+P="bench.py --steps 16 --cpu-seconds 2 --parity-steps 1"  # with the in-bench parity check
+run merged 300 $P --semantics voxblox --method merged
+run vb_simple 300 $P --semantics voxblox
+run vb_const 300 $P --semantics voxblox --const-weight
+for nr in 2 4 8; do
+  run reh_index_n$nr 300 $B --rank-rehearsal $nr --sector-rule index
+  run reh_world_n$nr 300 $B --rank-rehearsal $nr --sector-rule world
 done
 run border_bytes 600 profiles/border_bytes.py --scans 128 640 --n 2 4 8
 run live_index_s4 300 profiles/host_path.py --sectors 4 --sector-rule index
