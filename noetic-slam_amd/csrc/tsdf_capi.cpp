@@ -1719,6 +1719,107 @@ int tsdf_integrate_sectors_origin(tsdf_ctx* const* ctxs, uint32_t n_ctx, const v
 
 }  // extern "C"
 
+// tsdf_integrate_sectors under TSDF_SECTOR_RULE_INDEX: context k receives points [lo_k, hi_k)
+// (idx_share).  The packing is one parallel pass on the staging threads of ALL the contexts (each
+// part of the cloud to the pinned buffers of the contexts whose shares it covers), then per
+// context one H2D copy of its share and the scan joins its pending batch.
+static int sectors_shares(tsdf_ctx* const* ctxs, uint32_t n_ctx, const void* pts, uint64_t n,
+                          uint32_t point_step, uint32_t xyz_offset, int32_t xyz_is_f64,
+                          const ScanPose& P) {
+    tsdf_ctx* c0 = ctxs[0];
+    HostTiming& ht = c0->split_ht;
+    ht.start();
+    uint64_t lo[TSDF_MAX_WORLD + 1];
+    for (uint32_t k = 0; k < n_ctx; k++) {
+        uint64_t l, h;
+        idx_share(ctxs[k], n, l, h);
+        lo[k] = l;
+        if (h - l > ctxs[k]->max_points)
+            return fail(c0, TSDF_EINVAL, "share of %llu points exceeds max_points of context %u",
+                        (unsigned long long)(h - l), k);
+    }
+    lo[n_ctx] = n;
+    float* h[TSDF_MAX_WORLD];
+    int hb[TSDF_MAX_WORLD];
+    for (uint32_t k = 0; k < n_ctx; k++) {  // room in every pending batch, a free pinned buffer
+        tsdf_ctx* c = ctxs[k];
+        HIPCHK(c, hipSetDevice(c->device));
+        const int rc = pend_room(c, lo[k + 1] - lo[k]);
+        if (rc) {
+            if (k) c0->err = c->err;
+            return rc;
+        }
+        hb[k] = c->stage_cur;
+        c->stage_cur ^= 1;
+        HIPCHK(c, hipEventSynchronize(c->stage_done[hb[k]]));
+        h[k] = c->h_stage[hb[k]];
+    }
+    ht.lap(0);
+    const char* base = static_cast<const char*>(pts);
+    auto pack = [&](uint64_t i0, uint64_t i1) {
+        uint32_t k = 0;
+        while (k + 1 < n_ctx && lo[k + 1] <= i0) k++;
+        for (uint64_t i = i0; i < i1;) {
+            const uint64_t e = std::min(i1, lo[k + 1]);  // this context's part of [i0, i1)
+            float* dst = h[k] + 3 * (i - lo[k]);
+            if (!xyz_is_f64 && point_step == 12 && xyz_offset == 0) {
+                std::memcpy(dst, base + 12 * i, (e - i) * 12);
+            } else {
+                for (uint64_t j = i; j < e; j++, dst += 3) {
+                    const char* q = base + j * point_step + xyz_offset;
+                    if (xyz_is_f64) {
+                        double d[3];
+                        std::memcpy(d, q, sizeof d);
+                        dst[0] = (float)d[0];
+                        dst[1] = (float)d[1];
+                        dst[2] = (float)d[2];
+                    } else {
+                        std::memcpy(dst, q, 12);
+                    }
+                }
+            }
+            i = e;
+            k++;
+        }
+    };
+    int pbase[TSDF_MAX_WORLD + 1];
+    pbase[0] = 0;
+    for (uint32_t k = 0; k < n_ctx; k++)
+        pbase[k + 1] = pbase[k] + (ctxs[k]->pack ? ctxs[k]->pack->parts() - (k ? 1 : 0) : (k ? 0 : 1));
+    const int parts = n >= (1u << 15) ? pbase[n_ctx] : 1;
+    auto part = [&](int q) { pack(n * (uint64_t)q / parts, n * (uint64_t)(q + 1) / parts); };
+    if (parts == 1) {
+        part(0);
+    } else {
+        for (uint32_t k = 1; k < n_ctx; k++)
+            if (ctxs[k]->pack) ctxs[k]->pack->start(part, pbase[k] - 1);
+        if (c0->pack) c0->pack->run(part);
+        else part(0);
+        for (uint32_t k = 1; k < n_ctx; k++)
+            if (ctxs[k]->pack) ctxs[k]->pack->wait();
+    }
+    ht.lap(1);
+    for (uint32_t k = 0; k < n_ctx; k++) {
+        tsdf_ctx* c = ctxs[k];
+        const uint64_t nk = lo[k + 1] - lo[k];
+        HIPCHK(c, hipSetDevice(c->device));
+        int rc = pend_stage_buffer(c);
+        if (!rc && nk)
+            HIPCHK(c, hipMemcpyAsync(c->stage2[c->pend_stage] + 3 * (uint64_t)c->pend.s[c->pend.n_scans].off,
+                                     h[k], nk * 12, hipMemcpyHostToDevice, c->stream));
+        if (!rc) HIPCHK(c, hipEventRecord(c->stage_done[hb[k]], c->stream));
+        if (!rc) rc = pend_push(c, nk, P);
+        if (rc) {
+            if (k) c0->err = c->err;
+            return rc;
+        }
+    }
+    HIPCHK(c0, hipSetDevice(c0->device));
+    ht.lap(3);
+    ht.n++;
+    return TSDF_OK;
+}
+
 static int sectors_impl(tsdf_ctx* const* ctxs, uint32_t n_ctx, const void* pts, uint64_t n,
                         uint32_t point_step, uint32_t xyz_offset, int32_t xyz_is_f64,
                         const ScanPose& P) {
@@ -1742,23 +1843,11 @@ static int sectors_impl(tsdf_ctx* const* ctxs, uint32_t n_ctx, const void* pts, 
                         n_ctx);
     }
     // TSDF_SECTOR_RULE_INDEX (ABI v10): context k's share is a contiguous index range of the
-    // cloud, so it packs and copies only that range over its own PCIe link -- one pass over the
-    // cloud in total, no classification, no fan-out (a Merged context bundles its share's points)
-    if (n_ctx > 1 && c0->idx_rule) {
-        HostTiming& hti = c0->split_ht;
-        hti.start();
-        hti.lap(0);
-        for (uint32_t k = 0; k < n_ctx; k++) {
-            const int rc = integrate_impl(ctxs[k], pts, n, point_step, xyz_offset, xyz_is_f64, P);
-            if (rc) {
-                if (k) c0->err = ctxs[k]->err;
-                return rc;
-            }
-        }
-        hti.lap(3);
-        hti.n++;
-        return TSDF_OK;
-    }
+    // cloud: every context's staging threads pack the whole cloud once, each point into its own
+    // context's pinned buffer, then each context copies only its share over its own PCIe link --
+    // one pass over the cloud, no classification, no fan-out (a Merged context bundles its share)
+    if (n_ctx > 1 && c0->idx_rule) return sectors_shares(ctxs, n_ctx, pts, n, point_step,
+                                                         xyz_offset, xyz_is_f64, P);
     for (uint32_t k = 0; k < n_ctx; k++) {
         const tsdf_ctx* c = ctxs[k];
         if (n > c->max_points)  // a context may receive every point
