@@ -1782,20 +1782,28 @@ static int sectors_shares(tsdf_ctx* const* ctxs, uint32_t n_ctx, const void* pts
             k++;
         }
     };
+    // the staging pools of the first few contexts only: every pool's workers spin ~100 us after a
+    // job, so N pools' workers (4 N threads) would crowd the calling thread off a 16-CPU share
+    // (TSDF_SECTOR_PACK_POOLS, default 2: 8 threads)
+    static const uint32_t max_pools = [] {
+        const char* e = std::getenv("TSDF_SECTOR_PACK_POOLS");
+        return e ? (uint32_t)std::max(1, std::atoi(e)) : 2u;
+    }();
+    const uint32_t np = std::min(n_ctx, max_pools);
     int pbase[TSDF_MAX_WORLD + 1];
     pbase[0] = 0;
-    for (uint32_t k = 0; k < n_ctx; k++)
+    for (uint32_t k = 0; k < np; k++)
         pbase[k + 1] = pbase[k] + (ctxs[k]->pack ? ctxs[k]->pack->parts() - (k ? 1 : 0) : (k ? 0 : 1));
-    const int parts = n >= (1u << 15) ? pbase[n_ctx] : 1;
+    const int parts = n >= (1u << 15) ? pbase[np] : 1;
     auto part = [&](int q) { pack(n * (uint64_t)q / parts, n * (uint64_t)(q + 1) / parts); };
     if (parts == 1) {
         part(0);
     } else {
-        for (uint32_t k = 1; k < n_ctx; k++)
+        for (uint32_t k = 1; k < np; k++)
             if (ctxs[k]->pack) ctxs[k]->pack->start(part, pbase[k] - 1);
         if (c0->pack) c0->pack->run(part);
         else part(0);
-        for (uint32_t k = 1; k < n_ctx; k++)
+        for (uint32_t k = 1; k < np; k++)
             if (ctxs[k]->pack) ctxs[k]->pack->wait();
     }
     ht.lap(1);

@@ -1,10 +1,11 @@
 #!/bin/bash
-# rocprofv3 kernel stats of the merged bench (the pre-pass kernels' times), into gpurun_out/r06/<tag>/
+# rocprofv3 kernel stats of one bench configuration (default: the merged pre-pass), into
+# gpurun_out/r06/<tag>/; only the *_stats.csv files are kept (the traces exceed gpurun's pull cap).
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r06/$1
+O=gpurun_out/r06/$1; shift
+ARGS=${@:---semantics voxblox --method merged}
 mkdir -p $O
-cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o merged -- python3 bench.py --semantics voxblox --method merged --no-cpu --steps 8 --warmup 2 --no-profile > $O/merged_prof.json 2> $O/merged_prof.err || { tail -5 $O/merged_prof.err; exit 1; }
-find $O/prof -name "*kernel_stats.csv" | head -3
-for f in $(find $O/prof -name "*kernel_stats.csv"); do head -12 $f | cut -d, -f1-8; done
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py $ARGS --no-cpu --steps 8 --warmup 2 --no-profile > $O/bench.json 2> $O/bench.err || { tail -5 $O/bench.err; exit 1; }
+find $O/prof -type f ! -name "*stats.csv" -delete
+for f in $(find $O/prof -name "*kernel_stats.csv"); do head -14 $f | cut -d, -f1-8; done
