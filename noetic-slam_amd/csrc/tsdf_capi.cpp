@@ -1301,7 +1301,7 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
             HIPCHK(c, hipMemset(M.tab, 0, (size_t)32 << M.tab_bits));  // every record empty
             HIPCHK(c, hipMalloc(&M.grp, (size_t)32 << M.grp_bits));
             HIPCHK(c, hipMemset(M.grp, 0, (size_t)32 << M.grp_bits));
-            HIPCHK(c, hipMalloc(&M.slot, n * 4));
+            HIPCHK(c, hipMalloc(&M.slot, (n + 4) * 4));  // (+4: k_mg_lead reads 16-B groups)
             HIPCHK(c, hipMalloc(&M.gid, n * 4));
             HIPCHK(c, hipMalloc(&M.next, n * 4));
             HIPCHK(c, hipMalloc(&M.xyz_out, n * 12));

@@ -16,11 +16,11 @@
 //                of the chain head; `next` per point)
 //   k_mg_lead    one lane per point: every point frees its key-table record for the next batch; a
 //                group's first point merges the group's members in cloud order and writes the
-//                bundle's ray into its own slot, then frees the group record.  It finds the members
-//                either by walking the scan's slots forward from itself (cost: the span from first
-//                to last member) or, for a few members spread far apart -- a voxel on the seam of
-//                the spin, whose members sit at both ends of the cloud -- by repeated selection of
-//                the next index from the chain (cost: members^2)
+//                bundle's ray into its own slot, then frees the group record.  A group of at most
+//                MG_SMALL members (nearly all) is read from its chain into registers and sorted
+//                there -- its members may lie anywhere in the cloud (a voxel on the seam of the
+//                spin has members at both ends); a larger one (a near-range blob) walks the scan's
+//                slots from its first member to its last
 // Scans t and t + 64 of one batch share a mask bit: two one-point bundles of such scans in one voxel
 // both take the group path, which is exact too (each group merges its own scan's points).
 // The walk kernels then run unchanged over the batch's slots (RayConst::ray_w), so block counts,
@@ -41,6 +41,7 @@ constexpr int MG_VOX_LIM = 1 << 20;     // voxel indices beyond drop the point (
 // an empty key-table slot: no key is 0 (a kept voxel's biased axes lie in [1, 2^21 - 1])
 constexpr uint64_t MG_EMPTY = 0ull;
 constexpr uint32_t MG_NONE = ~0u;  // a dropped point's slot / a one-point bundle's group
+constexpr int MG_SMALL = 8;        // a group of up to this many members merges from its chain
 
 // One point's bundle facts, shared by the three kernels (the oracle's mg_bundle, op for op):
 // validity, the clearing flag, the bundle key, p - o and getVoxelWeight.
@@ -244,29 +245,46 @@ __global__ __launch_bounds__(MG_THREADS) void k_mg_lead(const float* __restrict_
             clearing = p.clearing;  // (the slot's key carries it: the same for every member)
             mg_step(p, clearing, mx, my, mz, mw);
         };
-        const uint32_t span = last - i + 1u;
-        if (span <= 4096u || (uint64_t)cnt * cnt > span / 8u) {
-            // forward over the scan's slots (sequential 4-B reads)
-            uint32_t found = 0;
-            for (uint32_t j = i; j <= last && j < hi && found < cnt; j++) {
-                if (M.slot[j] != h) continue;
-                merge_at(j);
-                found++;
+        if (cnt <= MG_SMALL) {
+            // a small group (nearly all of them: two or three points): its chain, loaded once into
+            // registers (a static index per slot: no scratch), sorted by a compare-exchange
+            // network, merged in cloud order; cnt dependent loads, wherever the members lie (a
+            // voxel on the seam of the spin has members at both ends of the cloud)
+            uint32_t m[MG_SMALL];
+            uint32_t e = head;
+#pragma unroll
+            for (int q = 0; q < MG_SMALL; q++) {
+                const bool on = e != 0u;
+                m[q] = on ? e - 1u : ~0u;
+                e = on ? M.next[e - 1u] : 0u;
             }
-        } else {
-            // few members far apart: the next member is the smallest chain index above the
-            // current one (the chain holds exactly the group's members)
-            uint32_t cur = i;
-            merge_at(cur);
-            for (uint32_t k = 1; k < cnt; k++) {
-                uint32_t best = ~0u;
-                for (uint32_t e = head; e != 0u; e = M.next[e - 1u]) {
-                    const uint32_t j = e - 1u;
-                    best = j > cur && j < best ? j : best;
+#pragma unroll
+            for (int a = 0; a < MG_SMALL; a++)  // odd-even transposition sort (MG_SMALL rounds)
+#pragma unroll
+                for (int q = a & 1; q + 1 < MG_SMALL; q += 2) {
+                    const uint32_t lo_ = min(m[q], m[q + 1]), hi_ = max(m[q], m[q + 1]);
+                    m[q] = lo_;
+                    m[q + 1] = hi_;
                 }
-                if (best == ~0u) break;  // (cannot happen: cnt members are chained)
-                cur = best;
-                merge_at(cur);
+#pragma unroll
+            for (int q = 0; q < MG_SMALL; q++)
+                if (m[q] != ~0u) merge_at(m[q]);
+        } else {
+            // a large group (a near-range blob): forward over the scan's slots from the first
+            // member to the last, four slots per 16-B load
+            uint32_t found = 0;
+            const uint32_t end = min(last + 1u, hi);
+            for (uint32_t j0 = i & ~3u; j0 < end && found < cnt; j0 += 4u) {
+                const uint4 q4 = *reinterpret_cast<const uint4*>(M.slot + j0);
+                const uint32_t sl[4] = {q4.x, q4.y, q4.z, q4.w};
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const uint32_t j = j0 + (uint32_t)u;
+                    if (j >= i && j < end && sl[u] == h) {
+                        merge_at(j);
+                        found++;
+                    }
+                }
             }
         }
         mg_out(M, i, s, clearing, mx, my, mz, mw);
