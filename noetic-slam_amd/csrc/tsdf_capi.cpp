@@ -1296,11 +1296,11 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
             MgBufs& M = c->mg[q];
             const uint64_t n = c->batch_points;
             M.cap = n;
-            M.tab_bits = M.grp_bits = mg_tab_bits(n);  // >= 1.25 n records each
-            HIPCHK(c, hipMalloc(&M.tab, (size_t)32 << M.tab_bits));
-            HIPCHK(c, hipMemset(M.tab, 0, (size_t)32 << M.tab_bits));  // every record empty
-            HIPCHK(c, hipMalloc(&M.grp, (size_t)32 << M.grp_bits));
-            HIPCHK(c, hipMemset(M.grp, 0, (size_t)32 << M.grp_bits));
+            M.tab_n = M.grp_n = mg_table_records(n);  // >= 1.25 n records each
+            HIPCHK(c, hipMalloc(&M.tab, (size_t)24 * M.tab_n));
+            HIPCHK(c, hipMemset(M.tab, 0, (size_t)24 * M.tab_n));  // every record empty
+            HIPCHK(c, hipMalloc(&M.grp, (size_t)32 * M.grp_n));
+            HIPCHK(c, hipMemset(M.grp, 0, (size_t)32 * M.grp_n));
             HIPCHK(c, hipMalloc(&M.slot, (n + 4) * 4));  // (+4: k_mg_lead reads 16-B groups)
             HIPCHK(c, hipMalloc(&M.gid, n * 4));
             HIPCHK(c, hipMalloc(&M.next, n * 4));

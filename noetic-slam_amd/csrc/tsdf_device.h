@@ -414,15 +414,15 @@ struct MgBufs {
     float* xyz_out = nullptr;  // per point slot: the bundle ray's end point (NaN: no ray)
     float* w_out = nullptr;    // its weight (negative: clearing)
     uint64_t cap = 0;          // points
-    // bundle key -> record {key, seen mask, dup mask, pad} (4 u64): open addressing over
-    // 2^tab_bits >= 1.25 cap records, all zero between batches (k_mg_lead frees what it used)
+    // bundle key -> record {key, seen mask, dup mask} (3 u64): open addressing over tab_n >= 1.25
+    // cap records, all zero between batches (a fill after each pre-pass)
     uint64_t* tab = nullptr;
     // (slot, scan) -> record {key, (~first member) | members << 32, last member | chain head << 32,
-    // pad} (4 u64), the same size and life
+    // pad} (4 u64) over grp_n records, zero between batches (each group's leader frees its record)
     uint64_t* grp = nullptr;
-    uint32_t tab_bits = 0, grp_bits = 0;
+    uint32_t tab_n = 0, grp_n = 0;
 };
-uint32_t mg_tab_bits(uint64_t n_points);
+uint32_t mg_table_records(uint64_t n_points);
 hipError_t launch_mg_prepass(const float* d_xyz, const BatchRef& B, uint32_t n_blocks,
                              uint64_t n_points, const RayConst& R, MgBufs& M, uint32_t* ovf,
                              hipStream_t st);

@@ -7,14 +7,15 @@
 // batch-wide key table whose records carry per-scan bitmasks, merges only those, in place.
 //   k_mg_keys    one lane per point (k_count's block layout: RPB points of one scan per block):
 //                isPointValid and the bundle key (clearing bit | the point's voxel, 21 biased bits per
-//                axis) inserted into the table (its slot h is the point's `slot`), then
-//                seen[h] |= bit(scan) -- a second point of the scan in h also sets dup[h] |= bit(scan)
+//                axis) inserted into the table of {key, seen, dup} records (its record h is the
+//                point's `slot`), then seen[h] |= bit(scan) -- a second point of the scan in h also
+//                sets dup[h] |= bit(scan)
 //   k_mg_single  one lane per point: a point whose (slot, scan) is not dup is a one-point bundle and
 //                writes its ray at once (the merge's arithmetic for one point, bit for bit); a dup
 //                point joins its (slot, scan) group in a second table: the member count, the first
 //                and last members (atomic max of ~index / index) and a member chain (atomic exchange
 //                of the chain head; `next` per point)
-//   k_mg_lead    one lane per point: every point frees its key-table record for the next batch; a
+//   k_mg_lead    one lane per point (the key table is emptied by a fill after k_mg_single): a
 //                group's first point merges the group's members in cloud order and writes the
 //                bundle's ray into its own slot, then frees the group record.  A group of at most
 //                MG_SMALL members (nearly all) is read from its chain into registers and sorted
@@ -81,6 +82,13 @@ __device__ __forceinline__ MgPoint mg_point(const RayConst& R, float px, float p
     return m;
 }
 
+// A key's home slot in a table of n records (n need not be a power of two: the tables are sized
+// 1.25 x the batch's points, so the key table of a 64-scan batch fits the 256 MiB MALL)
+__device__ __forceinline__ uint32_t mg_home(uint64_t key, uint32_t n) {
+    return (uint32_t)(((mix64(key) >> 32) * (uint64_t)n) >> 32);
+}
+__device__ __forceinline__ uint32_t mg_next(uint32_t q, uint32_t n) { return q + 1u == n ? 0u : q + 1u; }
+
 // integrateVoxel's merge step (kEpsilon; a clearing bundle keeps its first kept point only)
 __device__ __forceinline__ void mg_step(const MgPoint& p, bool clearing, float& mx, float& my,
                                         float& mz, float& mw) {
@@ -117,7 +125,6 @@ __global__ __launch_bounds__(MG_THREADS) void k_mg_keys(const float* __restrict_
     const bool axis = s.zx != 0.0f || s.zy != 0.0f || s.zz != 0.0f;
     const float* __restrict__ xs = xyz + 3 * (size_t)s.xoff;  // the input (ABI v10 xoff)
     const uint64_t bit = 1ull << (t & 63u);
-    const uint64_t mask = (1ull << M.tab_bits) - 1ull;
     for (uint32_t i = r0 + threadIdx.x; i < r1; i += MG_THREADS) {
         const MgPoint p = mg_point(R, xs[3 * (size_t)i], xs[3 * (size_t)i + 1],
                                    xs[3 * (size_t)i + 2], s.ox, s.oy, s.oz, s.zx, s.zy, s.zz, axis);
@@ -125,19 +132,19 @@ __global__ __launch_bounds__(MG_THREADS) void k_mg_keys(const float* __restrict_
         if (p.ok) {
             // the table holds >= 1.25 x the batch's points, so a free slot exists; the probe count
             // is capped all the same (an exhausted probe drops the point and raises OVF_MG)
-            uint64_t q = mix64(p.key) & mask;
-            for (uint64_t n = 0; n <= mask; n++, q = (q + 1) & mask) {
-                const uint64_t k = M.tab[4 * q];
+            uint32_t q = mg_home(p.key, M.tab_n);
+            for (uint32_t n = 0; n < M.tab_n; n++, q = mg_next(q, M.tab_n)) {
+                const uint64_t k = M.tab[3 * (size_t)q];
                 if (k == p.key) {
-                    h = (uint32_t)q;
+                    h = q;
                     break;
                 }
                 if (k == MG_EMPTY) {
-                    const unsigned long long old = atomicCAS((unsigned long long*)&M.tab[4 * q],
+                    const unsigned long long old = atomicCAS((unsigned long long*)&M.tab[3 * (size_t)q],
                                                              (unsigned long long)MG_EMPTY,
                                                              (unsigned long long)p.key);
                     if (old == MG_EMPTY || old == p.key) {
-                        h = (uint32_t)q;
+                        h = q;
                         break;
                     }
                 }
@@ -145,8 +152,8 @@ __global__ __launch_bounds__(MG_THREADS) void k_mg_keys(const float* __restrict_
             if (h == MG_NONE) {
                 atomicOr(ovf, OVF_MG);
             } else {
-                const unsigned long long old = atomicOr((unsigned long long*)&M.tab[4 * (size_t)h + 1], bit);
-                if (old & bit) atomicOr((unsigned long long*)&M.tab[4 * (size_t)h + 2], bit);
+                const unsigned long long old = atomicOr((unsigned long long*)&M.tab[3 * (size_t)h + 1], bit);
+                if (old & bit) atomicOr((unsigned long long*)&M.tab[3 * (size_t)h + 2], bit);
             }
         }
         M.slot[i] = h;
@@ -160,12 +167,11 @@ __global__ __launch_bounds__(MG_THREADS) void k_mg_single(const float* __restric
     const ScanRec s = D.s[t];
     const bool axis = s.zx != 0.0f || s.zy != 0.0f || s.zz != 0.0f;
     const float* __restrict__ xs = xyz + 3 * (size_t)s.xoff;
-    const uint64_t gmask = (1ull << M.grp_bits) - 1ull;
     for (uint32_t i = r0 + threadIdx.x; i < r1; i += MG_THREADS) {
         const uint32_t h = M.slot[i];
         uint32_t g = MG_NONE;
         bool single = false;
-        if (h != MG_NONE) single = ((M.tab[4 * (size_t)h + 2] >> (t & 63u)) & 1ull) == 0ull;
+        if (h != MG_NONE) single = ((M.tab[3 * (size_t)h + 2] >> (t & 63u)) & 1ull) == 0ull;
         if (single) {  // a one-point bundle: its ray now
             const MgPoint p = mg_point(R, xs[3 * (size_t)i], xs[3 * (size_t)i + 1],
                                        xs[3 * (size_t)i + 2], s.ox, s.oy, s.oz, s.zx, s.zy, s.zz,
@@ -177,19 +183,19 @@ __global__ __launch_bounds__(MG_THREADS) void k_mg_single(const float* __restric
             mg_out(M, i, s, false, 0.0f, 0.0f, 0.0f, 0.0f);  // no ray here (a group's leader's later)
             if (h != MG_NONE) {  // join the (slot, scan) group
                 const uint64_t key = ((uint64_t)h << 16) | (uint64_t)(t + 1u);  // never 0
-                uint64_t q = mix64(key) & gmask;
-                for (uint64_t n = 0; n <= gmask; n++, q = (q + 1) & gmask) {
-                    const uint64_t k = M.grp[4 * q];
+                uint32_t q = mg_home(key, M.grp_n);
+                for (uint32_t n = 0; n < M.grp_n; n++, q = mg_next(q, M.grp_n)) {
+                    const uint64_t k = M.grp[4 * (size_t)q];
                     if (k == key) {
-                        g = (uint32_t)q;
+                        g = q;
                         break;
                     }
                     if (k == MG_EMPTY) {
-                        const unsigned long long old = atomicCAS((unsigned long long*)&M.grp[4 * q],
+                        const unsigned long long old = atomicCAS((unsigned long long*)&M.grp[4 * (size_t)q],
                                                                  (unsigned long long)MG_EMPTY,
                                                                  (unsigned long long)key);
                         if (old == MG_EMPTY || old == key) {
-                            g = (uint32_t)q;
+                            g = q;
                             break;
                         }
                     }
@@ -218,16 +224,11 @@ __global__ __launch_bounds__(MG_THREADS) void k_mg_lead(const float* __restrict_
     const bool axis = s.zx != 0.0f || s.zy != 0.0f || s.zz != 0.0f;
     const float* __restrict__ xs = xyz + 3 * (size_t)s.xoff;
     for (uint32_t i = r0 + threadIdx.x; i < r1; i += MG_THREADS) {
-        const uint32_t h = M.slot[i];
-        if (h == MG_NONE) continue;
-        // every read of this record happened in k_mg_keys / k_mg_single: free it for the next batch
-        // (idempotent: every point of the slot writes the same zeros)
-        *reinterpret_cast<ulonglong2*>(&M.tab[4 * (size_t)h]) = make_ulonglong2(0ull, 0ull);
-        M.tab[4 * (size_t)h + 2] = 0ull;
         const uint32_t g = M.gid[i];
         if (g == MG_NONE) continue;
         const uint64_t v = M.grp[4 * (size_t)g + 1];
         if (~(uint32_t)v != i) continue;  // not the group's first point (or already freed: 0)
+        const uint32_t h = M.slot[i];
         const uint32_t cnt = (uint32_t)(v >> 32);
         const uint64_t v2 = M.grp[4 * (size_t)g + 2];
         const uint32_t last = (uint32_t)v2, head = (uint32_t)(v2 >> 32);
@@ -293,10 +294,8 @@ __global__ __launch_bounds__(MG_THREADS) void k_mg_lead(const float* __restrict_
 
 }  // namespace
 
-uint32_t mg_tab_bits(uint64_t n_points) {
-    uint32_t b = 4;
-    while ((1ull << b) < n_points + n_points / 4) b++;  // >= 1.25 x the batch's points
-    return b;
+uint32_t mg_table_records(uint64_t n_points) {
+    return (uint32_t)std::min<uint64_t>(n_points + n_points / 4 + 64, 0xFFFFFFF0ull);  // >= 1.25 x
 }
 
 hipError_t launch_mg_prepass(const float* d_xyz, const BatchRef& B, uint32_t n_blocks,
@@ -307,12 +306,15 @@ hipError_t launch_mg_prepass(const float* d_xyz, const BatchRef& B, uint32_t n_b
     k_mg_keys<<<n_blocks, MG_THREADS, 0, st>>>(d_xyz, B, R, M, ovf);
     k_mg_single<<<n_blocks, MG_THREADS, 0, st>>>(d_xyz, B, R, M, ovf);
     k_mg_lead<<<n_blocks, MG_THREADS, 0, st>>>(d_xyz, B, R, M);
+    // the key table's last readers ran (k_mg_single): empty it for the next batch in one streaming
+    // fill (24 B a record; clearing each point's record from k_mg_lead cost 0.4 ms of scattered
+    // partial-line stores per 64-scan batch)
+    (void)hipMemsetAsync(M.tab, 0, (size_t)24 * M.tab_n, st);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
-        // a pre-pass cut short may leave keys and groups in the tables: empty them, so the next
-        // batch starts from empty tables
-        (void)hipMemsetAsync(M.tab, 0, (size_t)32 << M.tab_bits, st);
-        (void)hipMemsetAsync(M.grp, 0, (size_t)32 << M.grp_bits, st);
+        // a pre-pass cut short may leave groups in the group table: empty it too, so the next batch
+        // starts from empty tables
+        (void)hipMemsetAsync(M.grp, 0, (size_t)32 * M.grp_n, st);
     }
     return e;
 }
