@@ -292,10 +292,19 @@ __global__ __launch_bounds__(MG_THREADS) void k_mg_lead(const float* __restrict_
     }
 }
 
+// Empties the key table for the next batch: one grid-stride streaming fill of 16-B stores (the
+// table is 24 B x a multiple of 64 records)
+__global__ __launch_bounds__(256) void k_mg_clear(uint4* __restrict__ p, uint64_t n16) {
+    for (uint64_t q = blockIdx.x * 256ull + threadIdx.x; q < n16; q += (uint64_t)gridDim.x * 256ull)
+        p[q] = make_uint4(0u, 0u, 0u, 0u);
+}
+
 }  // namespace
 
 uint32_t mg_table_records(uint64_t n_points) {
-    return (uint32_t)std::min<uint64_t>(n_points + n_points / 4 + 64, 0xFFFFFFF0ull);  // >= 1.25 x
+    // >= 1.25 x the batch's points, a multiple of 64 records (k_mg_clear's 16-B stores)
+    const uint64_t n = (n_points + n_points / 4 + 127) & ~63ull;
+    return (uint32_t)std::min<uint64_t>(n, 0xFFFFFFC0ull);
 }
 
 hipError_t launch_mg_prepass(const float* d_xyz, const BatchRef& B, uint32_t n_blocks,
@@ -309,7 +318,9 @@ hipError_t launch_mg_prepass(const float* d_xyz, const BatchRef& B, uint32_t n_b
     // the key table's last readers ran (k_mg_single): empty it for the next batch in one streaming
     // fill (24 B a record; clearing each point's record from k_mg_lead cost 0.4 ms of scattered
     // partial-line stores per 64-scan batch)
-    (void)hipMemsetAsync(M.tab, 0, (size_t)24 * M.tab_n, st);
+    const uint64_t n16 = (uint64_t)24 * M.tab_n / 16;
+    k_mg_clear<<<(uint32_t)std::min<uint64_t>((n16 + 255) / 256, 8192), 256, 0, st>>>(
+        reinterpret_cast<uint4*>(M.tab), n16);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         // a pre-pass cut short may leave groups in the group table: empty it too, so the next batch
