@@ -1133,8 +1133,8 @@ void tsdf_destroy(tsdf_ctx* c) {
         if (c->h_stage[i]) (void)hipHostFree(c->h_stage[i]);
         if (c->stage_done[i]) (void)hipEventDestroy(c->stage_done[i]);
         MgBufs& M = c->mg[i];
-        for (void* q : {(void*)M.slot, (void*)M.gid, (void*)M.next, (void*)M.xyz_out,
-                        (void*)M.w_out, (void*)M.tab, (void*)M.grp})
+        for (void* q : {(void*)M.xyz_out, (void*)M.w_out, (void*)M.ekey, (void*)M.eidx,
+                        (void*)M.bcnt, (void*)M.bst})
             if (q) (void)hipFree(q);
     }
     if (c->bc_ev) (void)hipEventDestroy(c->bc_ev);
@@ -1296,14 +1296,12 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
             MgBufs& M = c->mg[q];
             const uint64_t n = c->batch_points;
             M.cap = n;
-            M.tab_n = M.grp_n = mg_table_records(n);  // >= 1.25 n records each
-            HIPCHK(c, hipMalloc(&M.tab, (size_t)24 * M.tab_n));
-            HIPCHK(c, hipMemset(M.tab, 0, (size_t)24 * M.tab_n));  // every record empty
-            HIPCHK(c, hipMalloc(&M.grp, (size_t)32 * M.grp_n));
-            HIPCHK(c, hipMemset(M.grp, 0, (size_t)32 * M.grp_n));
-            HIPCHK(c, hipMalloc(&M.slot, (n + 4) * 4));  // (+4: k_mg_lead reads 16-B groups)
-            HIPCHK(c, hipMalloc(&M.gid, n * 4));
-            HIPCHK(c, hipMalloc(&M.next, n * 4));
+            M.nb_cap = mg_buckets_max(n);
+            HIPCHK(c, hipMalloc(&M.ekey, n * 8));
+            HIPCHK(c, hipMalloc(&M.eidx, n * 4));
+            HIPCHK(c, hipMalloc(&M.bcnt, (size_t)4 * M.nb_cap));
+            HIPCHK(c, hipMemset(M.bcnt, 0, (size_t)4 * M.nb_cap));  // zero between batches
+            HIPCHK(c, hipMalloc(&M.bst, (size_t)4 * (M.nb_cap + 1)));
             HIPCHK(c, hipMalloc(&M.xyz_out, n * 12));
             HIPCHK(c, hipMalloc(&M.w_out, n * 4));
         }

@@ -408,21 +408,18 @@ hipError_t launch_halo_build(const Table& H, const Pool& HP, const uint32_t* d_t
 // (other slots: NaN point, weight 0), so the batch keeps its ray layout and block counts
 // Merged pre-pass buffers (tsdf_merged.hip), one set per batch parity
 struct MgBufs {
-    uint32_t* slot = nullptr;  // per point: its key's record in tab (~0: dropped point)
-    uint32_t* gid = nullptr;   // per point: its (slot, scan) group in grp (~0: a one-point bundle)
-    uint32_t* next = nullptr;  // per group member: the next chain entry (index + 1; 0 ends it)
     float* xyz_out = nullptr;  // per point slot: the bundle ray's end point (NaN: no ray)
     float* w_out = nullptr;    // its weight (negative: clearing)
     uint64_t cap = 0;          // points
-    // bundle key -> record {key, seen mask, dup mask} (3 u64): open addressing over tab_n >= 1.25
-    // cap records, all zero between batches (a fill after each pre-pass)
-    uint64_t* tab = nullptr;
-    // (slot, scan) -> record {key, (~first member) | members << 32, last member | chain head << 32,
-    // pad} (4 u64) over grp_n records, zero between batches (each group's leader frees its record)
-    uint64_t* grp = nullptr;
-    uint32_t tab_n = 0, grp_n = 0;
+    // the batch's (key, point) entries, grouped by bucket (a hash of the key among its scan's
+    // buckets of ~1024 points): bucket b holds entries [bst[b], bst[b + 1])
+    uint64_t* ekey = nullptr;
+    uint32_t* eidx = nullptr;
+    uint32_t* bcnt = nullptr;  // per bucket: size, then cursor; zero between batches
+    uint32_t* bst = nullptr;   // per bucket: first entry (nb_cap + 1)
+    uint32_t nb_cap = 0;       // buckets
 };
-uint32_t mg_table_records(uint64_t n_points);
+uint32_t mg_buckets_max(uint64_t n_points);
 hipError_t launch_mg_prepass(const float* d_xyz, const BatchRef& B, uint32_t n_blocks,
                              uint64_t n_points, const RayConst& R, MgBufs& M, uint32_t* ovf,
                              hipStream_t st);

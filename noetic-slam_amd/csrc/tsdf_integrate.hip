@@ -49,6 +49,14 @@ typedef unsigned long long MaskT;  // a voxel's scans in the window, one bit per
 typedef uint32_t MaskT;
 #define MASK_POPC(m) __popc(m)
 #endif
+// LDS position of brick voxel l = (z * 8 + y) * 8 + x in k_integrate's per-voxel arrays: each z
+// layer is skewed by one element, so voxels of one (x, y) column (64 elements apart: one bank) that
+// the rays of neighbouring beams hit in the same wave fall in different banks
+#ifndef TSDF_INT_SKEW
+#define TSDF_INT_SKEW 1
+#endif
+#define VOXL(l) ((l) + TSDF_INT_SKEW * ((l) >> 6))
+constexpr int BRICK_VOX_LDS = BRICK_VOX + TSDF_INT_SKEW * (BRICK_VOX / 64);
 constexpr uint32_t INT_MAX_WIN = TSDF_INT_WIN;       // scans per window (mask bits)
 // single walk (FUSED): the register cache holds INT_SPT span records' samples per thread, so a
 // chunk is INT_SCH spans; a window also keeps its spans <= INT_SCH (one chunk per window)
@@ -102,9 +110,9 @@ __global__ __launch_bounds__(INT_THREADS, TSDF_INT_WAVES) void k_integrate(Batch
     __shared__ unsigned long long cA[CAP];  // live cell: sum of trunc(s w * 2^32)
     __shared__ CellB cB[CAP];               // live cell: sample count / sum of trunc(w 2^32)
     const float tau = R.tau;
-    __shared__ MaskT sMask[BRICK_VOX];          // voxel: scans (bit t - t0) observed in the window
-    __shared__ uint32_t sBase[BRICK_VOX];       // voxel: first live cell
-    __shared__ float sS[BRICK_VOX], sW[BRICK_VOX];
+    __shared__ MaskT sMask[BRICK_VOX_LDS];     // voxel: scans (bit t - t0) observed in the window
+    __shared__ uint32_t sBase[BRICK_VOX_LDS];  // voxel: first live cell
+    __shared__ float sS[BRICK_VOX_LDS], sW[BRICK_VOX_LDS];
     __shared__ uint16_t sLive[BRICK_VOX];  // live voxels of the window
     // brick's per-scan sample prefix, double-buffered by brick parity: a wave may still read the
     // previous brick's prefix while another writes the next one
@@ -121,8 +129,8 @@ __global__ __launch_bounds__(INT_THREADS, TSDF_INT_WAVES) void k_integrate(Batch
     // a batch that overflowed (or follows one) is replayed after the host grows the buffers: its
     // field writes are skipped, everything else (cell clean-up) runs
     const bool commit = !(G->retry && (C->ovf || G->failed));
-    sMask[tid] = 0;
-    sMask[tid + 256] = 0;
+    sMask[VOXL(tid)] = 0;
+    sMask[VOXL(tid + 256)] = 0;
     uint32_t nvox = 0, ndirty = 0, par = 0;
 #ifdef TSDF_PHASE_TIMING
     unsigned long long ph[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, t_last = clock64();
@@ -266,10 +274,10 @@ __global__ __launch_bounds__(INT_THREADS, TSDF_INT_WAVES) void k_integrate(Batch
         float* Sg = Pl.sdf + (size_t)(has_slot ? cur.y : 0) * BRICK_VOX;
         float* Wg = Pl.weight + (size_t)(has_slot ? cur.y : 0) * BRICK_VOX;
         // sS / sW of voxels tid, tid + 256: the previous brick's last readers are past a barrier
-        sS[tid] = B.s0;
-        sS[tid + 256] = B.s1;
-        sW[tid] = B.w0;
-        sW[tid + 256] = B.w1;
+        sS[VOXL(tid)] = B.s0;
+        sS[VOXL(tid + 256)] = B.s1;
+        sW[VOXL(tid)] = B.w0;
+        sW[VOXL(tid + 256)] = B.w1;
         uint32_t dirty = 0;  // voxels 2 tid, 2 tid + 1 (bits 0, 1)
         PHASE(0);
         __syncthreads();  // s_cs, sS, sW visible
@@ -309,14 +317,14 @@ __global__ __launch_bounds__(INT_THREADS, TSDF_INT_WAVES) void k_integrate(Batch
 #else
                     if (w < nw)
 #endif
-                        atomicOr(&sMask[c[j].y & 511u], (MaskT)1 << w);
+                        atomicOr(&sMask[VOXL(c[j].y & 511u)], (MaskT)1 << w);
                 }
             }
             __syncthreads();
             PHASE(3);
             // P2: live cells and live voxels (packed block scan: cells | voxels << 16)
             {
-                const MaskT m0 = sMask[2 * tid], m1 = sMask[2 * tid + 1];
+                const MaskT m0 = sMask[VOXL(2 * tid)], m1 = sMask[VOXL(2 * tid + 1)];
                 const uint32_t c0 = MASK_POPC(m0), c1 = MASK_POPC(m1);
                 const uint32_t v0 = m0 ? 1u : 0u, v1 = m1 ? 1u : 0u;
                 dirty |= v0 | (v1 << 1);
@@ -342,8 +350,8 @@ __global__ __launch_bounds__(INT_THREADS, TSDF_INT_WAVES) void k_integrate(Batch
                 }
                 const uint32_t ex = incl - x + off;
                 const uint32_t cb = ex & 0xFFFFu, vb = ex >> 16;
-                sBase[2 * tid] = cb;
-                sBase[2 * tid + 1] = cb + c0;
+                sBase[VOXL(2 * tid)] = cb;
+                sBase[VOXL(2 * tid + 1)] = cb + c0;
                 if (v0) sLive[vb] = (uint16_t)(2 * tid);
                 if (v1) sLive[vb + v0] = (uint16_t)(2 * tid + 1);
                 if (tid == 0) {
@@ -368,7 +376,7 @@ __global__ __launch_bounds__(INT_THREADS, TSDF_INT_WAVES) void k_integrate(Batch
                 for (int j = 0; j < NSLOT; j++) {
                     const uint32_t w = (c[j].y >> 9) - t0;
                     if (w < nw) {
-                        const uint32_t l = c[j].y & 511u;
+                        const uint32_t l = VOXL(c[j].y & 511u);
                         const uint32_t cell = sBase[l] + MASK_POPC(sMask[l] & (((MaskT)1 << w) - 1));
                         const float sv = __uint_as_float(c[j].x);
                         if constexpr (VB) {
@@ -428,7 +436,7 @@ __global__ __launch_bounds__(INT_THREADS, TSDF_INT_WAVES) void k_integrate(Batch
                 const uint32_t nlive = s_nlive;
 #endif
                 for (uint32_t vi = tid; vi < nlive; vi += INT_THREADS) {
-                    const uint32_t l = sLive[vi];
+                    const uint32_t l = VOXL(sLive[vi]);
                     const uint32_t cell = sBase[l];
                     const uint32_t rem = MASK_POPC(sMask[l]);
                     sMask[l] = 0;
@@ -516,12 +524,12 @@ __global__ __launch_bounds__(INT_THREADS, TSDF_INT_WAVES) void k_integrate(Batch
         }
         if (has_slot && commit) {
             if (dirty & 1u) {
-                Sg[2 * tid] = sS[2 * tid];
-                Wg[2 * tid] = sW[2 * tid];
+                Sg[2 * tid] = sS[VOXL(2 * tid)];
+                Wg[2 * tid] = sW[VOXL(2 * tid)];
             }
             if (dirty & 2u) {
-                Sg[2 * tid + 1] = sS[2 * tid + 1];
-                Wg[2 * tid + 1] = sW[2 * tid + 1];
+                Sg[2 * tid + 1] = sS[VOXL(2 * tid + 1)];
+                Wg[2 * tid + 1] = sW[VOXL(2 * tid + 1)];
             }
         }
         ndirty += __popc(dirty);

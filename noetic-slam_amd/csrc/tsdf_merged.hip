@@ -3,30 +3,29 @@
 //
 // A bundle is the points of ONE scan that fall into one (clearing, voxel) key; it casts one ray from
 // the running weighted mean of its points in cloud order.  About 97 % of a scan's points are alone in
-// their bundle, so the pre-pass (round 6) never sorts: it finds the multi-point bundles through a
-// batch-wide key table whose records carry per-scan bitmasks, merges only those, in place.
-//   k_mg_keys    one lane per point (k_count's block layout: RPB points of one scan per block):
-//                isPointValid and the bundle key (clearing bit | the point's voxel, 21 biased bits per
-//                axis) inserted into the table of {key, seen, dup} records (its record h is the
-//                point's `slot`), then seen[h] |= bit(scan) -- a second point of the scan in h also
-//                sets dup[h] |= bit(scan)
-//   k_mg_single  one lane per point: a point whose (slot, scan) is not dup is a one-point bundle and
-//                writes its ray at once (the merge's arithmetic for one point, bit for bit); a dup
-//                point joins its (slot, scan) group in a second table: the member count, the first
-//                and last members (atomic max of ~index / index) and a member chain (atomic exchange
-//                of the chain head; `next` per point)
-//   k_mg_lead    one lane per point (the key table is emptied by a fill after k_mg_single): a
-//                group's first point merges the group's members in cloud order and writes the
-//                bundle's ray into its own slot, then frees the group record.  A group of at most
-//                MG_SMALL members (nearly all) is read from its chain into registers and sorted
-//                there -- its members may lie anywhere in the cloud (a voxel on the seam of the
-//                spin has members at both ends); a larger one (a near-range blob) walks the scan's
-//                slots from its first member to its last
-// Scans t and t + 64 of one batch share a mask bit: two one-point bundles of such scans in one voxel
-// both take the group path, which is exact too (each group merges its own scan's points).
+// their bundle.  The pre-pass (round 6, second form) keeps every random access in LDS: the points are
+// partitioned by a hash of their key into buckets of about 1024 points of one scan, and one
+// workgroup per bucket finds and merges that bucket's multi-point bundles in an LDS table.
+//   k_mg_count    one lane per point (k_count's block layout: RPB points of one scan per block):
+//                 isPointValid, the bundle key (clearing bit | the point's voxel, 21 biased bits per
+//                 axis) and its bucket; the point's ray as a one-point bundle (the merge's arithmetic
+//                 for one point, bit for bit; no ray for a dropped one); bucket sizes through an LDS
+//                 histogram, one global add per (block, bucket)
+//   k_mg_scan     one workgroup: bucket starts (exclusive prefix); the sizes zeroed for use as
+//                 cursors
+//   k_mg_scatter  the same blocks again: (key, point) entries into their buckets (an LDS rank plus
+//                 one returning global add per (block, bucket) for the block's run)
+//   k_mg_group    one workgroup per bucket: its keys into an LDS hash table (a key met again is
+//                 marked); the entries of keys seen more than once (the multi-point bundles' members) gathered in
+//                 LDS as (table slot, point) and sorted, so each bundle's members lie together in
+//                 cloud order; the first member's lane merges them and writes the bundle's ray into
+//                 its slot, the other members write "no ray" over their one-point rays.  A bucket with
+//                 more members than the LDS list holds (a coarse voxel near the sensor) walks each
+//                 bundle's points from its first member to its last instead.
 // The walk kernels then run unchanged over the batch's slots (RayConst::ray_w), so block counts,
 // offsets and the ray layout stay those of the input; empty slots (NaN point, weight 0) leave at the
-// walk's init.
+// walk's init.  Limit: a bucket holds at most MG_TAB distinct keys (about 2 x its expected count;
+// scans of more than ~2^22 points may exceed it): beyond, the batch fails with OVF_MG.
 #include <hip/hip_runtime.h>
 
 #include "tsdf_device.h"
@@ -39,13 +38,31 @@ namespace {
 constexpr int MG_THREADS = 256;
 constexpr float MG_W_CAP = 1048576.0f;  // a bundle's weight cap (the fixed-point sums' headroom)
 constexpr int MG_VOX_LIM = 1 << 20;     // voxel indices beyond drop the point (21-bit key axes)
-// an empty key-table slot: no key is 0 (a kept voxel's biased axes lie in [1, 2^21 - 1])
+// an empty LDS table slot: no key is 0 (a kept voxel's biased axes lie in [1, 2^21 - 1])
 constexpr uint64_t MG_EMPTY = 0ull;
-constexpr uint32_t MG_NONE = ~0u;  // a dropped point's slot / a one-point bundle's group
-constexpr int MG_SMALL = 8;        // a group of up to this many members merges from its chain
+constexpr uint32_t MG_NONE = ~0u;
+constexpr int MG_BSHIFT = 10;       // a scan's buckets hold about 2^MG_BSHIFT points each
+constexpr uint32_t MG_PMAX = 4096;  // buckets per scan at most (the LDS histograms)
+constexpr uint32_t MG_TAB = 2048;   // k_mg_group: distinct keys per bucket (LDS hash table)
+constexpr uint32_t MG_GM = 2048;    // k_mg_group: multi-point bundle members sorted in LDS
+constexpr int MG_PPT = RPB / MG_THREADS;  // points per lane in k_mg_scatter
+static_assert(RPB % MG_THREADS == 0, "k_mg_scatter keeps RPB / MG_THREADS points per lane");
 
-// One point's bundle facts, shared by the three kernels (the oracle's mg_bundle, op for op):
-// validity, the clearing flag, the bundle key, p - o and getVoxelWeight.
+// scan t's bucket count and first bucket: base(t) = off(t) / 2^MG_BSHIFT + t, so that
+// base(t) + buckets(t) <= base(t + 1), and a batch has n_points / 2^MG_BSHIFT + scans buckets
+__device__ __forceinline__ uint32_t mg_buckets(uint32_t n) {
+    return min(max((n + (1u << MG_BSHIFT) - 1u) >> MG_BSHIFT, 1u), MG_PMAX);
+}
+__device__ __forceinline__ uint32_t mg_bucket_base(uint32_t off, uint32_t t) {
+    return (off >> MG_BSHIFT) + t;
+}
+// a key's bucket among P (the hash's high half; the LDS table takes its low half)
+__device__ __forceinline__ uint32_t mg_bucket(uint64_t key, uint32_t P) {
+    return (uint32_t)(((mix64(key) >> 32) * (uint64_t)P) >> 32);
+}
+
+// One point's bundle facts, shared by the kernels (the oracle's mg_bundle, op for op): validity,
+// the clearing flag, the bundle key, p - o and getVoxelWeight.
 struct MgPoint {
     bool ok, clearing;
     uint64_t key;
@@ -82,13 +99,6 @@ __device__ __forceinline__ MgPoint mg_point(const RayConst& R, float px, float p
     return m;
 }
 
-// A key's home slot in a table of n records (n need not be a power of two: the tables are sized
-// 1.25 x the batch's points, so the key table of a 64-scan batch fits the 256 MiB MALL)
-__device__ __forceinline__ uint32_t mg_home(uint64_t key, uint32_t n) {
-    return (uint32_t)(((mix64(key) >> 32) * (uint64_t)n) >> 32);
-}
-__device__ __forceinline__ uint32_t mg_next(uint32_t q, uint32_t n) { return q + 1u == n ? 0u : q + 1u; }
-
 // integrateVoxel's merge step (kEpsilon; a clearing bundle keeps its first kept point only)
 __device__ __forceinline__ void mg_step(const MgPoint& p, bool clearing, float& mx, float& my,
                                         float& mz, float& mw) {
@@ -117,215 +127,350 @@ __device__ __forceinline__ void mg_out(const MgBufs& M, uint32_t i, const ScanRe
     M.w_out[i] = w;
 }
 
-__global__ __launch_bounds__(MG_THREADS) void k_mg_keys(const float* __restrict__ xyz, BatchRef D,
-                                                        RayConst R, MgBufs M, uint32_t* ovf) {
+__global__ __launch_bounds__(MG_THREADS) void k_mg_count(const float* __restrict__ xyz, BatchRef D,
+                                                         RayConst R, MgBufs M) {
+    __shared__ uint32_t hist[MG_PMAX];
     uint32_t t, r0, r1;
     block_range(D, blockIdx.x, t, r0, r1);
     const ScanRec s = D.s[t];
+    const uint32_t P = mg_buckets(D.s[t + 1].off - s.off);
     const bool axis = s.zx != 0.0f || s.zy != 0.0f || s.zz != 0.0f;
     const float* __restrict__ xs = xyz + 3 * (size_t)s.xoff;  // the input (ABI v10 xoff)
-    const uint64_t bit = 1ull << (t & 63u);
-    for (uint32_t i = r0 + threadIdx.x; i < r1; i += MG_THREADS) {
-        const MgPoint p = mg_point(R, xs[3 * (size_t)i], xs[3 * (size_t)i + 1],
-                                   xs[3 * (size_t)i + 2], s.ox, s.oy, s.oz, s.zx, s.zy, s.zz, axis);
-        uint32_t h = MG_NONE;
-        if (p.ok) {
-            // the table holds >= 1.25 x the batch's points, so a free slot exists; the probe count
-            // is capped all the same (an exhausted probe drops the point and raises OVF_MG)
-            uint32_t q = mg_home(p.key, M.tab_n);
-            for (uint32_t n = 0; n < M.tab_n; n++, q = mg_next(q, M.tab_n)) {
-                const uint64_t k = M.tab[3 * (size_t)q];
-                if (k == p.key) {
-                    h = q;
-                    break;
-                }
-                if (k == MG_EMPTY) {
-                    const unsigned long long old = atomicCAS((unsigned long long*)&M.tab[3 * (size_t)q],
-                                                             (unsigned long long)MG_EMPTY,
-                                                             (unsigned long long)p.key);
-                    if (old == MG_EMPTY || old == p.key) {
-                        h = q;
-                        break;
-                    }
-                }
-            }
-            if (h == MG_NONE) {
-                atomicOr(ovf, OVF_MG);
-            } else {
-                const unsigned long long old = atomicOr((unsigned long long*)&M.tab[3 * (size_t)h + 1], bit);
-                if (old & bit) atomicOr((unsigned long long*)&M.tab[3 * (size_t)h + 2], bit);
-            }
-        }
-        M.slot[i] = h;
+    for (uint32_t j = threadIdx.x; j < P; j += MG_THREADS) hist[j] = 0u;
+    __syncthreads();
+    float px[MG_PPT], py[MG_PPT], pz[MG_PPT];  // the block's points, all loads in flight at once
+#pragma unroll
+    for (int k = 0; k < MG_PPT; k++) {
+        const uint32_t i = min(r0 + threadIdx.x + k * MG_THREADS, r1 - 1u);
+        px[k] = xs[3 * (size_t)i];
+        py[k] = xs[3 * (size_t)i + 1];
+        pz[k] = xs[3 * (size_t)i + 2];
     }
+#pragma unroll
+    for (int k = 0; k < MG_PPT; k++) {
+        const uint32_t i = r0 + threadIdx.x + k * MG_THREADS;
+        if (i >= r1) break;
+        const MgPoint p = mg_point(R, px[k], py[k], pz[k], s.ox, s.oy, s.oz, s.zx, s.zy, s.zz, axis);
+        // every point's ray as a one-point bundle (k_mg_group rewrites the multi-point ones)
+        float mx = 0.0f, my = 0.0f, mz = 0.0f, mw = 0.0f;
+        if (p.ok) {
+            mg_step(p, p.clearing, mx, my, mz, mw);
+            atomicAdd(&hist[mg_bucket(p.key, P)], 1u);
+        }
+        mg_out(M, i, s, p.clearing, mx, my, mz, mw);
+    }
+    __syncthreads();
+    const uint32_t base = mg_bucket_base(s.off, t);
+    for (uint32_t j = threadIdx.x; j < P; j += MG_THREADS)
+        if (hist[j]) atomicAdd(&M.bcnt[base + j], hist[j]);
 }
 
-__global__ __launch_bounds__(MG_THREADS) void k_mg_single(const float* __restrict__ xyz, BatchRef D,
-                                                          RayConst R, MgBufs M, uint32_t* ovf) {
+// bucket starts: bst[b] = the sizes of the buckets before b, bst[nb] = the entries; the sizes are
+// zeroed (k_mg_scatter's cursors)
+constexpr int MG_SCAN_THREADS = 1024;
+__global__ __launch_bounds__(MG_SCAN_THREADS) void k_mg_scan(MgBufs M, uint32_t nb) {
+    __shared__ uint32_t s_w[MG_SCAN_THREADS / 64];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+    const uint32_t per = (nb + MG_SCAN_THREADS - 1) / MG_SCAN_THREADS;
+    const uint32_t j0 = min(nb, tid * per), j1 = min(nb, j0 + per);
+    uint32_t sum = 0;
+    for (uint32_t j = j0; j < j1; j++) sum += M.bcnt[j];
+    const uint32_t incl = wave_incl_scan(sum);
+    if (lane == 63u) s_w[wid] = incl;
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < MG_SCAN_THREADS / 64; k++) {
+        off += k < wid ? s_w[k] : 0u;
+        tot += s_w[k];
+    }
+    uint32_t run = incl - sum + off;
+    for (uint32_t j = j0; j < j1; j++) {
+        const uint32_t c = M.bcnt[j];
+        M.bst[j] = run;
+        M.bcnt[j] = 0u;
+        run += c;
+    }
+    if (tid == 0) M.bst[nb] = tot;
+}
+
+__global__ __launch_bounds__(MG_THREADS) void k_mg_scatter(const float* __restrict__ xyz, BatchRef D,
+                                                           RayConst R, MgBufs M) {
+    __shared__ uint32_t hist[MG_PMAX];
     uint32_t t, r0, r1;
     block_range(D, blockIdx.x, t, r0, r1);
     const ScanRec s = D.s[t];
+    const uint32_t P = mg_buckets(D.s[t + 1].off - s.off);
+    const float* __restrict__ xs = xyz + 3 * (size_t)s.xoff;
+    for (uint32_t j = threadIdx.x; j < P; j += MG_THREADS) hist[j] = 0u;
+    __syncthreads();
+    uint64_t key[MG_PPT];
+    uint32_t bk[MG_PPT], rk[MG_PPT];
+    float px[MG_PPT], py[MG_PPT], pz[MG_PPT];  // all loads in flight at once
+#pragma unroll
+    for (int k = 0; k < MG_PPT; k++) {
+        const uint32_t i = min(r0 + threadIdx.x + k * MG_THREADS, r1 - 1u);
+        px[k] = xs[3 * (size_t)i];
+        py[k] = xs[3 * (size_t)i + 1];
+        pz[k] = xs[3 * (size_t)i + 2];
+    }
+#pragma unroll
+    for (int k = 0; k < MG_PPT; k++) {
+        const uint32_t i = r0 + threadIdx.x + k * MG_THREADS;
+        bk[k] = MG_NONE;
+        key[k] = MG_EMPTY;
+        rk[k] = 0u;
+        if (i < r1) {
+            // (the key and validity only: the weight's inputs do not enter them)
+            const MgPoint p = mg_point(R, px[k], py[k], pz[k], s.ox, s.oy, s.oz, 0.0f, 0.0f, 0.0f,
+                                       false);
+            if (p.ok) {
+                key[k] = p.key;
+                bk[k] = mg_bucket(p.key, P);
+                rk[k] = atomicAdd(&hist[bk[k]], 1u);
+            }
+        }
+    }
+    __syncthreads();
+    // the block's run in each of its buckets: its first entry replaces the count
+    const uint32_t base = mg_bucket_base(s.off, t);
+    for (uint32_t j = threadIdx.x; j < P; j += MG_THREADS) {
+        const uint32_t c = hist[j];
+        if (c) hist[j] = M.bst[base + j] + atomicAdd(&M.bcnt[base + j], c);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < MG_PPT; k++) {
+        if (bk[k] == MG_NONE) continue;
+        const uint32_t e = hist[bk[k]] + rk[k];
+        M.ekey[e] = key[k];
+        M.eidx[e] = r0 + threadIdx.x + k * MG_THREADS;
+    }
+}
+
+constexpr int MG_GTHREADS = 512;  // k_mg_group: lanes per bucket
+constexpr int MG_EPT = 3;         // k_mg_group: entries per lane kept in registers
+__global__ __launch_bounds__(MG_GTHREADS) void k_mg_group(const float* __restrict__ xyz, BatchRef D,
+                                                          RayConst R, MgBufs M, uint32_t* ovf) {
+    __shared__ uint64_t tkey[MG_TAB];  // the bucket's keys (open addressing)
+    __shared__ uint8_t tdup[MG_TAB];   // the key was seen more than once
+    __shared__ uint64_t gm[MG_GM];     // the multi-point bundles' members: slot << 32 | point
+    __shared__ uint32_t n_gm;
+    const uint32_t b = blockIdx.x, tid = threadIdx.x;
+    const uint32_t e0 = M.bst[b], e1 = M.bst[b + 1];
+    if (e0 == e1) return;
+    if (tid == 0) {
+        M.bcnt[b] = 0u;  // the cursor: zero for the next batch
+        n_gm = 0u;
+    }
+    // the bucket's scan: the last t with base(t) <= b (base strictly increases with t)
+    uint32_t lo = 0, hi = D.n_scans;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (mg_bucket_base(D.s[mid].off, mid) <= b) lo = mid;
+        else hi = mid;
+    }
+    const ScanRec s = D.s[lo];
     const bool axis = s.zx != 0.0f || s.zy != 0.0f || s.zz != 0.0f;
     const float* __restrict__ xs = xyz + 3 * (size_t)s.xoff;
-    for (uint32_t i = r0 + threadIdx.x; i < r1; i += MG_THREADS) {
-        const uint32_t h = M.slot[i];
-        uint32_t g = MG_NONE;
-        bool single = false;
-        if (h != MG_NONE) single = ((M.tab[3 * (size_t)h + 2] >> (t & 63u)) & 1ull) == 0ull;
-        if (single) {  // a one-point bundle: its ray now
-            const MgPoint p = mg_point(R, xs[3 * (size_t)i], xs[3 * (size_t)i + 1],
-                                       xs[3 * (size_t)i + 2], s.ox, s.oy, s.oz, s.zx, s.zy, s.zz,
-                                       axis);
-            float mx = 0.0f, my = 0.0f, mz = 0.0f, mw = 0.0f;
-            mg_step(p, p.clearing, mx, my, mz, mw);
-            mg_out(M, i, s, p.clearing, mx, my, mz, mw);
-        } else {
-            mg_out(M, i, s, false, 0.0f, 0.0f, 0.0f, 0.0f);  // no ray here (a group's leader's later)
-            if (h != MG_NONE) {  // join the (slot, scan) group
-                const uint64_t key = ((uint64_t)h << 16) | (uint64_t)(t + 1u);  // never 0
-                uint32_t q = mg_home(key, M.grp_n);
-                for (uint32_t n = 0; n < M.grp_n; n++, q = mg_next(q, M.grp_n)) {
-                    const uint64_t k = M.grp[4 * (size_t)q];
-                    if (k == key) {
-                        g = q;
-                        break;
-                    }
-                    if (k == MG_EMPTY) {
-                        const unsigned long long old = atomicCAS((unsigned long long*)&M.grp[4 * (size_t)q],
-                                                                 (unsigned long long)MG_EMPTY,
-                                                                 (unsigned long long)key);
-                        if (old == MG_EMPTY || old == key) {
-                            g = q;
-                            break;
+    // the first MG_EPT x MG_GTHREADS entries stay in registers (nearly every bucket: ~1024)
+    uint64_t ek[MG_EPT];
+    uint32_t ei[MG_EPT], eq[MG_EPT];
+#pragma unroll
+    for (int k = 0; k < MG_EPT; k++) {
+        const uint32_t e = min(e0 + tid + k * MG_GTHREADS, e1 - 1u);
+        ek[k] = M.ekey[e];
+        ei[k] = M.eidx[e];
+    }
+    for (uint32_t j = tid; j < MG_TAB; j += MG_GTHREADS) {
+        tkey[j] = MG_EMPTY;
+        tdup[j] = 0;
+    }
+    __syncthreads();
+    // the key's slot; insert: a key already present (or inserted meanwhile) is marked as seen twice
+    auto find = [&](uint64_t key, bool insert) {
+        uint32_t q = (uint32_t)mix64(key) & (MG_TAB - 1u);
+        for (uint32_t n = 0; n < MG_TAB; n++, q = (q + 1u) & (MG_TAB - 1u)) {
+            uint64_t k = tkey[q];
+            if (k == MG_EMPTY && insert)
+                k = atomicCAS((unsigned long long*)&tkey[q], (unsigned long long)MG_EMPTY,
+                              (unsigned long long)key);
+            if (k == key) {
+                if (insert) tdup[q] = 1;
+                return q;
+            }
+            if (k == MG_EMPTY) {
+                if (!insert) return MG_NONE;
+                return q;  // this lane inserted it
+            }
+        }
+        return MG_NONE;
+    };
+    const uint32_t e_reg = e0 + MG_EPT * MG_GTHREADS;  // entries from here on are re-read
+#pragma unroll
+    for (int k = 0; k < MG_EPT; k++) {
+        eq[k] = MG_NONE;
+        if (e0 + tid + k * MG_GTHREADS < e1) {
+            eq[k] = find(ek[k], true);
+            if (eq[k] == MG_NONE) atomicOr(ovf, OVF_MG);  // more distinct keys than MG_TAB
+        }
+    }
+    for (uint32_t e = e_reg + tid; e < e1; e += MG_GTHREADS)
+        if (find(M.ekey[e], true) == MG_NONE) atomicOr(ovf, OVF_MG);
+    __syncthreads();
+    auto add_member = [&](uint32_t q, uint32_t i) {
+        if (q != MG_NONE && tdup[q]) {
+            const uint32_t g = atomicAdd(&n_gm, 1u);
+            if (g < MG_GM) gm[g] = ((uint64_t)q << 32) | i;
+        }
+    };
+#pragma unroll
+    for (int k = 0; k < MG_EPT; k++) add_member(eq[k], ei[k]);
+    for (uint32_t e = e_reg + tid; e < e1; e += MG_GTHREADS) add_member(find(M.ekey[e], false), M.eidx[e]);
+    __syncthreads();
+    const uint32_t ng = n_gm;
+    if (ng == 0) return;
+    float mx, my, mz, mw;
+    bool clearing;
+    auto merge_at = [&](float px, float py, float pz) {
+        const MgPoint p = mg_point(R, px, py, pz, s.ox, s.oy, s.oz, s.zx, s.zy, s.zz, axis);
+        clearing = p.clearing;  // (the key carries it: the same for every member)
+        mg_step(p, clearing, mx, my, mz, mw);
+    };
+    if (ng <= MG_GM) {
+        // sort (slot, point): a bundle's members together, in cloud order
+        if (ng <= (uint32_t)MG_GTHREADS) {
+            // one member per lane: its rank among the (distinct) members is its place
+            const uint64_t v = tid < ng ? gm[tid] : 0ull;
+            uint32_t rank = 0;
+            if (tid < ng)
+                for (uint32_t g = 0; g < ng; g++) rank += gm[g] < v ? 1u : 0u;
+            __syncthreads();
+            if (tid < ng) gm[rank] = v;
+            __syncthreads();
+        } else {  // bitonic
+            uint32_t N = 2;
+            while (N < ng) N <<= 1;
+            for (uint32_t j = ng + tid; j < N; j += MG_GTHREADS) gm[j] = ~0ull;
+            __syncthreads();
+            for (uint32_t k = 2; k <= N; k <<= 1)
+                for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                    for (uint32_t x = tid; x < N; x += MG_GTHREADS) {
+                        const uint32_t y = x ^ j;
+                        if (y > x) {
+                            const uint64_t u = gm[x], v = gm[y];
+                            if ((u > v) == ((x & k) == 0u)) {
+                                gm[x] = v;
+                                gm[y] = u;
+                            }
                         }
                     }
+                    __syncthreads();
                 }
-                if (g == MG_NONE) {
-                    atomicOr(ovf, OVF_MG);
-                } else {
-                    uint32_t* v = reinterpret_cast<uint32_t*>(&M.grp[4 * (size_t)g + 1]);
-                    atomicMax(&v[0], ~i);                 // the first member (~index; 0: none)
-                    atomicAdd(&v[1], 1u);                 // the members
-                    atomicMax(&v[2], i);                  // the last member
-                    M.next[i] = atomicExch(&v[3], i + 1u);  // the chain (index + 1; 0 ends it)
-                }
-            }
         }
-        M.gid[i] = g;
-    }
-}
-
-__global__ __launch_bounds__(MG_THREADS) void k_mg_lead(const float* __restrict__ xyz, BatchRef D,
-                                                        RayConst R, MgBufs M) {
-    uint32_t t, r0, r1;
-    block_range(D, blockIdx.x, t, r0, r1);
-    const ScanRec s = D.s[t];
-    const uint32_t hi = D.s[t + 1].off;  // scan t's points end here
-    const bool axis = s.zx != 0.0f || s.zy != 0.0f || s.zz != 0.0f;
-    const float* __restrict__ xs = xyz + 3 * (size_t)s.xoff;
-    for (uint32_t i = r0 + threadIdx.x; i < r1; i += MG_THREADS) {
-        const uint32_t g = M.gid[i];
-        if (g == MG_NONE) continue;
-        const uint64_t v = M.grp[4 * (size_t)g + 1];
-        if (~(uint32_t)v != i) continue;  // not the group's first point (or already freed: 0)
-        const uint32_t h = M.slot[i];
-        const uint32_t cnt = (uint32_t)(v >> 32);
-        const uint64_t v2 = M.grp[4 * (size_t)g + 2];
-        const uint32_t last = (uint32_t)v2, head = (uint32_t)(v2 >> 32);
-        // the group record is read by its members only for this test: the leader frees it now (a
-        // member reading the zeros afterwards sees ~0 != its index, i.e. not the leader, as before)
-        *reinterpret_cast<ulonglong2*>(&M.grp[4 * (size_t)g]) = make_ulonglong2(0ull, 0ull);
-        M.grp[4 * (size_t)g + 2] = 0ull;
-        // the members are the points of scan t in slot h, in cloud order from this one on
-        float mx = 0.0f, my = 0.0f, mz = 0.0f, mw = 0.0f;
-        bool clearing = false;
-        auto merge_at = [&](uint32_t j) {
-            const MgPoint p = mg_point(R, xs[3 * (size_t)j], xs[3 * (size_t)j + 1],
-                                       xs[3 * (size_t)j + 2], s.ox, s.oy, s.oz, s.zx, s.zy, s.zz,
-                                       axis);
-            clearing = p.clearing;  // (the slot's key carries it: the same for every member)
-            mg_step(p, clearing, mx, my, mz, mw);
-        };
-        if (cnt <= MG_SMALL) {
-            // a small group (nearly all of them: two or three points): its chain, loaded once into
-            // registers (a static index per slot: no scratch), sorted by a compare-exchange
-            // network, merged in cloud order; cnt dependent loads, wherever the members lie (a
-            // voxel on the seam of the spin has members at both ends of the cloud)
-            uint32_t m[MG_SMALL];
-            uint32_t e = head;
-#pragma unroll
-            for (int q = 0; q < MG_SMALL; q++) {
-                const bool on = e != 0u;
-                m[q] = on ? e - 1u : ~0u;
-                e = on ? M.next[e - 1u] : 0u;
+        for (uint32_t g = tid; g < ng; g += MG_GTHREADS) {
+            const uint64_t cur = gm[g];
+            const uint32_t i = (uint32_t)cur, q0 = (uint32_t)(cur >> 32);
+            if (g > 0 && (uint32_t)(gm[g - 1] >> 32) == q0) {  // a later member: no ray here
+                mg_out(M, i, s, false, 0.0f, 0.0f, 0.0f, 0.0f);
+                continue;
             }
-#pragma unroll
-            for (int a = 0; a < MG_SMALL; a++)  // odd-even transposition sort (MG_SMALL rounds)
-#pragma unroll
-                for (int q = a & 1; q + 1 < MG_SMALL; q += 2) {
-                    const uint32_t lo_ = min(m[q], m[q + 1]), hi_ = max(m[q], m[q + 1]);
-                    m[q] = lo_;
-                    m[q + 1] = hi_;
-                }
-#pragma unroll
-            for (int q = 0; q < MG_SMALL; q++)
-                if (m[q] != ~0u) merge_at(m[q]);
-        } else {
-            // a large group (a near-range blob): forward over the scan's slots from the first
-            // member to the last, four slots per 16-B load
-            uint32_t found = 0;
-            const uint32_t end = min(last + 1u, hi);
-            for (uint32_t j0 = i & ~3u; j0 < end && found < cnt; j0 += 4u) {
-                const uint4 q4 = *reinterpret_cast<const uint4*>(M.slot + j0);
-                const uint32_t sl[4] = {q4.x, q4.y, q4.z, q4.w};
+            // the first member merges the bundle, four members' points in flight at a time
+            mx = my = mz = mw = 0.0f;
+            clearing = false;
+            for (uint32_t q = g; q < ng;) {
+                float px[4], py[4], pz[4];
+                uint32_t m = 0;
 #pragma unroll
                 for (int u = 0; u < 4; u++) {
-                    const uint32_t j = j0 + (uint32_t)u;
-                    if (j >= i && j < end && sl[u] == h) {
-                        merge_at(j);
-                        found++;
-                    }
+                    const uint64_t c = q + u < ng ? gm[q + u] : ~0ull;
+                    const bool on = m == (uint32_t)u && (uint32_t)(c >> 32) == q0;
+                    const uint32_t j = on ? (uint32_t)c : i;
+                    m += on ? 1u : 0u;
+                    px[u] = xs[3 * (size_t)j];
+                    py[u] = xs[3 * (size_t)j + 1];
+                    pz[u] = xs[3 * (size_t)j + 2];
                 }
+#pragma unroll
+                for (int u = 0; u < 4; u++)
+                    if ((uint32_t)u < m) merge_at(px[u], py[u], pz[u]);
+                if (m < 4u) break;
+                q += 4u;
+            }
+            mg_out(M, i, s, clearing, mx, my, mz, mw);
+        }
+    } else {
+        // too many members for the list: each bundle's first member walks the scan's points from
+        // itself to its last member (first / last per slot, in the list's space)
+        uint32_t* tfirst = reinterpret_cast<uint32_t*>(gm);
+        uint32_t* tlast = tfirst + MG_TAB;
+        static_assert(2 * MG_TAB * sizeof(uint32_t) <= MG_GM * sizeof(uint64_t), "first / last fit");
+        for (uint32_t j = tid; j < MG_TAB; j += MG_GTHREADS) {
+            tfirst[j] = MG_NONE;
+            tlast[j] = 0u;
+        }
+        __syncthreads();
+        for (uint32_t e = e0 + tid; e < e1; e += MG_GTHREADS) {
+            const uint32_t q = find(M.ekey[e], false);
+            if (q != MG_NONE && tdup[q]) {
+                atomicMin(&tfirst[q], M.eidx[e]);
+                atomicMax(&tlast[q], M.eidx[e]);
             }
         }
-        mg_out(M, i, s, clearing, mx, my, mz, mw);
+        __syncthreads();
+        for (uint32_t q = tid; q < MG_TAB; q += MG_GTHREADS) {
+            if (!tdup[q]) continue;
+            const uint64_t key = tkey[q];
+            const uint32_t i = tfirst[q], last = tlast[q];
+            mx = my = mz = mw = 0.0f;
+            clearing = false;
+            for (uint32_t j0 = i; j0 <= last; j0 += 4u) {  // four points in flight at a time
+                float px[4], py[4], pz[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const uint32_t j = min(j0 + u, last);
+                    px[u] = xs[3 * (size_t)j];
+                    py[u] = xs[3 * (size_t)j + 1];
+                    pz[u] = xs[3 * (size_t)j + 2];
+                }
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const uint32_t j = j0 + u;
+                    if (j > last) break;
+                    const MgPoint p = mg_point(R, px[u], py[u], pz[u], s.ox, s.oy, s.oz, s.zx,
+                                               s.zy, s.zz, axis);
+                    if (!p.ok || p.key != key) continue;
+                    clearing = p.clearing;
+                    mg_step(p, clearing, mx, my, mz, mw);
+                    if (j != i) mg_out(M, j, s, false, 0.0f, 0.0f, 0.0f, 0.0f);
+                }
+            }
+            mg_out(M, i, s, clearing, mx, my, mz, mw);
+        }
     }
-}
-
-// Empties the key table for the next batch: one grid-stride streaming fill of 16-B stores (the
-// table is 24 B x a multiple of 64 records)
-__global__ __launch_bounds__(256) void k_mg_clear(uint4* __restrict__ p, uint64_t n16) {
-    for (uint64_t q = blockIdx.x * 256ull + threadIdx.x; q < n16; q += (uint64_t)gridDim.x * 256ull)
-        p[q] = make_uint4(0u, 0u, 0u, 0u);
 }
 
 }  // namespace
 
-uint32_t mg_table_records(uint64_t n_points) {
-    // >= 1.25 x the batch's points, a multiple of 64 records (k_mg_clear's 16-B stores)
-    const uint64_t n = (n_points + n_points / 4 + 127) & ~63ull;
-    return (uint32_t)std::min<uint64_t>(n, 0xFFFFFFC0ull);
+uint32_t mg_buckets_max(uint64_t n_points) {
+    return (uint32_t)std::min<uint64_t>((n_points >> MG_BSHIFT) + MAX_BATCH + 1, 0xFFFFFFF0ull);
 }
 
 hipError_t launch_mg_prepass(const float* d_xyz, const BatchRef& B, uint32_t n_blocks,
                              uint64_t n_points, const RayConst& R, MgBufs& M, uint32_t* ovf,
                              hipStream_t st) {
     if (!n_points) return hipSuccess;
-    if (n_points > M.cap) return hipErrorInvalidValue;
-    k_mg_keys<<<n_blocks, MG_THREADS, 0, st>>>(d_xyz, B, R, M, ovf);
-    k_mg_single<<<n_blocks, MG_THREADS, 0, st>>>(d_xyz, B, R, M, ovf);
-    k_mg_lead<<<n_blocks, MG_THREADS, 0, st>>>(d_xyz, B, R, M);
-    // the key table's last readers ran (k_mg_single): empty it for the next batch in one streaming
-    // fill (24 B a record; clearing each point's record from k_mg_lead cost 0.4 ms of scattered
-    // partial-line stores per 64-scan batch)
-    const uint64_t n16 = (uint64_t)24 * M.tab_n / 16;
-    k_mg_clear<<<(uint32_t)std::min<uint64_t>((n16 + 255) / 256, 8192), 256, 0, st>>>(
-        reinterpret_cast<uint4*>(M.tab), n16);
+    const uint64_t nb = (n_points >> MG_BSHIFT) + B.n_scans;
+    if (n_points > M.cap || nb > M.nb_cap) return hipErrorInvalidValue;
+    k_mg_count<<<n_blocks, MG_THREADS, 0, st>>>(d_xyz, B, R, M);
+    k_mg_scan<<<1, MG_SCAN_THREADS, 0, st>>>(M, (uint32_t)nb);
+    k_mg_scatter<<<n_blocks, MG_THREADS, 0, st>>>(d_xyz, B, R, M);
+    k_mg_group<<<(uint32_t)nb, MG_GTHREADS, 0, st>>>(d_xyz, B, R, M, ovf);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
-        // a pre-pass cut short may leave groups in the group table: empty it too, so the next batch
-        // starts from empty tables
-        (void)hipMemsetAsync(M.grp, 0, (size_t)32 * M.grp_n, st);
+        // a pre-pass cut short may leave bucket counters set: zero them, so the next batch starts
+        // from zero counters
+        (void)hipMemsetAsync(M.bcnt, 0, (size_t)4 * M.nb_cap, st);
     }
     return e;
 }

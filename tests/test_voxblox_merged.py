@@ -131,7 +131,7 @@ def test_method_validation():
         ora(method="fast")
 
 
-# -- GPU: the pre-pass (k_mg_keys, radix sort, k_mg_merge) + the walk, bit for bit ----------------
+# -- GPU: the pre-pass (k_mg_count, k_mg_scan, k_mg_scatter, k_mg_group) + the walk, bit for bit --
 
 def assert_bitwise(g, o):
     gi, gs, gw = g.export_voxels()
@@ -191,16 +191,18 @@ def test_gpu_merged_full_scans_device_batches(sim):
 
 
 @pytest.mark.gpu
-def test_gpu_merged_single_voxel_blob_bounded(sim):
-    """A degenerate cloud: half of a full scan's points collapsed into ONE voxel 0.4 m from the
-    sensor (self-returns / a near-range blob).  k_mg_merge walks a bundle on one lane (the running
-    weighted mean is sequential, bit for bit upstream's integrateVoxel), so this is the longest
-    bundle a scan can hold; the field stays bit-exact and the scan's integration stays bounded
-    (measured against the same scan without the blob)."""
+@pytest.mark.parametrize("frac", [0.5, 0.012], ids=["half-scan", "1500-points"])
+def test_gpu_merged_single_voxel_blob_bounded(sim, frac):
+    """A degenerate cloud: part of a full scan's points collapsed into ONE voxel 0.4 m from the
+    sensor (self-returns / a near-range blob).  The bundle's running weighted mean is sequential
+    (bit for bit upstream's integrateVoxel), so it runs on one lane: half a scan is more members
+    than k_mg_group's LDS list holds (its bucket takes the forward walk), 1500 points fit it (the
+    sorted-list path with one long bundle).  The field stays bit-exact and the scan's integration
+    stays bounded (measured against the same scan without the blob)."""
     import time
     p, org = sim.scan(3)
     rng = np.random.default_rng(7)
-    n = p.shape[0] // 2
+    n = int(p.shape[0] * frac)
     centre = np.floor((org + np.array([0.4, 0.1, -0.05])) / VS) * VS + VS / 2
     blob = p.copy()
     blob[:n] = (centre + rng.uniform(-0.45 * VS, 0.45 * VS, (n, 3))).astype(F)
