@@ -49,11 +49,12 @@ typedef unsigned long long MaskT;  // a voxel's scans in the window, one bit per
 typedef uint32_t MaskT;
 #define MASK_POPC(m) __popc(m)
 #endif
-// LDS position of brick voxel l = (z * 8 + y) * 8 + x in k_integrate's per-voxel arrays: each z
-// layer is skewed by one element, so voxels of one (x, y) column (64 elements apart: one bank) that
-// the rays of neighbouring beams hit in the same wave fall in different banks
+// LDS position of brick voxel l = (z * 8 + y) * 8 + x in k_integrate's per-voxel arrays.  A/B knob
+// (round 6): TSDF_INT_SKEW=1 skews each z layer by one element, so voxels of one (x, y) column (64
+// elements apart: one bank) fall in different banks -- measured slower (k_integrate 0.399 vs 0.377
+// ms headline, 1.18 vs 1.07 ms C4: the index arithmetic costs more than the conflicts it removes)
 #ifndef TSDF_INT_SKEW
-#define TSDF_INT_SKEW 1
+#define TSDF_INT_SKEW 0
 #endif
 #define VOXL(l) ((l) + TSDF_INT_SKEW * ((l) >> 6))
 constexpr int BRICK_VOX_LDS = BRICK_VOX + TSDF_INT_SKEW * (BRICK_VOX / 64);
