@@ -96,7 +96,7 @@ def parse():
                          "every ray walked once (k_walk + k_spans) when the band allows it")
     ap.add_argument("--no-profile", action="store_true",
                     help="do not record per-kernel HIP events in the timed region")
-    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_r05.json"),
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_r06.json"),
                     help="PMC-measured HBM bytes per launch (from a separate rocprofv3 --pmc run)")
     return ap.parse_args()
 
