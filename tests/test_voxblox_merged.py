@@ -191,6 +191,38 @@ def test_gpu_merged_full_scans_device_batches(sim):
 
 
 @pytest.mark.gpu
+def test_gpu_merged_many_small_scans_one_batch(sim):
+    """300 small scans as ONE device batch (the pre-pass's bucket bases off(t) / 1024 + t over
+    hundreds of scans, scans of one bucket): decimated scans with a few jittered copies of their
+    points (multi-point bundles in every scan), empty scans and one-point scans between them."""
+    import torch
+    rng = np.random.default_rng(11)
+    scans = []
+    for k in range(300):
+        if k % 37 == 5:
+            scans.append((np.zeros((0, 3), F), sim.scan(k % 40)[1]))
+            continue
+        p, org = sim.scan(k % 40)
+        if k % 53 == 7:
+            scans.append((p[rng.integers(0, p.shape[0], 1)], org))
+            continue
+        q = p[rng.integers(0, p.shape[0], 600)]
+        dup = q[:40] + rng.uniform(-0.004, 0.004, (40, 3)).astype(F)
+        scans.append((np.concatenate([q, dup]).astype(F), org))
+    x = torch.from_numpy(np.concatenate([p for p, _ in scans])).cuda()
+    offs = np.cumsum([0] + [p.shape[0] for p, _ in scans])
+    g = hip(method="merged", max_batch=300, use_const_weight=False)
+    g.integrate_batch_device(x.data_ptr(), offs, np.stack([o for _, o in scans]))
+    o = ora(method="merged", use_const_weight=False)
+    for p, q in scans:
+        o.integrate(p, q)
+    g.sync()
+    assert assert_bitwise(g, o) > 10000
+    assert g.stats()["n_rays_total"] == o.stats()["n_rays_total"]
+    assert o.stats()["n_rays_total"] < offs[-1]  # bundles formed
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("frac", [0.5, 0.012], ids=["half-scan", "1500-points"])
 def test_gpu_merged_single_voxel_blob_bounded(sim, frac):
     """A degenerate cloud: part of a full scan's points collapsed into ONE voxel 0.4 m from the
