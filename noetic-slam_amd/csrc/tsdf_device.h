@@ -98,8 +98,9 @@ constexpr uint32_t OVF_TABLE = 1u, OVF_POOL = 2u, OVF_PAIRS = 4u, OVF_ACTIVE = 8
                    OVF_SMP = 32u,  // the batch's samples exceed the sample list (single walk:
                                    // the workgroup regions)
                    OVF_SPN = 64u,  // single walk: the batch's spans exceed the span list
-                   OVF_MG = 128u;  // merged pre-pass: a key / group table probe found no slot
-                                   // (cannot happen at its 1.25x sizing; not a growable capacity)
+                   OVF_MG = 128u;  // merged pre-pass: a bucket holds more distinct bundle keys
+                                   // than k_mg_group's LDS table (a scan of more than ~2^22
+                                   // points; not a growable capacity)
 // a border tile whose brick this context lacks (tsdf_border_merge_device; sticky like OVF_*)
 constexpr uint32_t ERR_MERGE_KEY = 1u << 8;
 
