@@ -47,6 +47,7 @@
 #include <std_srvs/Trigger.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <memory>
@@ -271,8 +272,8 @@ class TsdfMapNode {
     // One map: every context's bricks, each observed brick once.  With several GPUs the border
     // reduce runs first (retried once); if it still fails, the contexts are unchanged (the reduce
     // is a transaction) and their border bricks are merged here instead, in context order, by
-    // the reduce's rule: S = (S_a W_a + S_b W_b) / (W_a + W_b), W = W_a + W_b (a voxel unobserved
-    // on one side is copied from the other).  Returns false when nothing could be read out.
+    // the reduce's rule: S = (S_a W_a + S_b W_b) / (W_a + W_b), W = W_a + W_b, capped at max_weight
+    // under Voxblox semantics (a voxel unobserved on one side is copied from the other).  Returns false when nothing could be read out.
     bool collect(std::vector<int32_t>& c, std::vector<float>& s, std::vector<float>& w,
                  bool& reduced) {
         const uint32_t n = (uint32_t)ctxs_.size();
@@ -293,6 +294,8 @@ class TsdfMapNode {
             }
         }
         std::unordered_map<uint64_t, uint64_t> at;  // brick key -> row (host merge only)
+        // the reduce's weight cap: Voxblox's max_weight, none otherwise (tsdf_border_merge_device)
+        const float w_cap = params_.semantics == TSDF_SEM_VOXBLOX ? params_.max_weight : INFINITY;
         for (tsdf_ctx* k : ctxs_) {
             uint64_t nb = 0, got = 0;
             if (tsdf_num_bricks(k, &nb) != TSDF_OK) return false;
@@ -322,7 +325,7 @@ class TsdfMapNode {
                             }
                             const float wt = wo[l] + wb[l];
                             so[l] = (so[l] * wo[l] + sb[l] * wb[l]) / wt;
-                            wo[l] = wt;
+                            wo[l] = wt > w_cap ? w_cap : wt;
                         }
                         continue;
                     }

@@ -278,3 +278,36 @@ def test_node_shutdown_save_after_failed_reduce(tmp_path, sim, node_exe):
     assert r.returncode == 0, r.stderr
     assert "host-merged" in r.stderr
     _check_map(out, want, 2)
+
+
+def test_node_failed_reduce_voxblox_weight_cap(tmp_path, sim, node_exe):
+    """The host merge after a failed reduce follows the reduce's own rule, Voxblox's max_weight cap
+    included: two Voxblox (Merged, 1/z^2) sector contexts with max_weight = 2, the reduce failing
+    twice -- the node's host-merged map equals the oracle's sector fields after a reduce that ran,
+    bit for bit (rank 0's bricks first, then rank 1's merged into them, W capped at 2)."""
+    from test_multigpu import emulated_reduce_host
+    recs, want = topic_stream(sim, tilt=0.5)
+    write_topics(tmp_path / "in.topics", recs)
+    out = tmp_path / "map.bricks"
+    env = dict(os.environ, TSDF_STUB_STREAM=str(tmp_path / "in.topics"), TSDF_ORACLE_REDUCE_FAIL="2",
+               TSDF_STUB_PARAMS="map_path=%s;min_range=0;num_gpus=2;save_every_n_clouds=0;"
+                                "semantics=voxblox;max_ray_length_m=1000;max_weight=2" % out)
+    r = subprocess.run([node_exe], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert "host-merged" in r.stderr
+    coords, s, w = read_bricks(out)
+    assert len({tuple(x) for x in coords.tolist()}) == coords.shape[0]  # each brick once
+    got = bricks_to_voxels(coords, s, w)
+    vols = sector_volumes(2, 0.0, semantics="voxblox", max_range=1000.0, use_const_weight=False,
+                          method="merged", max_weight=2.0)
+    feed(vols, want)
+    emulated_reduce_host(vols)
+    ref = [v.export_bricks() for v in vols]
+    keep = [(wk.reshape(len(ck), -1) > 0).any(1) for ck, _, wk in ref]
+    want_vox = bricks_to_voxels(np.concatenate([ck[k] for (ck, _, _), k in zip(ref, keep)]),
+                                np.concatenate([sk[k] for (_, sk, _), k in zip(ref, keep)]),
+                                np.concatenate([wk[k] for (_, _, wk), k in zip(ref, keep)]))
+    assert got[0].shape[0] > 1000 and np.any(got[2] == 2.0)  # the cap binds somewhere
+    for a, b in zip(got, want_vox):
+        assert np.array_equal(a.view(np.uint32) if a.dtype == np.float32 else a,
+                              b.view(np.uint32) if b.dtype == np.float32 else b)
