@@ -1134,7 +1134,7 @@ void tsdf_destroy(tsdf_ctx* c) {
         if (c->stage_done[i]) (void)hipEventDestroy(c->stage_done[i]);
         MgBufs& M = c->mg[i];
         for (void* q : {(void*)M.xyz_out, (void*)M.w_out, (void*)M.ekey, (void*)M.eidx,
-                        (void*)M.bcnt, (void*)M.bst})
+                        (void*)M.bcnt, (void*)M.bst, (void*)M.bscan})
             if (q) (void)hipFree(q);
     }
     if (c->bc_ev) (void)hipEventDestroy(c->bc_ev);
@@ -1299,9 +1299,10 @@ static int create_impl(tsdf_ctx* c, const tsdf_params* p) {
             M.nb_cap = mg_buckets_max(n);
             HIPCHK(c, hipMalloc(&M.ekey, n * 8));
             HIPCHK(c, hipMalloc(&M.eidx, n * 4));
-            HIPCHK(c, hipMalloc(&M.bcnt, (size_t)4 * M.nb_cap));
-            HIPCHK(c, hipMemset(M.bcnt, 0, (size_t)4 * M.nb_cap));  // zero between batches
+            HIPCHK(c, hipMalloc(&M.bcnt, (size_t)4 * MG_REPLICAS * M.nb_cap));
+            HIPCHK(c, hipMemset(M.bcnt, 0, (size_t)4 * MG_REPLICAS * M.nb_cap));  // zero between batches
             HIPCHK(c, hipMalloc(&M.bst, (size_t)4 * (M.nb_cap + 1)));
+            HIPCHK(c, hipMalloc(&M.bscan, (size_t)4 * M.nb_cap));
             HIPCHK(c, hipMalloc(&M.xyz_out, n * 12));
             HIPCHK(c, hipMalloc(&M.w_out, n * 4));
         }

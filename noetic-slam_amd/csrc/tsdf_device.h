@@ -416,11 +416,13 @@ struct MgBufs {
     // buckets of ~1024 points): bucket b holds entries [bst[b], bst[b + 1])
     uint64_t* ekey = nullptr;
     uint32_t* eidx = nullptr;
-    uint32_t* bcnt = nullptr;  // per bucket: size, then cursor; zero between batches
+    uint32_t* bcnt = nullptr;  // per (replica, bucket): size, then cursor; zero between batches
     uint32_t* bst = nullptr;   // per bucket: first entry (nb_cap + 1)
+    uint32_t* bscan = nullptr; // per bucket: its scan (k_mg_scan)
     uint32_t nb_cap = 0;       // buckets
 };
 uint32_t mg_buckets_max(uint64_t n_points);
+constexpr uint32_t MG_REPLICAS = 8;  // bucket counter replicas (tsdf_merged.hip MG_REP)
 hipError_t launch_mg_prepass(const float* d_xyz, const BatchRef& B, uint32_t n_blocks,
                              uint64_t n_points, const RayConst& R, MgBufs& M, uint32_t* ovf,
                              hipStream_t st);

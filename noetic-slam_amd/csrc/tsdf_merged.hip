@@ -10,11 +10,11 @@
 //                 isPointValid, the bundle key (clearing bit | the point's voxel, 21 biased bits per
 //                 axis) and its bucket; the point's ray as a one-point bundle (the merge's arithmetic
 //                 for one point, bit for bit; no ray for a dropped one); bucket sizes through an LDS
-//                 histogram, one global add per (block, bucket)
+//                 histogram, one global add per (block, bucket) to one of MG_REP replica counters
 //   k_mg_scan     one workgroup: bucket starts (exclusive prefix); the sizes zeroed for use as
-//                 cursors
+//                 cursors; each bucket's scan
 //   k_mg_scatter  the same blocks again: (key, point) entries into their buckets (an LDS rank plus
-//                 one returning global add per (block, bucket) for the block's run)
+//                 one returning global add per (block, bucket) on its replica's cursor)
 //   k_mg_group    one workgroup per bucket: its keys into an LDS hash table (a key met again is
 //                 marked); the entries of keys seen more than once (the multi-point bundles' members) gathered in
 //                 LDS as (table slot, point) and sorted, so each bundle's members lie together in
@@ -46,6 +46,10 @@ constexpr uint32_t MG_PMAX = 4096;  // buckets per scan at most (the LDS histogr
 constexpr uint32_t MG_TAB = 2048;   // k_mg_group: distinct keys per bucket (LDS hash table)
 constexpr uint32_t MG_GM = 2048;    // k_mg_group: multi-point bundle members sorted in LDS
 constexpr int MG_PPT = RPB / MG_THREADS;  // points per lane in k_mg_scatter
+// bucket counters in MG_REP replicas (replica r = block index mod MG_REP, each replica's counters
+// contiguous): the ~100 blocks of a scan reserve their runs in the same buckets at the same time,
+// and one counter per bucket queued their returning atomics at the memory side
+constexpr uint32_t MG_REP = MG_REPLICAS;
 static_assert(RPB % MG_THREADS == 0, "k_mg_scatter keeps RPB / MG_THREADS points per lane");
 
 // scan t's bucket count and first bucket: base(t) = off(t) / 2^MG_BSHIFT + t, so that
@@ -162,19 +166,29 @@ __global__ __launch_bounds__(MG_THREADS) void k_mg_count(const float* __restrict
     __syncthreads();
     const uint32_t base = mg_bucket_base(s.off, t);
     for (uint32_t j = threadIdx.x; j < P; j += MG_THREADS)
-        if (hist[j]) atomicAdd(&M.bcnt[base + j], hist[j]);
+        if (hist[j]) atomicAdd(&M.bcnt[(blockIdx.x % MG_REP) * M.nb_cap + base + j], hist[j]);
 }
 
-// bucket starts: bst[b] = the sizes of the buckets before b, bst[nb] = the entries; the sizes are
-// zeroed (k_mg_scatter's cursors)
+// bucket starts: bst[b] = the sizes of the buckets before b, bst[nb] = the entries; each replica
+// counter becomes its runs' first entry (k_mg_scatter's cursor: bucket b's entries hold replica 0's
+// runs, then replica 1's, ...)
 constexpr int MG_SCAN_THREADS = 1024;
-__global__ __launch_bounds__(MG_SCAN_THREADS) void k_mg_scan(MgBufs M, uint32_t nb) {
+__global__ __launch_bounds__(MG_SCAN_THREADS) void k_mg_scan(BatchRef D, MgBufs M, uint32_t nb) {
     __shared__ uint32_t s_w[MG_SCAN_THREADS / 64];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+    // 1. bucket sizes over the replicas into bst (lanes on consecutive buckets: coalesced)
+    for (uint32_t j = tid; j < nb; j += MG_SCAN_THREADS) {
+        uint32_t c = 0;
+#pragma unroll
+        for (uint32_t r = 0; r < MG_REP; r++) c += M.bcnt[r * M.nb_cap + j];
+        M.bst[j] = c;
+    }
+    __syncthreads();
+    // 2. their exclusive prefix (a contiguous range of buckets per lane)
     const uint32_t per = (nb + MG_SCAN_THREADS - 1) / MG_SCAN_THREADS;
     const uint32_t j0 = min(nb, tid * per), j1 = min(nb, j0 + per);
     uint32_t sum = 0;
-    for (uint32_t j = j0; j < j1; j++) sum += M.bcnt[j];
+    for (uint32_t j = j0; j < j1; j++) sum += M.bst[j];
     const uint32_t incl = wave_incl_scan(sum);
     if (lane == 63u) s_w[wid] = incl;
     __syncthreads();
@@ -186,12 +200,28 @@ __global__ __launch_bounds__(MG_SCAN_THREADS) void k_mg_scan(MgBufs M, uint32_t 
     }
     uint32_t run = incl - sum + off;
     for (uint32_t j = j0; j < j1; j++) {
-        const uint32_t c = M.bcnt[j];
+        const uint32_t c = M.bst[j];
         M.bst[j] = run;
-        M.bcnt[j] = 0u;
         run += c;
     }
+    __syncthreads();
+    // 3. each replica's first entry (coalesced again)
+    for (uint32_t j = tid; j < nb; j += MG_SCAN_THREADS) {
+        uint32_t r0 = M.bst[j];
+#pragma unroll
+        for (uint32_t r = 0; r < MG_REP; r++) {
+            const uint32_t c = M.bcnt[r * M.nb_cap + j];
+            M.bcnt[r * M.nb_cap + j] = r0;
+            r0 += c;
+        }
+    }
     if (tid == 0) M.bst[nb] = tot;
+    // each bucket's scan, for k_mg_group (a table instead of its binary search over the scans:
+    // nine dependent scalar loads per workgroup)
+    for (uint32_t t = tid; t < D.n_scans; t += MG_SCAN_THREADS) {
+        const uint32_t b0 = mg_bucket_base(D.s[t].off, t), P = mg_buckets(D.s[t + 1].off - D.s[t].off);
+        for (uint32_t j = 0; j < P; j++) M.bscan[b0 + j] = t;
+    }
 }
 
 __global__ __launch_bounds__(MG_THREADS) void k_mg_scatter(const float* __restrict__ xyz, BatchRef D,
@@ -232,11 +262,12 @@ __global__ __launch_bounds__(MG_THREADS) void k_mg_scatter(const float* __restri
         }
     }
     __syncthreads();
-    // the block's run in each of its buckets: its first entry replaces the count
+    // the block's run in each of its buckets (its replica's cursor): its first entry replaces the
+    // count
     const uint32_t base = mg_bucket_base(s.off, t);
     for (uint32_t j = threadIdx.x; j < P; j += MG_THREADS) {
         const uint32_t c = hist[j];
-        if (c) hist[j] = M.bst[base + j] + atomicAdd(&M.bcnt[base + j], c);
+        if (c) hist[j] = atomicAdd(&M.bcnt[(blockIdx.x % MG_REP) * M.nb_cap + base + j], c);
     }
     __syncthreads();
 #pragma unroll
@@ -258,19 +289,10 @@ __global__ __launch_bounds__(MG_GTHREADS) void k_mg_group(const float* __restric
     __shared__ uint32_t n_gm;
     const uint32_t b = blockIdx.x, tid = threadIdx.x;
     const uint32_t e0 = M.bst[b], e1 = M.bst[b + 1];
+    if (tid < MG_REP) M.bcnt[tid * M.nb_cap + b] = 0u;  // the cursors: zero for the next batch
     if (e0 == e1) return;
-    if (tid == 0) {
-        M.bcnt[b] = 0u;  // the cursor: zero for the next batch
-        n_gm = 0u;
-    }
-    // the bucket's scan: the last t with base(t) <= b (base strictly increases with t)
-    uint32_t lo = 0, hi = D.n_scans;
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (mg_bucket_base(D.s[mid].off, mid) <= b) lo = mid;
-        else hi = mid;
-    }
-    const ScanRec s = D.s[lo];
+    if (tid == 0) n_gm = 0u;
+    const ScanRec s = D.s[M.bscan[b]];  // the bucket's scan (k_mg_scan's table)
     const bool axis = s.zx != 0.0f || s.zy != 0.0f || s.zz != 0.0f;
     const float* __restrict__ xs = xyz + 3 * (size_t)s.xoff;
     // the first MG_EPT x MG_GTHREADS entries stay in registers (nearly every bucket: ~1024)
@@ -463,14 +485,14 @@ hipError_t launch_mg_prepass(const float* d_xyz, const BatchRef& B, uint32_t n_b
     const uint64_t nb = (n_points >> MG_BSHIFT) + B.n_scans;
     if (n_points > M.cap || nb > M.nb_cap) return hipErrorInvalidValue;
     k_mg_count<<<n_blocks, MG_THREADS, 0, st>>>(d_xyz, B, R, M);
-    k_mg_scan<<<1, MG_SCAN_THREADS, 0, st>>>(M, (uint32_t)nb);
+    k_mg_scan<<<1, MG_SCAN_THREADS, 0, st>>>(B, M, (uint32_t)nb);
     k_mg_scatter<<<n_blocks, MG_THREADS, 0, st>>>(d_xyz, B, R, M);
     k_mg_group<<<(uint32_t)nb, MG_GTHREADS, 0, st>>>(d_xyz, B, R, M, ovf);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         // a pre-pass cut short may leave bucket counters set: zero them, so the next batch starts
         // from zero counters
-        (void)hipMemsetAsync(M.bcnt, 0, (size_t)4 * M.nb_cap, st);
+        (void)hipMemsetAsync(M.bcnt, 0, (size_t)4 * MG_REP * M.nb_cap, st);
     }
     return e;
 }
