@@ -845,8 +845,8 @@ static int check_and_replay(tsdf_ctx* c) {
             return TSDF_OK;
         }
         int rc = TSDF_ENOMEM;
-        // pair slots per ray are a geometric bound, and the merged tables' 1.25x sizing a proof,
-        // not capacities
+        // pair slots per ray are a geometric bound, and a merged bucket's distinct keys exceed its
+        // LDS table only for scans of more than ~2^22 points: not capacities to grow
         if (!(g.overflow & (OVF_PAIRS | OVF_MG))) {
             rc = TSDF_OK;
             if (g.overflow & (OVF_TABLE | OVF_POOL | OVF_ACTIVE))

@@ -187,8 +187,8 @@ __device__ __forceinline__ bool ray_step_sel(RayState& r) {
 // Voxblox ray model (TSDF_SEM_VOXBLOX; the bit-exact twin of oracle/tsdf_oracle.c walk_ray_vb,
 // which restates voxblox SimpleTsdfIntegrator / RayCaster / updateTsdfVoxel — DESIGN.md §2b)
 
-// Scan and ray range of k_count / k_place workgroup b, and of the merged pre-pass' k_mg_keys
-// (uniform: scalar loads of the descriptor).
+// Scan and ray range of k_count / k_place workgroup b, and of the merged pre-pass' k_mg_count /
+// k_mg_scatter (uniform: scalar loads of the descriptor).
 __device__ __forceinline__ void block_range(const BatchRef& D, uint32_t b, uint32_t& t,
                                             uint32_t& r0, uint32_t& r1) {
     uint32_t lo = 0, hi = D.n_scans;  // blk[lo] <= b < blk[hi]
