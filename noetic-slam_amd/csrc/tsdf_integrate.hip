@@ -53,6 +53,12 @@ typedef uint32_t MaskT;
 // (round 6): TSDF_INT_SKEW=1 skews each z layer by one element, so voxels of one (x, y) column (64
 // elements apart: one bank) fall in different banks -- measured slower (k_integrate 0.399 vs 0.377
 // ms headline, 1.18 vs 1.07 ms C4: the index arithmetic costs more than the conflicts it removes)
+// A/B knob (round 6): TSDF_INT_ZERO_IN_FUSE=1 zeroes the live cells in the fuse chains that
+// consumed them instead of in a pass before each window's accumulation -- measured slower
+// (k_integrate 0.385 vs 0.375 ms headline, 1.085 vs 1.065 ms C4: the stores lengthen the chains)
+#ifndef TSDF_INT_ZERO_IN_FUSE
+#define TSDF_INT_ZERO_IN_FUSE 0
+#endif
 #ifndef TSDF_INT_SKEW
 #define TSDF_INT_SKEW 0
 #endif
@@ -132,6 +138,13 @@ __global__ __launch_bounds__(INT_THREADS, TSDF_INT_WAVES) void k_integrate(Batch
     const bool commit = !(G->retry && (C->ovf || G->failed));
     sMask[VOXL(tid)] = 0;
     sMask[VOXL(tid + 256)] = 0;
+#if TSDF_INT_ZERO_IN_FUSE
+    // every cell starts at zero; each window's fuse chains zero the cells they consumed
+    for (uint32_t j = tid; j < CAP; j += INT_THREADS) {
+        cA[j] = 0ull;
+        cB[j] = 0;
+    }
+#endif
     uint32_t nvox = 0, ndirty = 0, par = 0;
 #ifdef TSDF_PHASE_TIMING
     unsigned long long ph[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, t_last = clock64();
@@ -360,11 +373,13 @@ __global__ __launch_bounds__(INT_THREADS, TSDF_INT_WAVES) void k_integrate(Batch
                     s_ncell = tot & 0xFFFFu;
                     nvox += tot & 0xFFFFu;  // (voxel, scan) updates of the window
                 }
+#if !TSDF_INT_ZERO_IN_FUSE
                 // the window's cells start at zero (the previous window's P4 is past a barrier)
                 for (uint32_t j = tid; j < (tot & 0xFFFFu); j += INT_THREADS) {
                     cA[j] = 0ull;
                     cB[j] = 0;
                 }
+#endif
             }
             __syncthreads();
             PHASE(4);
@@ -468,6 +483,14 @@ __global__ __launch_bounds__(INT_THREADS, TSDF_INT_WAVES) void k_integrate(Batch
                             a1 = na1;
                             b0 = nb0;
                             b1 = nb1;
+#if TSDF_INT_ZERO_IN_FUSE
+                            cA[cell + k] = 0ull;  // consumed (read two steps ago)
+                            cB[cell + k] = 0;
+                            if (more) {
+                                cA[cell + k + 1] = 0ull;
+                                cB[cell + k + 1] = 0;
+                            }
+#endif
                         }
                         sS[l] = s;
                         sW[l] = wt;
@@ -514,6 +537,14 @@ __global__ __launch_bounds__(INT_THREADS, TSDF_INT_WAVES) void k_integrate(Batch
                         }
                         va = make_float2(__uint_as_float((uint32_t)na), __uint_as_float((uint32_t)(na >> 32)));
                         vb = make_float2(__uint_as_float((uint32_t)nb), __uint_as_float((uint32_t)(nb >> 32)));
+#if TSDF_INT_ZERO_IN_FUSE
+                        cA[cell + k] = 0ull;  // consumed (cF aliases cA)
+                        cB[cell + k] = 0;
+                        if (k + 1 < rem) {
+                            cA[cell + k + 1] = 0ull;
+                            cB[cell + k + 1] = 0;
+                        }
+#endif
                     }
                     sS[l] = s;
                     sW[l] = wt;
