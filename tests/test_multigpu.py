@@ -468,3 +468,35 @@ def test_index_rule_device_batches_bitwise(sim, kw):
         assert g.stats()["n_points_in"] == o.stats()["n_points_in"]
         rays += g.stats()["n_points_in"]
     assert rays == int(offs[-1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kw", [dict(), dict(semantics="voxblox", method="merged", use_const_weight=False)])
+def test_index_rule_tiny_and_empty_shares(sim, kw):
+    """The index rule with scans of fewer points than sectors: a 2-point scan (one sector's share
+    empty), an empty scan and a 1-point scan between full-size ones, as one device batch over 3
+    sectors -- every context equals its oracle twin bit for bit and the shares partition the
+    points (empty shares give zero-length ranges, ScanRec.xoff skips them)."""
+    import torch
+    n = 3
+    full = [np.ascontiguousarray(sim.scan(k)[0][::5]) for k in (1, 4)]
+    orgs = [sim.scan(k)[1] for k in (1, 2, 3, 4, 5)]
+    pts = [full[0], full[0][100:102].copy(), np.zeros((0, 3), np.float32), full[1][7:8].copy(),
+           full[1]]
+    offs = np.cumsum([0] + [p.shape[0] for p in pts]).astype(np.uint64)
+    poses = np.stack([np.concatenate([o, [0.0, 0.0, np.sin(0.2 * k), np.cos(0.2 * k)]])
+                      for k, o in enumerate(orgs)])
+    d = torch.from_numpy(np.concatenate(pts)).to("cuda:0")
+    torch.cuda.synchronize()
+    got = 0
+    for r in range(n):
+        g = hip(n_sectors=n, sector=r, max_batch=8, **kw)
+        o = ora(n_sectors=n, sector=r, **kw)
+        g.integrate_batch_device(d.data_ptr(), offs, poses)
+        for p, q in zip(pts, poses):
+            o.integrate(p, q)
+        g.sync()
+        assert voxels_equal_bitwise(g.export_voxels(), o.export_voxels()), r
+        assert g.stats()["n_points_in"] == o.stats()["n_points_in"]
+        got += g.stats()["n_points_in"]
+    assert got == int(offs[-1])
