@@ -106,9 +106,12 @@ def test_c4_geometry_single_walk(sim):
     assert fields_equal(g, o)
 
 
-def test_batch_of_512_scans_single_walk(sim):
+@pytest.mark.parametrize("walk", ["single", "two"])
+def test_batch_of_512_scans_single_walk(sim, walk):
     """The sector-sharded multi-GPU step is one batch of up to 512 scans (k_integrate<MAXS=512>
-    and 513 cells per brick row, the totals cell after the last scan)."""
+    and 513 cells per brick row, the totals cell after the last scan; windows of up to 128 scans
+    with two-word masks: decimated scans leave a brick few samples per scan, so its windows reach
+    past 64 scans)."""
     import torch
     scans = [(decimate(p, 32), o) for p, o in (sim.scan(k) for k in range(300))]
     allp = np.concatenate([p for p, _ in scans])
@@ -116,12 +119,12 @@ def test_batch_of_512_scans_single_walk(sim):
     org = np.stack([o for _, o in scans])
     d = torch.from_numpy(allp).to("cuda:0")
     torch.cuda.synchronize()
-    g = hip(max_batch=512, walk="single")
+    g = hip(max_batch=512, walk=walk)
     g.set_profiling(True)
     g.integrate_batch_device(d.data_ptr(), offs, org)
     g.sync()
     st = g.stats()
-    assert st["n_batches"] == 1 and st["kernel_launches"]["walk"] == 1
+    assert st["n_batches"] == 1 and st["kernel_launches"]["walk" if walk == "single" else "count"] == 1
     o = ora()
     for p, q in scans:
         o.integrate(p, q)
